@@ -1,0 +1,159 @@
+/*
+ * s3hc_lz4.h — C ABI of the MI355X LZ4 frame engine (libs3hc_lz4.so).
+ *
+ * Drop-in boundary for the LZ4 codec path of aws-samples/sample-s3-hybrid-cache
+ * (crate s3-proxy 2.6.0). The reference path is Rust: CompressionHandler in
+ * src/compression.rs plus two places where src/disk_cache.rs drives lz4_flex directly.
+ * Every entry point below names the reference item (file:line) it replaces; the Rust
+ * binding a maintainer would add is in INTEGRATION.md.
+ *
+ * Conventions: plain pointers and sizes, caller-owned buffers, no exceptions across the
+ * boundary, int status (S3HC_*), and a thread-local message via s3hc_last_error().
+ * Errors follow the reference's contract: any decode failure is an error for the whole
+ * call (ProxyError::CompressionError / CacheError, src/error.rs:19-23) and the caller
+ * treats it as a cache miss.
+ *
+ * Every compute entry point runs on the GPU. There is no CPU codec in this library:
+ * without a usable HIP device s3hc_create() fails with S3HC_DEVICE.
+ */
+#ifndef S3HC_LZ4_H
+#define S3HC_LZ4_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define S3HC_OK 0
+#define S3HC_CORRUPT 1        /* bad magic/header/block/offset, truncated frame */
+#define S3HC_CHECKSUM 2       /* content or block xxh32 mismatch */
+#define S3HC_DST_TOO_SMALL 3  /* caller buffer too small */
+#define S3HC_UNSUPPORTED 4    /* dictionary id, legacy/skippable frame, ... */
+#define S3HC_DEVICE 5         /* HIP runtime error / no device */
+#define S3HC_INVALID_ARG 6
+
+/* Frame layout policies for s3hc_compress_frame. */
+#define S3HC_BLK_AUTO_LZ4FLEX 0  /* lz4_flex FrameEncoder BlockSize::Auto: one frame, BD by input size */
+#define S3HC_BLK_64K_PER_FRAME 1 /* one BD=0x40 frame per 64 KiB of input (GPU batch format) */
+
+typedef struct s3hc_ctx s3hc_ctx;
+typedef struct s3hc_stream s3hc_stream;
+typedef struct s3hc_plan s3hc_plan;
+
+/* ---- context -------------------------------------------------------------- */
+/* One context per device; internally locked, safe to share between threads (the
+ * reference calls the codec from many spawn_blocking threads, http_proxy.rs:11608). */
+int s3hc_create(s3hc_ctx** out, int device);
+void s3hc_destroy(s3hc_ctx* ctx);
+const char* s3hc_last_error(void);
+const char* s3hc_version(void);
+
+/* Largest framed size any s3hc_compress_* call can produce for n input bytes. */
+size_t s3hc_frame_bound(size_t n);
+
+/* ---- whole-buffer codec (host buffers) ------------------------------------ */
+/* Replaces compress_with_algorithm(data, Lz4) (compression.rs:530-591) and the
+ * FrameEncoder in flush_batch (disk_cache.rs:1826-1846): an LZ4 frame with independent
+ * blocks and an xxh32 content checksum. A block whose compressed form is not smaller than
+ * its input is written stored, as lz4_flex does. *was_compressed is 1 (the reference tags
+ * every such frame "compressed" even when blocks end up stored). */
+int s3hc_compress_frame(s3hc_ctx* ctx, const uint8_t* src, size_t n, int policy,
+                        uint8_t* dst, size_t cap, size_t* out_len, int* was_compressed);
+
+/* Replaces CompressionHandler::encode_store_mode_frame (compression.rs:326-368):
+ * byte-identical output (BD 0x70, stored blocks of <= 4 MiB, xxh32 content checksum). */
+int s3hc_store_mode_frame(s3hc_ctx* ctx, const uint8_t* src, size_t n,
+                          uint8_t* dst, size_t cap, size_t* out_len);
+
+/* Upper bound of the decoded size of concatenated frames (walks headers only, host). */
+int s3hc_decompressed_bound(const uint8_t* src, size_t n, size_t* bound);
+
+/* Replaces CompressionHandler::decompress_data (compression.rs:463-502): decode
+ * concatenated frames; a frame that yields no bytes ends the loop (Ok(0) => break). */
+int s3hc_decompress_frames(s3hc_ctx* ctx, const uint8_t* src, size_t n,
+                           uint8_t* dst, size_t cap, size_t* out_len);
+
+/* ---- streaming decoder (stream_range_data, disk_cache.rs:3850-3935) ------- */
+/* Feed compressed bytes in any pieces; read decoded bytes frame by frame.
+ * s3hc_stream_read returns 0 bytes when it needs more input; after
+ * s3hc_stream_finish it returns 0 bytes at end of stream. */
+int s3hc_stream_open(s3hc_ctx* ctx, s3hc_stream** out);
+int s3hc_stream_feed(s3hc_stream* s, const uint8_t* src, size_t n);
+int s3hc_stream_finish(s3hc_stream* s);
+int s3hc_stream_read(s3hc_stream* s, uint8_t* dst, size_t cap, size_t* n);
+uint64_t s3hc_stream_total(const s3hc_stream* s);
+void s3hc_stream_close(s3hc_stream* s);
+
+/* ---- device-resident batches (benchmark path, configs 2/3/5) -------------- */
+/* A batch of n independent items already in HBM. Item i = d_src[src_off[i] ..
+ * src_off[i]+len[i]). mode[i]: 0 = compress (lz4_flex Auto layout, as flush_batch),
+ * 1 = store-mode frame (as encode_store_mode_frame; the extension denylist path,
+ * compression.rs:252-308). Metadata arrays are host arrays; the plan is reusable. */
+int s3hc_plan_encode(s3hc_ctx* ctx, const uint64_t* src_off, const uint32_t* len,
+                     const uint8_t* mode, uint32_t n, s3hc_plan** out);
+/* Frames of item i land contiguously in d_dst at d_item_off[i], d_item_len[i] bytes
+ * (device arrays written by the call). *total (host) = framed bytes of the batch;
+ * dst_cap must be >= s3hc_plan_dst_bound(plan). stream = hipStream_t (NULL = ctx stream). */
+int s3hc_encode_dev(s3hc_ctx* ctx, s3hc_plan* plan, const uint8_t* d_src, uint8_t* d_dst,
+                    uint64_t dst_cap, uint64_t* d_item_off, uint32_t* d_item_len, void* stream);
+uint64_t s3hc_plan_dst_bound(const s3hc_plan* plan);
+
+/* Decode n frames in HBM: frame i = d_src[frame_off[i] .. +frame_len[i]) decodes to
+ * d_dst[dst_off[i] ..) with room dst_cap[i]. Per-frame decoded length and status
+ * (S3HC_*) are written to the device arrays d_out_len / d_status. Host metadata. */
+int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const uint32_t* frame_len,
+                     const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t n, s3hc_plan** out);
+int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* plan, const uint8_t* d_src, uint8_t* d_dst,
+                    uint32_t* d_out_len, int32_t* d_status, void* stream);
+void s3hc_plan_free(s3hc_plan* plan);
+
+/* Time of the last s3hc_*_dev call per kernel (ms, HIP events on the launch stream),
+ * for roofline accounting. name = "enc_parse", "enc_emit", "decode", "xxh32", ... */
+float s3hc_last_kernel_ms(const s3hc_ctx* ctx, const char* name);
+void s3hc_set_timing(s3hc_ctx* ctx, int enabled);
+
+/* ---- device memory plumbing (lets callers stage batches in HBM without a second HIP
+ * runtime in the process). kind: 1 H2D, 2 D2H, 3 D2D; s3hc_memcpy is host-synchronous. */
+int s3hc_dev_alloc(s3hc_ctx* ctx, size_t n, void** out);
+int s3hc_dev_free(s3hc_ctx* ctx, void* p);
+int s3hc_memcpy(s3hc_ctx* ctx, void* dst, const void* src, size_t n, int kind);
+int s3hc_memset(s3hc_ctx* ctx, void* dst, int value, size_t n);
+int s3hc_sync(s3hc_ctx* ctx);
+
+/* ---- CompressionHandler mirror (compression.rs:169-604) ------------------- */
+/* The host-side mirror of the reference's handler: same decision inputs, same six
+ * counters (CompressionStatsAtomic, compression.rs:88-140), shared between clones. */
+typedef struct s3hc_handler s3hc_handler;
+s3hc_handler* s3hc_handler_new(s3hc_ctx* ctx, size_t threshold, int enabled);          /* :192 */
+s3hc_handler* s3hc_handler_new_with_shared_stats(size_t threshold, int enabled,
+                                                 const s3hc_handler* source);          /* :227 */
+s3hc_handler* s3hc_handler_clone(const s3hc_handler* h);                               /* Clone */
+void s3hc_handler_free(s3hc_handler* h);
+int s3hc_handler_is_compression_enabled(const s3hc_handler* h);                         /* :520 */
+/* compress_with_metadata (:376-460). Writes data (cap from s3hc_frame_bound) and metadata. */
+int s3hc_handler_compress_with_metadata(s3hc_handler* h, const uint8_t* src, size_t n,
+                                        const char* path, int should_compress, uint8_t* dst,
+                                        size_t cap, size_t* out_len, int* algorithm,
+                                        int* was_compressed);
+/* compress_with_algorithm (:530-591); algorithm 0 = Lz4, 1 = None. */
+int s3hc_handler_compress_with_algorithm(s3hc_handler* h, const uint8_t* src, size_t n, int algorithm,
+                                         uint8_t* dst, size_t cap, size_t* out_len, int* was_compressed);
+/* decompress_data (:463-502) / decompress_with_algorithm (:594-604). On error the
+ * decompression_failures counter is incremented and the status returned. */
+int s3hc_handler_decompress_with_algorithm(s3hc_handler* h, const uint8_t* src, size_t n, int algorithm,
+                                           uint8_t* dst, size_t cap, size_t* out_len);
+/* get_stats (:506): out = {compressed, uncompressed, bytes_before, bytes_after,
+ * compression_failures, decompression_failures}; ratio = after/before (1.0 if before == 0). */
+void s3hc_handler_stats(const s3hc_handler* h, uint64_t out[6], float* ratio);
+/* record_batch_bytes / record_object (:105-120) for streaming writers. */
+void s3hc_handler_record_batch_bytes(s3hc_handler* h, uint64_t before, uint64_t after);
+void s3hc_handler_record_object(s3hc_handler* h, int compressed);
+/* is_denylisted_extension (:252-308). */
+int s3hc_is_denylisted_extension(const char* path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

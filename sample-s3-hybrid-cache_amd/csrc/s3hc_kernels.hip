@@ -1,0 +1,1121 @@
+// s3hc_kernels.hip — CDNA4 (gfx950) kernels of the LZ4 frame engine.
+//
+// Everything here is integer byte work on 64-lane waves; none of it is GEMM-shaped,
+// so there is no MFMA. The kernels are:
+//   k_xxh32_ranges   xxh32 (twox-hash XxHash32, compression.rs:35/364) of many byte ranges;
+//                    4 lanes per range, one per XXH32 accumulator chain.
+//   k_decode_units   LZ4 block decode (lz4_flex FrameDecoder semantics, compression.rs:479-480):
+//                    one wave per unit; wave-speculative token parsing over 64 candidate
+//                    positions, an LDS ring of recent output for match sources, coalesced
+//                    1 KiB flushes to HBM.
+//   k_enc_parse      LZ4 match finding: one wave per 4 KiB segment, per-wave LDS hash table,
+//                    64 positions probed per step, ballot picks the first match (greedy).
+//   k_enc_sizes      per block: merges segment carries, sizes the payload, picks stored vs
+//                    compressed exactly like lz4_flex write_block (comp_len < src_len).
+//   k_enc_emit       one wave per segment: writes frame header, block word, tokens,
+//                    literals, offsets, EndMark and content checksum (compression.rs:326-368
+//                    byte layout for stored blocks).
+//   k_dframe_*       device-side frame walk for device-resident batches.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "s3hc_plan.hpp"
+#include "s3hc_lz4.h"
+
+namespace s3hc {
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) {
+    return __builtin_amdgcn_alignbit(x, x, 32 - r);
+}
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)); }
+
+// Orders this wave's LDS traffic across lanes (lanes of one wave share an in-order LDS queue;
+// this only stops the compiler from moving accesses across the point).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 4 bytes at any LDS byte offset: two aligned dword reads + v_alignbyte.
+__device__ __forceinline__ uint32_t lds32u(const uint8_t* lds, uint32_t i) {
+    const uint32_t* w = (const uint32_t*)(lds + (i & ~3u));
+    return __builtin_amdgcn_alignbyte(w[1], w[0], i & 3u);
+}
+
+// 4 bytes at any global address where `avail` (>= 1) bytes from p are valid. Only aligned
+// dwords that contain a valid byte are touched (never faults past the end of a buffer).
+__device__ __forceinline__ uint32_t gld32u(const uint8_t* p, uint32_t avail) {
+    uintptr_t a = (uintptr_t)p;
+    const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+    uint32_t sh = (uint32_t)(a & 3);
+    uint32_t lo = w[0];
+    uint32_t hi = (sh != 0 && avail > 4 - sh) ? w[1] : 0u;
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    return x - v;
+}
+
+// Wave-cooperative copy of n bytes global -> global, any alignment of either side.
+__device__ void wave_copy_global(uint8_t* dst, const uint8_t* src, uint32_t n, int lane) {
+    uintptr_t da = (uintptr_t)dst;
+    uint32_t head = (uint32_t)((16 - (da & 15)) & 15);
+    if (head > n) head = n;
+    if ((uint32_t)lane < head) dst[lane] = src[lane];
+    uint32_t body = (n - head) & ~15u;
+    const uint8_t* s = src + head;
+    uint8_t* d = dst + head;
+    if ((((uintptr_t)s) & 3) == 0) {
+        for (uint32_t c = (uint32_t)lane * 16; c < body; c += 64 * 16) {
+            const uint32_t* sw = (const uint32_t*)(s + c);
+            uint4 v = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+            *(uint4*)(d + c) = v;
+        }
+    } else {
+        uintptr_t sa = (uintptr_t)s;
+        uint32_t sh = (uint32_t)(sa & 3);
+        for (uint32_t c = (uint32_t)lane * 16; c < body; c += 64 * 16) {
+            const uint32_t* sw = (const uint32_t*)((sa + c) & ~(uintptr_t)3);
+            uint32_t w0 = sw[0], w1 = sw[1], w2 = sw[2], w3 = sw[3], w4 = sw[4];
+            uint4 v = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                 __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+            *(uint4*)(d + c) = v;
+        }
+    }
+    for (uint32_t t = head + body + (uint32_t)lane; t < n; t += 64) dst[t] = src[t];
+}
+
+// Wave-cooperative store of n bytes from (contiguous) LDS to global, any global alignment.
+__device__ void wave_store_from_lds(uint8_t* dst, const uint8_t* lds, uint32_t n, int lane) {
+    uintptr_t da = (uintptr_t)dst;
+    uint32_t head = (uint32_t)((16 - (da & 15)) & 15);
+    if (head > n) head = n;
+    if ((uint32_t)lane < head) dst[lane] = lds[lane];
+    uint32_t body = (n - head) & ~15u;
+    for (uint32_t c = (uint32_t)lane * 16; c < body; c += 64 * 16) {
+        uint32_t i = head + c;
+        uint4 v = make_uint4(lds32u(lds, i), lds32u(lds, i + 4), lds32u(lds, i + 8), lds32u(lds, i + 12));
+        *(uint4*)(dst + i) = v;
+    }
+    for (uint32_t t = head + body + (uint32_t)lane; t < n; t += 64) dst[t] = lds[t];
+}
+
+// ------------------------------------------------------------------- xxh32
+#define XP1 2654435761U
+#define XP2 2246822519U
+#define XP3 3266489917U
+#define XP4 668265263U
+#define XP5 374761393U
+
+__device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t in) {
+    acc += in * XP2;
+    acc = rotl32(acc, 13);
+    return acc * XP1;
+}
+
+// out[r] = xxh32(base + off[r], len[r], seed 0). Lanes 4r..4r+3 run the 4 accumulator chains.
+__global__ __launch_bounds__(256) void k_xxh32_ranges(const uint8_t* __restrict__ base,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ len, uint32_t n,
+                                                      uint32_t* __restrict__ out) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t r = gid >> 2, a = gid & 3;
+    const int lane = lane_id();
+    const bool act = r < n;
+    const uint32_t L = act ? len[r] : 0u;
+    const uint8_t* p = base + (act ? off[r] : 0);
+    const uint32_t ns = L >> 4;
+    uint32_t acc = a == 0 ? XP1 + XP2 : (a == 1 ? XP2 : (a == 2 ? 0u : 0u - XP1));
+    const uint8_t* q = p + 4 * a;
+    uint32_t s = 0;
+    if ((((uintptr_t)p) & 3) == 0) {
+        const uint32_t* w = (const uint32_t*)q;
+        for (; s + 8 <= ns; s += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = w[4 * (s + k)];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc = xround(acc, v[k]);
+        }
+        for (; s < ns; ++s) acc = xround(acc, w[4 * s]);
+    } else {
+        for (; s < ns; ++s) acc = xround(acc, gld32u(q + 16 * s, L - 16 * s - 4 * a));
+    }
+    const int qb = lane & ~3;
+    uint32_t v1 = __shfl(acc, qb), v2 = __shfl(acc, qb + 1), v3 = __shfl(acc, qb + 2), v4 = __shfl(acc, qb + 3);
+    if (!act || a != 0) return;
+    uint32_t h = L >= 16 ? rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18) : XP5;
+    h += L;
+    uint32_t t = ns * 16;
+    while (t + 4 <= L) {
+        h += gld32u(p + t, L - t) * XP3;
+        h = rotl32(h, 17) * XP4;
+        t += 4;
+    }
+    while (t < L) {
+        h += (uint32_t)p[t] * XP5;
+        h = rotl32(h, 11) * XP1;
+        t++;
+    }
+    h ^= h >> 15;
+    h *= XP2;
+    h ^= h >> 13;
+    h *= XP3;
+    h ^= h >> 16;
+    out[r] = h;
+}
+
+// ================================================================== decode
+namespace dec {
+constexpr uint32_t kStage = 512;   // compressed bytes staged per wave
+constexpr uint32_t kRing = 4096;   // recent output kept in LDS per wave (match sources)
+constexpr uint32_t kMask = kRing - 1;
+constexpr uint32_t kFlush = 1024;  // ring -> HBM flush granule
+constexpr uint32_t kWaveLds = kRing + kStage + 64;
+constexpr int kWaves = 4;
+enum : uint32_t { F_ERR = 1, F_LAST = 2, F_LONG = 4, F_MORE = 8 };
+}  // namespace dec
+
+struct DecWave {
+    uint8_t* ring;
+    uint8_t* stage;
+    uint8_t* out;        // unit output base in HBM
+    uint32_t upos;       // bytes produced in this unit
+    uint32_t flushed;    // bytes of the unit already written to HBM
+    int lane;
+};
+
+__device__ __forceinline__ void dec_flush(DecWave& w, uint32_t from, uint32_t n) {
+    // [from, from+n) is contiguous in the ring (from is a multiple of kFlush or n < kFlush
+    // and the range does not wrap) -> HBM.
+    const uint8_t* src = w.ring + (from & dec::kMask);
+    uint8_t* dst = w.out + from;
+    if ((((uintptr_t)dst) & 15) == 0 && n == dec::kFlush) {
+        uint4 v = *(const uint4*)(src + 16 * w.lane);
+        *(uint4*)(dst + 16 * w.lane) = v;
+    } else {
+        wave_store_from_lds(dst, src, n, w.lane);
+    }
+}
+__device__ __forceinline__ void dec_maybe_flush(DecWave& w) {
+    while (w.upos - w.flushed >= dec::kFlush) {
+        dec_flush(w, w.flushed, dec::kFlush);
+        w.flushed += dec::kFlush;
+    }
+}
+__device__ __forceinline__ void dec_final_flush(DecWave& w) {
+    dec_maybe_flush(w);
+    uint32_t rem = w.upos - w.flushed;
+    if (rem) {
+        uint32_t first = dec::kRing - (w.flushed & dec::kMask);
+        if (rem <= first) {
+            dec_flush(w, w.flushed, rem);
+        } else {
+            dec_flush(w, w.flushed, first);
+            dec_flush(w, w.flushed + first, rem - first);
+        }
+        w.flushed = w.upos;
+    }
+}
+
+// Literal run [lit, lit+ll) of the block input -> output.
+__device__ __forceinline__ void dec_literals(DecWave& w, const uint8_t* in, uint32_t lit, uint32_t ll,
+                                             uint32_t st_lo, bool staged) {
+    for (uint32_t k0 = 0; k0 < ll; k0 += 64) {
+        uint32_t piece = ll - k0 < 64 ? ll - k0 : 64;
+        uint32_t base = w.upos;
+        if ((uint32_t)w.lane < piece) {
+            uint32_t k = k0 + w.lane;
+            uint8_t b = staged ? w.stage[lit + k - st_lo] : in[lit + k];
+            w.ring[(base + w.lane) & dec::kMask] = b;
+        }
+        w.upos = base + piece;
+        dec_maybe_flush(w);
+    }
+}
+
+// Match of ml bytes at distance off (off validated by the caller).
+__device__ __forceinline__ void dec_match(DecWave& w, uint32_t off, uint32_t ml) {
+    const uint32_t p = w.upos;
+    for (uint32_t k0 = 0; k0 < ml; k0 += 64) {
+        uint32_t piece = ml - k0 < 64 ? ml - k0 : 64;
+        uint32_t base = w.upos;
+        if ((uint32_t)w.lane < piece) {
+            uint32_t k = k0 + w.lane;
+            uint32_t x = off >= ml ? p - off + k : p - off + (k % off);
+            uint8_t b;
+            if (x + (dec::kRing - 64) >= base) b = w.ring[x & dec::kMask];
+            else b = w.out[x];  // older than the ring: already flushed by this wave
+            w.ring[(base + w.lane) & dec::kMask] = b;
+        }
+        w.upos = base + piece;
+        dec_maybe_flush(w);
+    }
+}
+
+// Stage [lo, lo+kStage) of the block input (bytes >= C left undefined).
+__device__ __forceinline__ void dec_stage(const uint8_t* in, uint32_t C, uint32_t lo, uint8_t* stage, int lane) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        uint32_t i = 8u * lane + 4u * k;
+        if (lo + i < C) *(uint32_t*)(stage + i) = gld32u(in + lo + i, C - lo - i);
+    }
+    wave_sync();
+}
+
+// Wave-cooperative LZ4 length-extension scan at pos (bytes of 255 continue the run).
+__device__ __forceinline__ int dec_ext_scan(const uint8_t* in, uint32_t C, uint32_t& pos, uint32_t& acc, int lane) {
+    for (;;) {
+        uint32_t k = pos + lane;
+        uint32_t b = k < C ? (uint32_t)in[k] : 0x100u;
+        uint64_t m = __ballot(b != 255u);
+        if (m == 0) {
+            acc += 255u * 64u;
+            pos += 64;
+            if (acc > (64u << 20)) return S3HC_CORRUPT;
+            continue;
+        }
+        uint32_t f = (uint32_t)__builtin_ctzll(m);
+        uint32_t bf = rdl(b, f);
+        if (bf == 0x100u) return S3HC_CORRUPT;
+        acc += 255u * f + bf;
+        pos += f + 1;
+        return S3HC_OK;
+    }
+}
+
+// Decode one compressed block of C bytes. hist = bytes of earlier unit output matches may use.
+// Output overflowing `limit` is corruption (lz4_flex: output sink bounded by the block size);
+// overflowing only `cap` is DST_TOO_SMALL.
+__device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t limit, uint32_t cap, uint32_t hist) {
+    using namespace dec;
+    const int lane = w.lane;
+    const uint32_t bstart = w.upos;
+    uint32_t q = 0;
+    uint32_t st_lo = 0xFFFFFFFFu;
+    for (;;) {
+        if (q >= C) return S3HC_CORRUPT;  // a token was expected
+        if (st_lo == 0xFFFFFFFFu || q < st_lo || q + 192 > st_lo + kStage) {
+            st_lo = q & ~3u;
+            dec_stage(in, C, st_lo, w.stage, lane);
+        }
+        // ---- speculative parse: lane assumes a token at qq = q + lane
+        const uint32_t qq = q + lane;
+        const uint32_t i = qq - st_lo;
+        uint32_t flags = 0, nxt = 0, lit = 0, ll = 0, off = 0, ml = 0;
+        {
+            const uint32_t t = w.stage[i];
+            uint32_t j = i + 1;
+            ll = t >> 4;
+            if (ll == 15) {
+                uint32_t e = w.stage[j++];
+                ll += e;
+                if (e == 255) {
+                    e = w.stage[j++];
+                    ll += e;
+                    if (e == 255) flags |= F_LONG;
+                }
+            }
+            lit = st_lo + j;
+            if (qq >= C || lit > C || ll > C - lit) {
+                flags |= F_ERR;
+            } else {
+                const uint32_t mp = lit + ll;
+                if (mp == C) {
+                    flags |= F_LAST;
+                    nxt = C;
+                } else if (C - mp < 2) {
+                    flags |= F_ERR;
+                } else if (mp - st_lo + 4 > kStage) {
+                    flags |= F_MORE;
+                } else {
+                    const uint32_t mi = mp - st_lo;
+                    off = (uint32_t)w.stage[mi] | ((uint32_t)w.stage[mi + 1] << 8);
+                    uint32_t k = mp + 2;
+                    ml = (t & 15) + 4;
+                    if ((t & 15) == 15) {
+                        if (k >= C) {
+                            flags |= F_ERR;
+                        } else {
+                            uint32_t e = w.stage[k - st_lo];
+                            k++;
+                            ml += e;
+                            if (e == 255) {
+                                if (k >= C) {
+                                    flags |= F_ERR;
+                                } else {
+                                    e = w.stage[k - st_lo];
+                                    k++;
+                                    ml += e;
+                                    if (e == 255) flags |= F_LONG;
+                                }
+                            }
+                        }
+                    }
+                    nxt = k;
+                }
+            }
+        }
+        // ---- walk the true token chain through the window (scalar)
+        uint64_t members = 0;
+        uint32_t cur = q;
+        int stop = 0;  // 0 window exhausted, 1 last sequence, 2 error, 3 slow path at cur
+        for (;;) {
+            uint32_t l = cur - q;
+            if (l >= 64) break;
+            uint32_t f = rdl(flags, l);
+            if (f & (F_LONG | F_MORE)) { stop = 3; break; }
+            if (f & F_ERR) { stop = 2; break; }
+            members |= 1ull << l;
+            if (f & F_LAST) { stop = 1; break; }
+            cur = rdl(nxt, l);
+        }
+        // ---- execute the chain in order
+        while (members) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(members);
+            members &= members - 1;
+            const uint32_t mlit = rdl(lit, l), mll = rdl(ll, l), mf = rdl(flags, l);
+            const uint32_t produced = w.upos - bstart;
+            if (mll > limit - produced) return S3HC_CORRUPT;
+            if (mll > cap - produced) return S3HC_DST_TOO_SMALL;
+            dec_literals(w, in, mlit, mll, st_lo, mlit >= st_lo && mlit + mll <= st_lo + kStage);
+            if (mf & F_LAST) break;
+            const uint32_t moff = rdl(off, l), mml = rdl(ml, l);
+            const uint32_t have = w.upos - bstart;
+            if (moff == 0 || moff > have + hist) return S3HC_CORRUPT;
+            if (mml > limit - have) return S3HC_CORRUPT;
+            if (mml > cap - have) return S3HC_DST_TOO_SMALL;
+            dec_match(w, moff, mml);
+        }
+        if (stop == 1) return S3HC_OK;
+        if (stop == 2) return S3HC_CORRUPT;
+        if (stop == 3) {
+            // Slow path: this sequence has long length runs or reaches past the stage.
+            uint32_t pos = cur;
+            const uint32_t t = in[pos];
+            pos++;
+            uint32_t sll = t >> 4;
+            if (sll == 15 && dec_ext_scan(in, C, pos, sll, lane)) return S3HC_CORRUPT;
+            if (sll > C - pos) return S3HC_CORRUPT;
+            const uint32_t slit = pos;
+            pos += sll;
+            const uint32_t produced = w.upos - bstart;
+            if (sll > limit - produced) return S3HC_CORRUPT;
+            if (sll > cap - produced) return S3HC_DST_TOO_SMALL;
+            dec_literals(w, in, slit, sll, st_lo, slit >= st_lo && slit + sll <= st_lo + kStage);
+            if (pos == C) return S3HC_OK;
+            if (C - pos < 2) return S3HC_CORRUPT;
+            const uint32_t soff = (uint32_t)in[pos] | ((uint32_t)in[pos + 1] << 8);
+            pos += 2;
+            uint32_t sml = (t & 15) + 4;
+            if ((t & 15) == 15 && dec_ext_scan(in, C, pos, sml, lane)) return S3HC_CORRUPT;
+            const uint32_t have = w.upos - bstart;
+            if (soff == 0 || soff > have + hist) return S3HC_CORRUPT;
+            if (sml > limit - have) return S3HC_CORRUPT;
+            if (sml > cap - have) return S3HC_DST_TOO_SMALL;
+            dec_match(w, soff, sml);
+            cur = pos;
+        }
+        q = cur;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict__ src, uint8_t* dst,
+                                                      const DecBlock* __restrict__ blk,
+                                                      const DecUnit* __restrict__ units, uint32_t nunits,
+                                                      uint32_t* __restrict__ blk_out,
+                                                      int32_t* __restrict__ blk_status) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[dec::kWaves * dec::kWaveLds];
+    const int lane = lane_id();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t u = blockIdx.x * dec::kWaves + wv;
+    if (u >= nunits) return;
+    const DecUnit U = units[u];
+    if (U.n == 0) return;
+    DecWave w;
+    w.ring = smem + wv * dec::kWaveLds;
+    w.stage = w.ring + dec::kRing;
+    w.out = dst + blk[U.first].dst_off;
+    w.upos = 0;
+    w.flushed = 0;
+    w.lane = lane;
+    int status = S3HC_OK;
+    for (uint32_t b = 0; b < U.n; ++b) {
+        const DecBlock B = blk[U.first + b];
+        const uint32_t start = w.upos;
+        if (status == S3HC_OK) {
+            const uint8_t* in = src + B.src_off;
+            const uint32_t hist = (B.flags & DB_LINKED) ? start : 0u;
+            if (B.flags & DB_STORED) {
+                if (B.csize > B.limit) status = S3HC_CORRUPT;
+                else if (B.csize > B.cap) status = S3HC_DST_TOO_SMALL;
+                else if (U.n == 1) {
+                    wave_copy_global(w.out, in, B.csize, lane);
+                    w.upos = w.flushed = B.csize;
+                } else {
+                    dec_literals(w, in, 0, B.csize, 0xFFFFFFFFu, false);
+                }
+            } else {
+                status = dec_block(w, in, B.csize, B.limit, B.cap, hist);
+            }
+        }
+        if (lane == 0) {
+            blk_out[U.first + b] = status == S3HC_OK ? w.upos - start : 0u;
+            blk_status[U.first + b] = status;
+        }
+    }
+    dec_final_flush(w);
+}
+
+// ================================================================== encode
+namespace enc {
+constexpr uint32_t kIn = kPrewarm + kSeg + 128;         // staged input bytes (+ read-ahead pad)
+constexpr uint32_t kTbl = 1u << kHashLog;
+constexpr uint32_t kWaveLds = kIn + kTbl * 2;
+constexpr int kWaves = 4;
+constexpr uint16_t kEmpty = 0xFFFF;
+}  // namespace enc
+
+__device__ __forceinline__ uint32_t ext_bytes(uint32_t n) { return n >= 15 ? (n - 15) / 255 + 1 : 0; }
+__device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
+
+// Stage block bytes [lo, hi) into lds (lds[x - lo]); any alignment.
+__device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* lds, int lane) {
+    const uint32_t n = hi - lo;
+    for (uint32_t i = 4u * lane; i < n; i += 256) *(uint32_t*)(lds + i) = gld32u(blk + lo + i, n - i);
+    wave_sync();
+}
+
+__global__ __launch_bounds__(256) void k_enc_parse(const uint8_t* __restrict__ src,
+                                                   const EncBlock* __restrict__ blocks,
+                                                   const uint32_t* __restrict__ seg_block, uint32_t nseg,
+                                                   uint2* __restrict__ recs, SegSummary* __restrict__ summ) {
+    using namespace enc;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kWaves * kWaveLds];
+    const int lane = lane_id();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t s = blockIdx.x * kWaves + wv;
+    if (s >= nseg) return;
+    const uint32_t b = seg_block[s];
+    const EncBlock B = blocks[b];
+    if (B.flags & (EB_STORE | EB_EMPTY)) return;
+    uint8_t* inb = smem + wv * kWaveLds;
+    uint16_t* tbl = (uint16_t*)(inb + kIn);
+    const uint32_t U = B.len;
+    const uint32_t k = s - B.seg0;
+    const uint32_t seg_lo = k * kSeg;
+    const uint32_t seg_hi = seg_lo + kSeg < U ? seg_lo + kSeg : U;
+    const uint32_t pw_lo = seg_lo > kPrewarm ? seg_lo - kPrewarm : 0;
+    const uint32_t st_hi = seg_hi + 64 < U ? seg_hi + 64 : U;
+    const uint8_t* bin = src + B.src_off;
+    stage_in(bin, pw_lo, st_hi, inb, lane);
+    for (uint32_t t = lane; t < kTbl / 2; t += 64) ((uint32_t*)tbl)[t] = 0xFFFFFFFFu;
+    wave_sync();
+    // Largest match end, largest match start (LZ4: last 5 bytes literal, last match starts
+    // >= 12 bytes before the block end; segment matches end inside the segment).
+    const uint32_t blk_end_lim = U >= 5 ? U - 5 : 0;
+    const uint32_t end_lim = seg_hi < blk_end_lim ? seg_hi : blk_end_lim;
+    int64_t smax = (int64_t)end_lim - 4;
+    if ((int64_t)U - 12 < smax) smax = (int64_t)U - 12;
+    // prewarm the table with the window before the segment
+    for (uint32_t x = pw_lo + lane; x + 4 <= seg_lo; x += 64) tbl[hash4(lds32u(inb, x - pw_lo))] = (uint16_t)(x - pw_lo);
+    wave_sync();
+
+    uint32_t lit_start = seg_lo;
+    uint32_t W = seg_lo;
+    uint32_t nseq = 0, body = 0, ll0 = 0;
+    uint32_t rx = 0, ry = 0;
+    uint2* myrec = recs + (size_t)s * kMaxSeqPerSeg;
+    while ((int64_t)W <= smax) {
+        const uint32_t P = W + lane;
+        const bool valid = (int64_t)P <= smax;
+        const uint32_t v = lds32u(inb, P - pw_lo);
+        const uint32_t h = hash4(v);
+        const uint32_t c16 = tbl[h];
+        uint32_t c = pw_lo + c16;
+        bool good = valid && c16 != kEmpty && c < P && lds32u(inb, c - pw_lo) == v;
+        // short-period repeats inside the probe window (runs, 2-4 byte patterns)
+        const uint32_t v1 = __shfl_up(v, 1), v2 = __shfl_up(v, 2), v3 = __shfl_up(v, 3), v4 = __shfl_up(v, 4);
+        if (!good && valid) {
+            if (lane >= 1 && v1 == v) { good = true; c = P - 1; }
+            else if (lane >= 2 && v2 == v) { good = true; c = P - 2; }
+            else if (lane >= 3 && v3 == v) { good = true; c = P - 3; }
+            else if (lane >= 4 && v4 == v) { good = true; c = P - 4; }
+        }
+        const uint64_t mask = __ballot(good);
+        // Insert only the positions the parse has passed (lanes up to the first match):
+        // later lanes are probed again by the next window, and inserting them now would
+        // shadow their own older candidates.
+        const uint32_t f = mask ? (uint32_t)__builtin_ctzll(mask) : 63u;
+        if (valid && (uint32_t)lane <= f) tbl[h] = (uint16_t)(P - pw_lo);
+        if (mask == 0) {
+            W += 64;
+            continue;
+        }
+        uint32_t p = W + f;
+        uint32_t cc = rdl(c, f);
+        // backward extension into the pending literals
+        {
+            const uint32_t lim = (p - lit_start) < (cc - pw_lo) ? (p - lit_start) : (cc - pw_lo);
+            uint32_t nb = 0;
+            while (nb < lim) {
+                const uint32_t kk = nb + lane;
+                const bool eq = kk < lim && inb[p - 1 - kk - pw_lo] == inb[cc - 1 - kk - pw_lo];
+                const uint64_t m = __ballot(!eq);
+                if (m == 0) { nb += 64; continue; }
+                nb += (uint32_t)__builtin_ctzll(m);
+                break;
+            }
+            if (nb > lim) nb = lim;
+            p -= nb;
+            cc -= nb;
+            // forward extension
+            const uint32_t maxlen = end_lim - p;
+            uint32_t len = nb + 4;
+            for (;;) {
+                const uint32_t rel = len + 4u * lane;
+                uint32_t eqb;
+                if (rel >= maxlen) {
+                    eqb = 0;
+                } else {
+                    uint32_t ia = p + rel - pw_lo, ib = cc + rel - pw_lo;
+                    if (ia > kIn - 8) ia = kIn - 8;
+                    const uint32_t x = lds32u(inb, ia), y = lds32u(inb, ib);
+                    eqb = x == y ? 4u : (uint32_t)__builtin_ctz(x ^ y) >> 3;
+                    if (eqb > maxlen - rel) eqb = maxlen - rel;
+                }
+                const uint64_t m = __ballot(eqb != 4u);
+                if (m == 0) { len += 256; continue; }
+                const uint32_t g = (uint32_t)__builtin_ctzll(m);
+                len += 4u * g + rdl(eqb, g);
+                break;
+            }
+            const uint32_t ll = p - lit_start;
+            const uint32_t off = p - cc;
+            if (nseq == 0) {
+                ll0 = ll;
+                body += ll + 2 + ext_bytes(len - 4);
+            } else {
+                body += 1 + ext_bytes(ll) + ll + 2 + ext_bytes(len - 4);
+            }
+            if ((uint32_t)lane == (nseq & 63)) {
+                rx = ll | (len << 16);
+                ry = off;
+            }
+            nseq++;
+            if ((nseq & 63) == 0) {
+                myrec[nseq - 64 + lane] = make_uint2(rx, ry);
+            }
+            lit_start = p + len;
+            W = lit_start;
+            if (lane == 0) {  // as lz4_flex: remember the position two bytes before the match end
+                const uint32_t x = lit_start - 2;
+                tbl[hash4(lds32u(inb, x - pw_lo))] = (uint16_t)(x - pw_lo);
+            }
+            wave_sync();
+        }
+    }
+    if (nseq & 63) {
+        if ((uint32_t)lane < (nseq & 63)) myrec[(nseq & ~63u) + lane] = make_uint2(rx, ry);
+    }
+    if (lane == 0) {
+        SegSummary S;
+        S.nseq = nseq;
+        S.ll0 = ll0;
+        S.body = body;
+        S.trail = seg_hi - lit_start;
+        summ[s] = S;
+    }
+}
+
+// One thread per block: stitch segment carries, size the payload, decide stored/compressed.
+__global__ void k_enc_sizes(const EncBlock* __restrict__ blocks, uint32_t nblocks,
+                            const SegSummary* __restrict__ summ, SegPlace* __restrict__ place,
+                            uint32_t* __restrict__ blk_payload, uint32_t* __restrict__ blk_size,
+                            uint32_t* __restrict__ blk_carry) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblocks) return;
+    const EncBlock B = blocks[b];
+    const uint32_t hdr = (B.flags & EB_FIRST) ? 7u : 0u;
+    const uint32_t trl = (B.flags & EB_LAST) ? 8u : 0u;
+    if (B.flags & EB_EMPTY) {
+        blk_payload[b] = 0;
+        blk_size[b] = hdr + trl;
+        blk_carry[b] = 0;
+        return;
+    }
+    uint32_t payload = B.len;
+    bool stored = true;
+    uint32_t carry = 0;
+    if (!(B.flags & EB_STORE)) {
+        uint32_t off = 0;
+        for (uint32_t k = 0; k < B.nseg; ++k) {
+            const SegSummary S = summ[B.seg0 + k];
+            const uint32_t lo = k * kSeg;
+            const uint32_t hi = lo + kSeg < B.len ? lo + kSeg : B.len;
+            SegPlace P;
+            P.out_off = off;
+            P.carry = carry;
+            place[B.seg0 + k] = P;
+            if (S.nseq == 0) {
+                carry += hi - lo;
+                continue;
+            }
+            const uint32_t lle = carry + S.ll0;
+            off += 1 + ext_bytes(lle) + carry + S.body;
+            carry = S.trail;
+        }
+        off += 1 + ext_bytes(carry) + carry;
+        if (off < B.len) {  // lz4_flex write_block: Compressed iff comp_len < src.len()
+            stored = false;
+            payload = off;
+        }
+    }
+    blk_payload[b] = payload | (stored ? kStoredBit : 0u);
+    blk_size[b] = hdr + 4 + payload + trl;
+    blk_carry[b] = carry;
+}
+
+// One wave per segment: write this segment's share of the framed output.
+__global__ __launch_bounds__(256) void k_enc_emit(const uint8_t* __restrict__ src,
+                                                  const EncBlock* __restrict__ blocks,
+                                                  const uint32_t* __restrict__ seg_block, uint32_t nseg,
+                                                  const uint2* __restrict__ recs,
+                                                  const SegSummary* __restrict__ summ,
+                                                  const SegPlace* __restrict__ place,
+                                                  const uint32_t* __restrict__ blk_payload,
+                                                  const uint32_t* __restrict__ blk_carry,
+                                                  const uint64_t* __restrict__ blk_off,
+                                                  const uint32_t* __restrict__ frame_hash, uint8_t* dst) {
+    constexpr uint32_t kOut = 2 * kSeg + 1024;  // encoded segment body bound
+    constexpr uint32_t kIb = kSeg + 64;
+    constexpr uint32_t kWaveLds = kOut + kIb;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kWaveLds];
+    const int lane = lane_id();
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t s = blockIdx.x * 2 + wv;
+    if (s >= nseg) return;
+    uint8_t* ob = smem + wv * kWaveLds;
+    uint8_t* ib = ob + kOut;
+    const uint32_t b = seg_block[s];
+    const EncBlock B = blocks[b];
+    const uint32_t k = s - B.seg0;
+    uint8_t* fo = dst + blk_off[b];
+    const uint32_t hdr = (B.flags & EB_FIRST) ? 7u : 0u;
+    const uint32_t pw = blk_payload[b];
+    const bool stored = (pw & kStoredBit) != 0;
+    const uint32_t payload = pw & ~kStoredBit;
+    const uint32_t fh = frame_hash[B.frame];
+    if (k == 0 && lane == 0) {
+        if (B.flags & EB_FIRST) {
+            fo[0] = 0x04; fo[1] = 0x22; fo[2] = 0x4D; fo[3] = 0x18;
+            fo[4] = kFlgIndependentChecksum; fo[5] = B.bd; fo[6] = B.hc;
+        }
+        if (!(B.flags & EB_EMPTY)) {
+            const uint32_t word = stored ? (B.len | kStoredBit) : payload;
+            fo[hdr + 0] = (uint8_t)word; fo[hdr + 1] = (uint8_t)(word >> 8);
+            fo[hdr + 2] = (uint8_t)(word >> 16); fo[hdr + 3] = (uint8_t)(word >> 24);
+        }
+    }
+    const bool last_seg = k + 1 == B.nseg;
+    if ((B.flags & EB_LAST) && last_seg && lane < 8) {
+        const uint32_t tpos = (B.flags & EB_EMPTY) ? hdr : hdr + 4 + payload;
+        const uint32_t v = lane < 4 ? 0u : fh;
+        fo[tpos + lane] = (uint8_t)(v >> (8 * (lane & 3)));
+    }
+    if (B.flags & EB_EMPTY) return;
+    uint8_t* pay = fo + hdr + 4;
+    const uint32_t seg_lo = k * kSeg;
+    const uint32_t seg_hi = seg_lo + kSeg < B.len ? seg_lo + kSeg : B.len;
+    const uint8_t* bin = src + B.src_off;
+    if (stored) {
+        wave_copy_global(pay + seg_lo, bin + seg_lo, seg_hi - seg_lo, lane);
+        return;
+    }
+    const SegSummary S = summ[s];
+    const SegPlace P = place[s];
+    uint32_t o = P.out_off;  // payload-relative write cursor
+    if (S.nseq > 0) {
+        const uint2* rr = recs + (size_t)s * kMaxSeqPerSeg;
+        const uint32_t ml0 = rr[0].x >> 16;
+        // first token: literal run = carry bytes (earlier segments) + ll0 (this segment)
+        const uint32_t lle = P.carry + S.ll0;
+        const uint32_t ne = ext_bytes(lle);
+        if (lane == 0) {
+            const uint32_t mn = ml0 - 4;
+            pay[o] = (uint8_t)(((lle < 15 ? lle : 15) << 4) | (mn < 15 ? mn : 15));
+        }
+        for (uint32_t e = lane; e < ne; e += 64) pay[o + 1 + e] = e + 1 < ne ? 255 : (uint8_t)((lle - 15) % 255);
+        o += 1 + ne;
+        wave_copy_global(pay + o, bin + seg_lo - P.carry, P.carry, lane);
+        o += P.carry;
+        // body: records -> LDS, then one coalesced store
+        stage_in(bin, seg_lo, seg_hi, ib, lane);
+        uint32_t ob_len = 0;   // bytes assembled in ob
+        uint32_t in_pos = 0;   // segment-relative input cursor
+        for (uint32_t g = 0; g < S.nseq; g += 64) {
+            const uint32_t j = g + lane;
+            const bool act = j < S.nseq;
+            const uint2 r = act ? rr[j] : make_uint2(0, 0);
+            const uint32_t ll = r.x & 0xFFFFu, ml = r.x >> 16, off = r.y;
+            const uint32_t hsz = j == 0 ? 0u : 1 + ext_bytes(ll);
+            const uint32_t sz = act ? hsz + ll + 2 + ext_bytes(ml - 4) : 0u;
+            const uint32_t opos = ob_len + wave_excl_scan(sz, lane);
+            const uint32_t ipos = in_pos + wave_excl_scan(act ? ll + ml : 0u, lane);
+            const uint32_t tot = rdl(opos + sz, 63) - ob_len;                 // this group's bytes
+            const uint32_t itot = rdl(ipos + (act ? ll + ml : 0u), 63) - in_pos;
+            if (act) {
+                uint32_t w = opos;
+                if (j != 0) {
+                    const uint32_t mn = ml - 4;
+                    ob[w++] = (uint8_t)(((ll < 15 ? ll : 15) << 4) | (mn < 15 ? mn : 15));
+                    if (ll >= 15) {
+                        uint32_t x = ll - 15;
+                        while (x >= 255) { ob[w++] = 255; x -= 255; }
+                        ob[w++] = (uint8_t)x;
+                    }
+                }
+                if (ll <= 48) {
+                    for (uint32_t t = 0; t < ll; ++t) ob[w + t] = ib[ipos + t];
+                }
+                w += ll;
+                ob[w++] = (uint8_t)off;
+                ob[w++] = (uint8_t)(off >> 8);
+                if (ml - 4 >= 15) {
+                    uint32_t x = ml - 4 - 15;
+                    while (x >= 255) { ob[w++] = 255; x -= 255; }
+                    ob[w++] = (uint8_t)x;
+                }
+            }
+            // long literal runs: wave-cooperative copy, one record at a time
+            uint64_t longm = __ballot(act && ll > 48);
+            while (longm) {
+                const uint32_t l = (uint32_t)__builtin_ctzll(longm);
+                longm &= longm - 1;
+                const uint32_t lll = rdl(ll, l), lo = rdl(opos, l) + rdl(hsz, l), li = rdl(ipos, l);
+                for (uint32_t t = lane; t < lll; t += 64) ob[lo + t] = ib[li + t];
+            }
+            wave_sync();
+            ob_len += tot;
+            in_pos += itot;
+        }
+        wave_store_from_lds(pay + o, ob, ob_len, lane);
+        o += ob_len;
+    }
+    if (last_seg) {
+        const uint32_t L = blk_carry[b];
+        const uint32_t ne = ext_bytes(L);
+        if (lane == 0) pay[o] = (uint8_t)((L < 15 ? L : 15) << 4);
+        for (uint32_t e = lane; e < ne; e += 64) pay[o + 1 + e] = e + 1 < ne ? 255 : (uint8_t)((L - 15) % 255);
+        o += 1 + ne;
+        wave_copy_global(pay + o, bin + B.len - L, L, lane);
+    }
+}
+
+// Per frame: offset and framed length from the block table.
+__global__ void k_enc_frames(const uint32_t* __restrict__ frame_blk0, const uint32_t* __restrict__ frame_nblk,
+                             uint32_t nframes, const uint64_t* __restrict__ blk_off,
+                             const uint32_t* __restrict__ blk_size, uint64_t* __restrict__ frame_off,
+                             uint32_t* __restrict__ frame_len) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    const uint32_t b0 = frame_blk0[f], nb = frame_nblk[f];
+    uint64_t len = 0;
+    for (uint32_t i = 0; i < nb; ++i) len += blk_size[b0 + i];
+    frame_off[f] = blk_off[b0];
+    frame_len[f] = (uint32_t)len;
+}
+
+// Exclusive scan of u32 sizes into u64 offsets: single workgroup, chunked (n up to millions).
+__global__ __launch_bounds__(1024) void k_scan_u32_u64(const uint32_t* __restrict__ in, uint32_t n,
+                                                       uint64_t* __restrict__ out, uint64_t* __restrict__ total) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry_s;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) carry_s = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < n; base += 1024 * 4) {
+        uint64_t v[4];
+        uint64_t loc = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t i = base + 4 * t + k;
+            v[k] = i < n ? in[i] : 0;
+            loc += v[k];
+        }
+        uint64_t x = loc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            uint64_t y = __shfl_up(x, d);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) wsum[wv] = x;
+        __syncthreads();
+        uint64_t wpre = 0;
+        for (int k = 0; k < wv; ++k) wpre += wsum[k];
+        uint64_t run = carry_s + wpre + x - loc;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t i = base + 4 * t + k;
+            if (i < n) out[i] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        if (t == 1023) carry_s = run;
+        __syncthreads();
+    }
+    if (t == 0) *total = carry_s;
+}
+
+// ============================================ device-side frame walk (decode)
+// One thread per frame: validate the header (FrameInfo::read), walk block words, count blocks.
+// Header/BD/HC rules follow lz4_flex frame/header.rs as restated in oracle/lz4_oracle.c.
+__device__ __forceinline__ uint32_t rd32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ uint32_t xxh32_small(const uint8_t* p, uint32_t n) {  // n < 16 (frame header bytes)
+    uint32_t h = XP5 + n, t = 0;
+    while (t + 4 <= n) { h += rd32(p + t) * XP3; h = rotl32(h, 17) * XP4; t += 4; }
+    while (t < n) { h += (uint32_t)p[t] * XP5; h = rotl32(h, 11) * XP1; t++; }
+    h ^= h >> 15; h *= XP2; h ^= h >> 13; h *= XP3; h ^= h >> 16;
+    return h;
+}
+
+struct FrameWalk {
+    int status;
+    uint32_t nblk;
+    uint32_t bmax;
+    uint32_t flg;
+    uint32_t hdr;
+    uint32_t end;        // bytes consumed by the frame (through its checksum)
+    uint32_t want;       // expected content checksum
+    uint32_t content_lo; // content size (low 32 bits) if FLG content-size bit
+};
+
+__device__ FrameWalk walk_frame(const uint8_t* f, uint32_t avail, DecBlock* out_blocks, uint64_t src_base,
+                                uint64_t dst_base, uint32_t dst_cap, uint32_t frame) {
+    FrameWalk r = {S3HC_OK, 0, 0, 0, 0, 0, 0, 0};
+    if (avail < 4) { r.status = S3HC_CORRUPT; return r; }
+    const uint32_t magic = rd32(f);
+    if (magic == 0x184C2102u || (magic & 0xFFFFFFF0u) == 0x184D2A50u) { r.status = S3HC_UNSUPPORTED; return r; }
+    if (magic != kMagic || avail < 7) { r.status = S3HC_CORRUPT; return r; }
+    const uint32_t flg = f[4], bd = f[5];
+    uint32_t need = 7 + ((flg & 0x08) ? 8 : 0) + ((flg & 0x01) ? 4 : 0);
+    if (avail < need || (flg & 0xC0) != 0x40 || (flg & 0x02) || (bd & 0x8F)) { r.status = S3HC_CORRUPT; return r; }
+    const uint32_t code = (bd >> 4) & 7;
+    if (code < 4) { r.status = S3HC_CORRUPT; return r; }
+    const uint32_t bmax = 1u << (16 + 2 * (code - 4));
+    if (((xxh32_small(f + 4, need - 5) >> 8) & 0xFF) != f[need - 1]) { r.status = S3HC_CORRUPT; return r; }
+    if (flg & 0x01) { r.status = S3HC_UNSUPPORTED; return r; }
+    r.flg = flg;
+    r.bmax = bmax;
+    r.hdr = need;
+    if (flg & 0x08) r.content_lo = rd32(f + 6);
+    uint32_t ip = need;
+    uint32_t k = 0;
+    for (;;) {
+        if (avail - ip < 4) { r.status = S3HC_CORRUPT; return r; }
+        const uint32_t w = rd32(f + ip);
+        ip += 4;
+        if (w == 0) {
+            if (flg & 0x04) {
+                if (avail - ip < 4) { r.status = S3HC_CORRUPT; return r; }
+                r.want = rd32(f + ip);
+                ip += 4;
+            }
+            break;
+        }
+        const uint32_t len = w & 0x7FFFFFFFu;
+        if (len > bmax || avail - ip < len + ((flg & 0x10) ? 4u : 0u)) { r.status = S3HC_CORRUPT; return r; }
+        if (out_blocks) {
+            DecBlock D;
+            D.src_off = src_base + ip;
+            const uint64_t slot = (uint64_t)k * bmax;
+            D.dst_off = dst_base + slot;
+            D.csize = len;
+            D.limit = (w & kStoredBit) ? len : bmax;
+            const uint64_t room = slot < dst_cap ? dst_cap - slot : 0;
+            D.cap = room < D.limit ? (uint32_t)room : D.limit;
+            D.flags = ((w & kStoredBit) ? DB_STORED : 0u) | ((flg & 0x20) ? 0u : DB_LINKED);
+            D.frame = frame;
+            out_blocks[k] = D;
+        }
+        ip += len + ((flg & 0x10) ? 4u : 0u);
+        k++;
+    }
+    r.nblk = k;
+    r.end = ip;
+    return r;
+}
+
+// Block slots per frame are bounded by dst_cap/64KiB + 2 (planner capacity); a frame with
+// more blocks than that cannot land contiguously anyway and is reported UNSUPPORTED.
+__global__ void k_dframe_count(const uint8_t* __restrict__ src, const uint64_t* __restrict__ frame_off,
+                               const uint32_t* __restrict__ frame_len, const uint32_t* __restrict__ dst_cap,
+                               uint32_t nframes, uint32_t* __restrict__ nblk, int32_t* __restrict__ fstatus) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    FrameWalk r = walk_frame(src + frame_off[f], frame_len[f], nullptr, 0, 0, 0, f);
+    if (r.status == S3HC_OK && r.end != frame_len[f]) r.status = S3HC_CORRUPT;  // one frame per entry
+    if (r.status == S3HC_OK && r.nblk > dst_cap[f] / 65536u + 2u) r.status = S3HC_UNSUPPORTED;
+    nblk[f] = r.status == S3HC_OK ? r.nblk : 0u;
+    fstatus[f] = r.status;
+}
+
+__global__ void k_dframe_fill(const uint8_t* __restrict__ src, const uint64_t* __restrict__ frame_off,
+                              const uint32_t* __restrict__ frame_len, uint32_t nframes,
+                              const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+                              const uint64_t* __restrict__ blk_base, const int32_t* __restrict__ fstatus,
+                              DecBlock* __restrict__ blocks, DecUnit* __restrict__ units,
+                              uint32_t* __restrict__ fwant) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    if (fstatus[f] != S3HC_OK) return;
+    const uint32_t b0 = (uint32_t)blk_base[f];
+    FrameWalk r = walk_frame(src + frame_off[f], frame_len[f], blocks + b0, frame_off[f], dst_off[f], dst_cap[f], f);
+    fwant[f] = r.want;
+    const bool linked = !(r.flg & 0x20);
+    for (uint32_t k = 0; k < r.nblk; ++k) {
+        DecUnit U;
+        if (linked) { U.first = b0; U.n = k == 0 ? r.nblk : 0; }
+        else { U.first = b0 + k; U.n = 1; }
+        units[b0 + k] = U;
+    }
+}
+
+// Per frame after block decode: status, decoded length, contiguity, checksum range.
+__global__ void k_dframe_finish(const uint64_t* __restrict__ blk_base, uint32_t nframes,
+                                const uint32_t* __restrict__ nblk, const DecBlock* __restrict__ blocks,
+                                const uint32_t* __restrict__ blk_out, const int32_t* __restrict__ blk_status,
+                                int32_t* __restrict__ fstatus, uint32_t* __restrict__ out_len) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    int st = fstatus[f];
+    uint64_t tot = 0;
+    if (st == S3HC_OK) {
+        const uint32_t b0 = (uint32_t)blk_base[f], nb = nblk[f];
+        for (uint32_t k = 0; k < nb; ++k) {
+            const int bs = blk_status[b0 + k];
+            if (bs != S3HC_OK) { st = bs; break; }
+            const DecBlock D = blocks[b0 + k];
+            // independent blocks decode into slots k*bmax; all but the last must be full
+            if (!(D.flags & DB_LINKED) && k + 1 < nb && blk_out[b0 + k] != D.limit) { st = S3HC_UNSUPPORTED; break; }
+            tot += blk_out[b0 + k];
+        }
+    }
+    fstatus[f] = st;
+    out_len[f] = st == S3HC_OK ? (uint32_t)tot : 0u;
+}
+
+__global__ void k_dframe_verify(const uint8_t* __restrict__ src, const uint64_t* __restrict__ frame_off,
+                                uint32_t nframes, const uint32_t* __restrict__ fwant,
+                                const uint32_t* __restrict__ got_hash, const uint32_t* __restrict__ out_len,
+                                int32_t* __restrict__ fstatus) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    if (fstatus[f] != S3HC_OK) return;
+    const uint8_t* fp = src + frame_off[f];
+    const uint32_t flg = fp[4];
+    if ((flg & 0x08) && rd32(fp + 6) != out_len[f]) { fstatus[f] = S3HC_CORRUPT; return; }
+    if ((flg & 0x04) && got_hash[f] != fwant[f]) fstatus[f] = S3HC_CHECKSUM;
+}
+
+}  // namespace s3hc
+
+// ================================================================ launchers
+// Host-side wrappers so the runtime (s3hc_runtime.cpp) never needs the kernel symbols.
+namespace s3hc {
+static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+hipError_t launch_xxh32(const uint8_t* base, const uint64_t* off, const uint32_t* len, uint32_t n, uint32_t* out,
+                        hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_xxh32_ranges, dim3(cdiv((uint64_t)n * 4, 256)), dim3(256), 0, st, base, off, len, n, out);
+    return hipGetLastError();
+}
+hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
+                               uint32_t nunits, uint32_t* blk_out, int32_t* blk_status, hipStream_t st) {
+    if (!nunits) return hipSuccess;
+    hipLaunchKernelGGL(k_decode_units, dim3(cdiv(nunits, dec::kWaves)), dim3(64 * dec::kWaves), 0, st, src, dst, blk,
+                       units, nunits, blk_out, blk_status);
+    return hipGetLastError();
+}
+hipError_t launch_enc_parse(const uint8_t* src, const EncBlock* blocks, const uint32_t* seg_block, uint32_t nseg,
+                            uint2* recs, SegSummary* summ, hipStream_t st) {
+    if (!nseg) return hipSuccess;
+    hipLaunchKernelGGL(k_enc_parse, dim3(cdiv(nseg, enc::kWaves)), dim3(64 * enc::kWaves), 0, st, src, blocks,
+                       seg_block, nseg, recs, summ);
+    return hipGetLastError();
+}
+hipError_t launch_enc_sizes(const EncBlock* blocks, uint32_t nblocks, const SegSummary* summ, SegPlace* place,
+                            uint32_t* blk_payload, uint32_t* blk_size, uint32_t* blk_carry, hipStream_t st) {
+    if (!nblocks) return hipSuccess;
+    hipLaunchKernelGGL(k_enc_sizes, dim3(cdiv(nblocks, 256)), dim3(256), 0, st, blocks, nblocks, summ, place,
+                       blk_payload, blk_size, blk_carry);
+    return hipGetLastError();
+}
+hipError_t launch_scan(const uint32_t* in, uint32_t n, uint64_t* out, uint64_t* total, hipStream_t st) {
+    hipLaunchKernelGGL(k_scan_u32_u64, dim3(1), dim3(1024), 0, st, in, n, out, total);
+    return hipGetLastError();
+}
+hipError_t launch_enc_emit(const uint8_t* src, const EncBlock* blocks, const uint32_t* seg_block, uint32_t nseg,
+                           const uint2* recs, const SegSummary* summ, const SegPlace* place,
+                           const uint32_t* blk_payload, const uint32_t* blk_carry, const uint64_t* blk_off,
+                           const uint32_t* frame_hash, uint8_t* dst, hipStream_t st) {
+    if (!nseg) return hipSuccess;
+    hipLaunchKernelGGL(k_enc_emit, dim3(cdiv(nseg, 2)), dim3(128), 0, st, src, blocks, seg_block, nseg, recs, summ,
+                       place, blk_payload, blk_carry, blk_off, frame_hash, dst);
+    return hipGetLastError();
+}
+hipError_t launch_enc_groups(const uint32_t* g_blk0, const uint32_t* g_nblk, uint32_t ng, const uint64_t* blk_off,
+                             const uint32_t* blk_size, uint64_t* g_off, uint32_t* g_len, hipStream_t st) {
+    if (!ng) return hipSuccess;
+    hipLaunchKernelGGL(k_enc_frames, dim3(cdiv(ng, 256)), dim3(256), 0, st, g_blk0, g_nblk, ng, blk_off, blk_size,
+                       g_off, g_len);
+    return hipGetLastError();
+}
+hipError_t launch_dframe_count(const uint8_t* src, const uint64_t* frame_off, const uint32_t* frame_len,
+                               const uint32_t* dst_cap, uint32_t n, uint32_t* nblk, int32_t* fstatus,
+                               hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_dframe_count, dim3(cdiv(n, 256)), dim3(256), 0, st, src, frame_off, frame_len, dst_cap, n,
+                       nblk, fstatus);
+    return hipGetLastError();
+}
+hipError_t launch_dframe_fill(const uint8_t* src, const uint64_t* frame_off, const uint32_t* frame_len, uint32_t n,
+                              const uint64_t* dst_off, const uint32_t* dst_cap, const uint64_t* blk_base,
+                              const int32_t* fstatus, DecBlock* blocks, DecUnit* units, uint32_t* fwant,
+                              hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_dframe_fill, dim3(cdiv(n, 256)), dim3(256), 0, st, src, frame_off, frame_len, n, dst_off,
+                       dst_cap, blk_base, fstatus, blocks, units, fwant);
+    return hipGetLastError();
+}
+hipError_t launch_dframe_finish(const uint64_t* blk_base, uint32_t n, const uint32_t* nblk, const DecBlock* blocks,
+                                const uint32_t* blk_out, const int32_t* blk_status, int32_t* fstatus,
+                                uint32_t* out_len, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_dframe_finish, dim3(cdiv(n, 256)), dim3(256), 0, st, blk_base, n, nblk, blocks, blk_out,
+                       blk_status, fstatus, out_len);
+    return hipGetLastError();
+}
+hipError_t launch_dframe_verify(const uint8_t* src, const uint64_t* frame_off, uint32_t n, const uint32_t* fwant,
+                                const uint32_t* got, const uint32_t* out_len, int32_t* fstatus, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_dframe_verify, dim3(cdiv(n, 256)), dim3(256), 0, st, src, frame_off, n, fwant, got, out_len,
+                       fstatus);
+    return hipGetLastError();
+}
+}  // namespace s3hc

@@ -1,0 +1,76 @@
+// s3hc_plan.hpp — descriptors shared by the host planner and the CDNA4 kernels.
+//
+// The GPU engine works on three granularities:
+//   frame   — one LZ4 frame (magic, FLG, BD, HC, blocks, EndMark, xxh32 content checksum)
+//   block   — one LZ4 block inside a frame (<= 64 KiB, 256 KiB or 4 MiB, frame BD decides)
+//   segment — kSeg input bytes of one block; the unit of parallel match finding on encode
+#pragma once
+#include <stdint.h>
+
+namespace s3hc {
+
+constexpr uint32_t kMagic = 0x184D2204u;         // compression.rs:50 LZ4F_MAGIC_NUMBER
+constexpr uint32_t kStoredBit = 0x80000000u;     // compression.rs:47 BLOCK_UNCOMPRESSED_SIZE_BIT
+constexpr uint32_t kStoreModeBlock = 4u << 20;   // compression.rs:42 STORE_MODE_MAX_BLOCK_SIZE
+constexpr uint8_t kFlgIndependentChecksum = 0x64;  // version 01 | independent | content checksum
+
+// ---- encode -------------------------------------------------------------
+constexpr uint32_t kSeg = 4096;          // bytes of input per match-finding wave
+constexpr uint32_t kPrewarm = 4096;      // bytes before a segment inserted into its hash table
+constexpr uint32_t kHashLog = 11;        // per-wave hash table: 2^11 x u16 positions
+constexpr uint32_t kMaxSeqPerSeg = kSeg / 4 + 1;
+
+enum : uint32_t {
+    EB_STORE = 1,        // write this block stored (store-mode frame or caller decision)
+    EB_FIRST = 2,        // first block of its frame: frame header precedes it
+    EB_LAST = 4,         // last block of its frame: EndMark + content checksum follow it
+    EB_EMPTY = 8,        // zero-length frame: header + EndMark + checksum only, no block
+};
+
+struct EncBlock {        // 40 bytes
+    uint64_t src_off;    // input byte offset of this block
+    uint32_t len;        // input bytes (<= block max of the frame)
+    uint32_t seg0;       // first segment index
+    uint32_t nseg;       // segments covering the block (>= 1)
+    uint32_t frame;      // owning frame
+    uint32_t flags;      // EB_*
+    uint8_t  bd;         // frame BD byte (written in the header when EB_FIRST)
+    uint8_t  hc;         // frame header checksum byte
+    uint8_t  pad[6];
+};
+
+struct SegSummary {      // written by k_enc_parse, read by k_enc_sizes / k_enc_emit
+    uint32_t nseq;       // sequences (matches) found in the segment
+    uint32_t ll0;        // literal bytes of the first sequence that lie inside the segment
+    uint32_t body;       // encoded bytes of all sequences minus the first token/literal-length run
+    uint32_t trail;      // literal bytes after the last match (carried into the next segment)
+};
+
+struct SegPlace {        // written by k_enc_sizes
+    uint32_t out_off;    // offset of this segment's first byte inside the block payload
+    uint32_t carry;      // literal bytes carried in from earlier segments (nseq > 0 only)
+};
+
+// ---- decode -------------------------------------------------------------
+enum : uint32_t {
+    DB_STORED = 1,       // stored (uncompressed) block
+    DB_LINKED = 2,       // linked-block frame: matches may reach into earlier blocks of the unit
+};
+
+struct DecBlock {        // 40 bytes
+    uint64_t src_off;    // payload offset in the compressed stream
+    uint64_t dst_off;    // output offset (first block of a unit); later blocks follow contiguously
+    uint32_t csize;      // payload bytes
+    uint32_t limit;      // frame max block size (more decoded bytes = corrupt frame)
+    uint32_t cap;        // room in the caller's buffer at dst_off (more = DST_TOO_SMALL)
+    uint32_t flags;      // DB_*
+    uint32_t frame;      // owning frame
+    uint32_t pad;
+};
+
+struct DecUnit {         // a run of blocks decoded in order by one wave
+    uint32_t first;
+    uint32_t n;
+};
+
+}  // namespace s3hc

@@ -1,0 +1,880 @@
+// s3hc_runtime.cpp — host side of the MI355X LZ4 frame engine: the C ABI of
+// include/s3hc_lz4.h, the batch planner, and the frame walker for host buffers.
+//
+// Division of labour: the host plans (frame/block/segment layout,
+// header bytes, frame-structure walk of host buffers) and moves bytes; every per-byte
+// computation of the codec — LZ4 match finding and token emission, LZ4 block decode,
+// stored-block copies and every xxh32 content/block checksum — runs in the HIP kernels
+// of s3hc_kernels.hip. There is no CPU codec fallback.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "s3hc_lz4.h"
+#include "s3hc_plan.hpp"
+
+namespace s3hc {
+hipError_t launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*, hipStream_t);
+hipError_t launch_decode_units(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*,
+                               int32_t*, hipStream_t);
+hipError_t launch_enc_parse(const uint8_t*, const EncBlock*, const uint32_t*, uint32_t, uint2*, SegSummary*,
+                            hipStream_t);
+hipError_t launch_enc_sizes(const EncBlock*, uint32_t, const SegSummary*, SegPlace*, uint32_t*, uint32_t*,
+                            uint32_t*, hipStream_t);
+hipError_t launch_scan(const uint32_t*, uint32_t, uint64_t*, uint64_t*, hipStream_t);
+hipError_t launch_enc_emit(const uint8_t*, const EncBlock*, const uint32_t*, uint32_t, const uint2*,
+                           const SegSummary*, const SegPlace*, const uint32_t*, const uint32_t*, const uint64_t*,
+                           const uint32_t*, uint8_t*, hipStream_t);
+hipError_t launch_enc_groups(const uint32_t*, const uint32_t*, uint32_t, const uint64_t*, const uint32_t*,
+                             uint64_t*, uint32_t*, hipStream_t);
+hipError_t launch_dframe_count(const uint8_t*, const uint64_t*, const uint32_t*, const uint32_t*, uint32_t,
+                               uint32_t*, int32_t*, hipStream_t);
+hipError_t launch_dframe_fill(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, const uint64_t*,
+                              const uint32_t*, const uint64_t*, const int32_t*, DecBlock*, DecUnit*, uint32_t*,
+                              hipStream_t);
+hipError_t launch_dframe_finish(const uint64_t*, uint32_t, const uint32_t*, const DecBlock*, const uint32_t*,
+                                const int32_t*, int32_t*, uint32_t*, hipStream_t);
+hipError_t launch_dframe_verify(const uint8_t*, const uint64_t*, uint32_t, const uint32_t*, const uint32_t*,
+                                const uint32_t*, int32_t*, hipStream_t);
+}  // namespace s3hc
+
+using namespace s3hc;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIPCHK(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(S3HC_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));    \
+    } while (0)
+
+extern "C" const char* s3hc_last_error(void) { return g_err.c_str(); }
+extern "C" const char* s3hc_version(void) { return "s3hc-lz4 0.1.0 (gfx950)"; }
+
+// ------------------------------------------------------ frame-header xxh32
+// Only ever applied to frame-descriptor bytes (<= 14 bytes: FLG, BD, content size,
+// dictionary id) to form/check the one-byte header checksum (compression.rs:340-342).
+static uint32_t hdr_xxh32(const uint8_t* p, size_t n) {
+    const uint32_t P1 = 2654435761U, P2 = 2246822519U, P3 = 3266489917U, P4 = 668265263U, P5 = 374761393U;
+    auto rotl = [](uint32_t x, int r) { return (x << r) | (x >> (32 - r)); };
+    uint32_t h = P5 + (uint32_t)n;
+    size_t t = 0;
+    for (; t + 4 <= n; t += 4) {
+        uint32_t w = (uint32_t)p[t] | ((uint32_t)p[t + 1] << 8) | ((uint32_t)p[t + 2] << 16) | ((uint32_t)p[t + 3] << 24);
+        h += w * P3;
+        h = rotl(h, 17) * P4;
+    }
+    for (; t < n; ++t) {
+        h += p[t] * P5;
+        h = rotl(h, 11) * P1;
+    }
+    h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
+    return h;
+}
+static uint8_t header_hc(uint8_t bd) {
+    uint8_t fd[2] = {kFlgIndependentChecksum, bd};
+    return (uint8_t)(hdr_xxh32(fd, 2) >> 8);
+}
+static inline uint32_t rd32h(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// ------------------------------------------------------------ device memory
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        size_t want = std::max<size_t>(n, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    template <class T> T* as() const { return (T*)p; }
+};
+
+template <class T> static hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t st) {
+    hipError_t e = b.ensure(v.size() * sizeof(T) + 16);
+    if (e != hipSuccess || v.empty()) return e;
+    return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st);
+}
+
+// --------------------------------------------------------------- context
+struct s3hc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    bool timing = false;
+    std::map<std::string, float> kernel_ms;
+    // scratch for host-buffer calls
+    DevBuf d_in, d_out;
+    s3hc_plan* host_plan = nullptr;
+    DevBuf d_blocks, d_units, d_blk_out, d_blk_status, d_rng_off, d_rng_len, d_hash;
+    ~s3hc_ctx();
+};
+
+// Per-kernel event timing (enabled by s3hc_set_timing; used by bench.py for roofline).
+struct KTimer {
+    s3hc_ctx* ctx;
+    hipStream_t st;
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> ev;
+    explicit KTimer(s3hc_ctx* c, hipStream_t s) : ctx(c), st(s) {}
+    void begin(const char* name) {
+        if (!ctx->timing) return;
+        hipEvent_t a, b;
+        (void)hipEventCreate(&a);
+        (void)hipEventCreate(&b);
+        (void)hipEventRecord(a, st);
+        ev.push_back({name, {a, b}});
+    }
+    void end() {
+        if (!ctx->timing || ev.empty()) return;
+        (void)hipEventRecord(ev.back().second.second, st);
+    }
+    ~KTimer() {
+        if (ev.empty()) return;
+        (void)hipEventSynchronize(ev.back().second.second);
+        std::map<std::string, float> acc;
+        for (auto& e : ev) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, e.second.first, e.second.second);
+            acc[e.first] += ms;
+            (void)hipEventDestroy(e.second.first);
+            (void)hipEventDestroy(e.second.second);
+        }
+        ctx->kernel_ms = acc;
+    }
+};
+
+// ------------------------------------------------------------------ plans
+struct s3hc_plan {
+    bool is_encode = true;
+    // ---- encode
+    std::vector<EncBlock> blocks;
+    std::vector<uint32_t> seg_block;
+    std::vector<uint32_t> frame_blk0, frame_nblk;
+    std::vector<uint64_t> frame_src_off;
+    std::vector<uint32_t> frame_src_len;
+    std::vector<uint32_t> item_blk0, item_nblk;
+    uint64_t dst_bound = 0;
+    DevBuf d_blocks, d_seg_block, d_frame_src_off, d_frame_src_len, d_item_blk0, d_item_nblk;
+    DevBuf d_recs, d_summ, d_place, d_blk_payload, d_blk_size, d_blk_carry, d_blk_off, d_frame_hash, d_total;
+    // ---- decode
+    uint32_t nframes = 0;
+    uint32_t blk_cap = 0;
+    DevBuf d_frame_off, d_frame_len, d_dst_off, d_dst_cap;
+    DevBuf d_nblk, d_fstatus, d_blk_base, d_fwant, d_dblocks, d_units, d_blk_out, d_blk_status, d_got;
+};
+
+s3hc_ctx::~s3hc_ctx() {
+    delete host_plan;
+    if (stream) (void)hipStreamDestroy(stream);
+}
+
+// Frame layout of one item (lz4_flex FrameEncoder Auto / 64K-per-frame / store mode).
+static void plan_item(s3hc_plan* P, uint64_t off, uint64_t len, int mode, int policy) {
+    P->item_blk0.push_back((uint32_t)P->blocks.size());
+    auto add_frame = [&](uint64_t foff, uint64_t flen, uint8_t bd, uint64_t bmax, bool store) {
+        const uint32_t f = (uint32_t)P->frame_blk0.size();
+        P->frame_blk0.push_back((uint32_t)P->blocks.size());
+        P->frame_src_off.push_back(foff);
+        P->frame_src_len.push_back((uint32_t)flen);
+        const uint8_t hc = header_hc(bd);
+        uint32_t nb = 0;
+        if (flen == 0) {
+            EncBlock B{};
+            B.src_off = foff;
+            B.len = 0;
+            B.seg0 = (uint32_t)P->seg_block.size();
+            B.nseg = 1;
+            B.frame = f;
+            B.flags = EB_FIRST | EB_LAST | EB_EMPTY;
+            B.bd = bd;
+            B.hc = hc;
+            P->seg_block.push_back((uint32_t)P->blocks.size());
+            P->blocks.push_back(B);
+            P->dst_bound += 15;
+            nb = 1;
+        } else {
+            for (uint64_t o = 0; o < flen; o += bmax, ++nb) {
+                EncBlock B{};
+                B.src_off = foff + o;
+                B.len = (uint32_t)std::min<uint64_t>(bmax, flen - o);
+                B.seg0 = (uint32_t)P->seg_block.size();
+                B.nseg = (B.len + kSeg - 1) / kSeg;
+                B.frame = f;
+                B.flags = (o == 0 ? EB_FIRST : 0u) | (o + bmax >= flen ? EB_LAST : 0u) | (store ? EB_STORE : 0u);
+                B.bd = bd;
+                B.hc = hc;
+                for (uint32_t s = 0; s < B.nseg; ++s) P->seg_block.push_back((uint32_t)P->blocks.size());
+                P->blocks.push_back(B);
+                P->dst_bound += 4 + B.len;
+            }
+            P->dst_bound += 15;
+        }
+        P->frame_nblk.push_back(nb);
+    };
+    if (mode == 1) {  // store-mode frame: BD 0x70, stored blocks <= 4 MiB (compression.rs:326-368)
+        add_frame(off, len, 0x70, kStoreModeBlock, true);
+    } else if (policy == S3HC_BLK_64K_PER_FRAME) {
+        if (len == 0) add_frame(off, 0, 0x40, 65536, false);
+        for (uint64_t o = 0; o < len; o += 65536) add_frame(off + o, std::min<uint64_t>(65536, len - o), 0x40, 65536, false);
+    } else {  // BlockSize::from_buf_length
+        const uint8_t bd = len <= 65536 ? 0x40 : (len <= 262144 ? 0x50 : 0x70);
+        const uint64_t bmax = len <= 65536 ? 65536 : (len <= 262144 ? 262144 : (4u << 20));
+        add_frame(off, len, bd, bmax, false);
+    }
+    P->item_nblk.push_back((uint32_t)P->blocks.size() - P->item_blk0.back());
+}
+
+static int plan_upload_encode(s3hc_plan* P, hipStream_t st) {
+    const size_t nseg = P->seg_block.size(), nb = P->blocks.size(), nf = P->frame_blk0.size();
+    HIPCHK(upload(P->d_blocks, P->blocks, st));
+    HIPCHK(upload(P->d_seg_block, P->seg_block, st));
+    HIPCHK(upload(P->d_frame_src_off, P->frame_src_off, st));
+    HIPCHK(upload(P->d_frame_src_len, P->frame_src_len, st));
+    HIPCHK(upload(P->d_item_blk0, P->item_blk0, st));
+    HIPCHK(upload(P->d_item_nblk, P->item_nblk, st));
+    HIPCHK(P->d_recs.ensure(nseg * kMaxSeqPerSeg * sizeof(uint2)));
+    HIPCHK(P->d_summ.ensure(nseg * sizeof(SegSummary)));
+    HIPCHK(P->d_place.ensure(nseg * sizeof(SegPlace)));
+    HIPCHK(P->d_blk_payload.ensure(nb * 4));
+    HIPCHK(P->d_blk_size.ensure(nb * 4));
+    HIPCHK(P->d_blk_carry.ensure(nb * 4));
+    HIPCHK(P->d_blk_off.ensure(nb * 8));
+    HIPCHK(P->d_frame_hash.ensure(nf * 4));
+    HIPCHK(P->d_total.ensure(8));
+    return S3HC_OK;
+}
+
+static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t* d_dst, uint64_t* d_item_off,
+                      uint32_t* d_item_len, hipStream_t st) {
+    const uint32_t nseg = (uint32_t)P->seg_block.size(), nb = (uint32_t)P->blocks.size();
+    const uint32_t nf = (uint32_t)P->frame_blk0.size(), ni = (uint32_t)P->item_blk0.size();
+    KTimer T(ctx, st);
+    T.begin("xxh32");
+    HIPCHK(launch_xxh32(d_src, P->d_frame_src_off.as<uint64_t>(), P->d_frame_src_len.as<uint32_t>(), nf,
+                        P->d_frame_hash.as<uint32_t>(), st));
+    T.end();
+    T.begin("enc_parse");
+    HIPCHK(launch_enc_parse(d_src, P->d_blocks.as<EncBlock>(), P->d_seg_block.as<uint32_t>(), nseg,
+                            P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), st));
+    T.end();
+    T.begin("enc_sizes");
+    HIPCHK(launch_enc_sizes(P->d_blocks.as<EncBlock>(), nb, P->d_summ.as<SegSummary>(), P->d_place.as<SegPlace>(),
+                            P->d_blk_payload.as<uint32_t>(), P->d_blk_size.as<uint32_t>(),
+                            P->d_blk_carry.as<uint32_t>(), st));
+    HIPCHK(launch_scan(P->d_blk_size.as<uint32_t>(), nb, P->d_blk_off.as<uint64_t>(), P->d_total.as<uint64_t>(), st));
+    T.end();
+    T.begin("enc_emit");
+    HIPCHK(launch_enc_emit(d_src, P->d_blocks.as<EncBlock>(), P->d_seg_block.as<uint32_t>(), nseg,
+                           P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), P->d_place.as<SegPlace>(),
+                           P->d_blk_payload.as<uint32_t>(), P->d_blk_carry.as<uint32_t>(),
+                           P->d_blk_off.as<uint64_t>(), P->d_frame_hash.as<uint32_t>(), d_dst, st));
+    HIPCHK(launch_enc_groups(P->d_item_blk0.as<uint32_t>(), P->d_item_nblk.as<uint32_t>(), ni,
+                             P->d_blk_off.as<uint64_t>(), P->d_blk_size.as<uint32_t>(), d_item_off, d_item_len, st));
+    T.end();
+    return S3HC_OK;
+}
+
+// ------------------------------------------------------------ C ABI: ctx
+extern "C" int s3hc_create(s3hc_ctx** out, int device) {
+    if (!out) return fail(S3HC_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return fail(S3HC_DEVICE, "no HIP device available (the engine has no CPU path)");
+    if (device < 0 || device >= n) return fail(S3HC_INVALID_ARG, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    std::unique_ptr<s3hc_ctx> c(new s3hc_ctx);
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    *out = c.release();
+    return S3HC_OK;
+}
+extern "C" void s3hc_destroy(s3hc_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    delete ctx;
+}
+extern "C" void s3hc_set_timing(s3hc_ctx* ctx, int enabled) { if (ctx) ctx->timing = enabled != 0; }
+extern "C" float s3hc_last_kernel_ms(const s3hc_ctx* ctx, const char* name) {
+    if (!ctx || !name) return -1.f;
+    auto it = ctx->kernel_ms.find(name);
+    return it == ctx->kernel_ms.end() ? -1.f : it->second;
+}
+
+extern "C" size_t s3hc_frame_bound(size_t n) {
+    // 64 KiB frames (header 7 + word 4 + trailer 8 per 64 KiB) bound every layout we write.
+    return n + 19 * (n / 65536 + 1) + 16;
+}
+
+// ------------------------------------------------------ C ABI: batch encode
+extern "C" int s3hc_plan_encode(s3hc_ctx* ctx, const uint64_t* src_off, const uint32_t* len, const uint8_t* mode,
+                                uint32_t n, s3hc_plan** out) {
+    if (!ctx || !out || (n && (!src_off || !len))) return fail(S3HC_INVALID_ARG, "bad arguments");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    std::unique_ptr<s3hc_plan> P(new s3hc_plan);
+    for (uint32_t i = 0; i < n; ++i) plan_item(P.get(), src_off[i], len[i], mode ? mode[i] : 0, S3HC_BLK_AUTO_LZ4FLEX);
+    int rc = plan_upload_encode(P.get(), ctx->stream);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *out = P.release();
+    return S3HC_OK;
+}
+extern "C" uint64_t s3hc_plan_dst_bound(const s3hc_plan* P) { return P ? P->dst_bound : 0; }
+extern "C" void s3hc_plan_free(s3hc_plan* P) { delete P; }
+
+extern "C" int s3hc_encode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t* d_dst, uint64_t dst_cap,
+                               uint64_t* d_item_off, uint32_t* d_item_len, void* stream) {
+    if (!ctx || !P || !P->is_encode || !d_item_off || !d_item_len) return fail(S3HC_INVALID_ARG, "bad arguments");
+    if (dst_cap < P->dst_bound) return fail(S3HC_DST_TOO_SMALL, "dst_cap < s3hc_plan_dst_bound(plan)");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    return run_encode(ctx, P, d_src, d_dst, d_item_off, d_item_len, st);
+}
+
+// ------------------------------------------------------ C ABI: batch decode
+extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const uint32_t* frame_len,
+                                const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t n, s3hc_plan** out) {
+    if (!ctx || !out || (n && (!frame_off || !frame_len || !dst_off || !dst_cap)))
+        return fail(S3HC_INVALID_ARG, "bad arguments");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    std::unique_ptr<s3hc_plan> P(new s3hc_plan);
+    P->is_encode = false;
+    P->nframes = n;
+    uint64_t cap = 0;
+    for (uint32_t i = 0; i < n; ++i) cap += dst_cap[i] / 65536u + 2u;
+    if (cap > 0xFFFFFFF0ull) return fail(S3HC_INVALID_ARG, "batch too large");
+    P->blk_cap = (uint32_t)cap;
+    hipStream_t st = ctx->stream;
+    std::vector<uint64_t> fo(frame_off, frame_off + n), d(dst_off, dst_off + n);
+    std::vector<uint32_t> fl(frame_len, frame_len + n), dc(dst_cap, dst_cap + n);
+    HIPCHK(upload(P->d_frame_off, fo, st));
+    HIPCHK(upload(P->d_frame_len, fl, st));
+    HIPCHK(upload(P->d_dst_off, d, st));
+    HIPCHK(upload(P->d_dst_cap, dc, st));
+    HIPCHK(P->d_nblk.ensure(n * 4 + 16));
+    HIPCHK(P->d_fstatus.ensure(n * 4 + 16));
+    HIPCHK(P->d_blk_base.ensure(n * 8 + 16));
+    HIPCHK(P->d_fwant.ensure(n * 4 + 16));
+    HIPCHK(P->d_got.ensure(n * 4 + 16));
+    HIPCHK(P->d_total.ensure(16));
+    HIPCHK(P->d_dblocks.ensure((size_t)P->blk_cap * sizeof(DecBlock) + 16));
+    HIPCHK(P->d_units.ensure((size_t)P->blk_cap * sizeof(DecUnit) + 16));
+    HIPCHK(P->d_blk_out.ensure((size_t)P->blk_cap * 4 + 16));
+    HIPCHK(P->d_blk_status.ensure((size_t)P->blk_cap * 4 + 16));
+    HIPCHK(hipStreamSynchronize(st));
+    *out = P.release();
+    return S3HC_OK;
+}
+
+extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t* d_dst, uint32_t* d_out_len,
+                               int32_t* d_status, void* stream) {
+    if (!ctx || !P || P->is_encode || !d_out_len || !d_status) return fail(S3HC_INVALID_ARG, "bad arguments");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+    const uint32_t n = P->nframes;
+    if (!n) return S3HC_OK;
+    KTimer T(ctx, st);
+    T.begin("dec_plan");
+    HIPCHK(launch_dframe_count(d_src, P->d_frame_off.as<uint64_t>(), P->d_frame_len.as<uint32_t>(),
+                               P->d_dst_cap.as<uint32_t>(), n, P->d_nblk.as<uint32_t>(), d_status, st));
+    HIPCHK(launch_scan(P->d_nblk.as<uint32_t>(), n, P->d_blk_base.as<uint64_t>(), P->d_total.as<uint64_t>(), st));
+    HIPCHK(hipMemsetAsync(P->d_units.p, 0, (size_t)P->blk_cap * sizeof(DecUnit), st));
+    HIPCHK(launch_dframe_fill(d_src, P->d_frame_off.as<uint64_t>(), P->d_frame_len.as<uint32_t>(), n,
+                              P->d_dst_off.as<uint64_t>(), P->d_dst_cap.as<uint32_t>(), P->d_blk_base.as<uint64_t>(),
+                              d_status, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(),
+                              P->d_fwant.as<uint32_t>(), st));
+    T.end();
+    T.begin("decode");
+    HIPCHK(launch_decode_units(d_src, d_dst, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(), P->blk_cap,
+                               P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st));
+    T.end();
+    T.begin("dec_finish");
+    HIPCHK(launch_dframe_finish(P->d_blk_base.as<uint64_t>(), n, P->d_nblk.as<uint32_t>(), P->d_dblocks.as<DecBlock>(),
+                                P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), d_status, d_out_len, st));
+    T.end();
+    T.begin("xxh32");
+    HIPCHK(launch_xxh32(d_dst, P->d_dst_off.as<uint64_t>(), d_out_len, n, P->d_got.as<uint32_t>(), st));
+    T.end();
+    T.begin("dec_finish");
+    HIPCHK(launch_dframe_verify(d_src, P->d_frame_off.as<uint64_t>(), n, P->d_fwant.as<uint32_t>(),
+                                P->d_got.as<uint32_t>(), d_out_len, d_status, st));
+    T.end();
+    return S3HC_OK;
+}
+
+// ------------------------------------------------- C ABI: host-buffer encode
+static int host_encode(s3hc_ctx* ctx, const uint8_t* src, size_t n, int mode, int policy, uint8_t* dst, size_t cap,
+                       size_t* out_len) {
+    if (!ctx || (!src && n) || !out_len) return fail(S3HC_INVALID_ARG, "bad arguments");
+    if (n > 0xFFFFFFFFull * 16) return fail(S3HC_INVALID_ARG, "input too large");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    s3hc_plan* P = new s3hc_plan;
+    // items of <= 4 GiB (u32 lengths); each item is one frame (Auto) or 64 KiB frames
+    const uint64_t item_max = (mode == 1 || policy == S3HC_BLK_64K_PER_FRAME) ? (1ull << 31) : (uint64_t)n;
+    if (n == 0) plan_item(P, 0, 0, mode, policy);
+    for (uint64_t o = 0; o < n; o += item_max) plan_item(P, o, std::min<uint64_t>(item_max, n - o), mode, policy);
+    if (mode != 1 && policy != S3HC_BLK_64K_PER_FRAME && n > 0xFFFFFFFFull) {
+        delete P;
+        return fail(S3HC_INVALID_ARG, "single-frame input above 4 GiB");
+    }
+    std::unique_ptr<s3hc_plan> guard(P);
+    if (cap < P->dst_bound) return fail(S3HC_DST_TOO_SMALL, "dst capacity below frame bound");
+    int rc = plan_upload_encode(P, st);
+    if (rc) return rc;
+    HIPCHK(ctx->d_in.ensure(n + 64));
+    HIPCHK(ctx->d_out.ensure(P->dst_bound + 64));
+    DevBuf d_io, d_il;
+    const size_t ni = P->item_blk0.size();
+    HIPCHK(d_io.ensure(ni * 8));
+    HIPCHK(d_il.ensure(ni * 4));
+    if (n) HIPCHK(hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
+    rc = run_encode(ctx, P, ctx->d_in.as<uint8_t>(), ctx->d_out.as<uint8_t>(), d_io.as<uint64_t>(),
+                    d_il.as<uint32_t>(), st);
+    if (rc) return rc;
+    uint64_t total = 0;
+    HIPCHK(hipMemcpyAsync(&total, P->d_total.p, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (total > cap) return fail(S3HC_DST_TOO_SMALL, "dst capacity below encoded size");
+    HIPCHK(hipMemcpyAsync(dst, ctx->d_out.p, total, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *out_len = total;
+    return S3HC_OK;
+}
+
+extern "C" int s3hc_compress_frame(s3hc_ctx* ctx, const uint8_t* src, size_t n, int policy, uint8_t* dst, size_t cap,
+                                   size_t* out_len, int* was_compressed) {
+    if (policy != S3HC_BLK_AUTO_LZ4FLEX && policy != S3HC_BLK_64K_PER_FRAME) return fail(S3HC_INVALID_ARG, "policy");
+    int rc = host_encode(ctx, src, n, 0, policy, dst, cap, out_len);
+    if (was_compressed) *was_compressed = rc == S3HC_OK;
+    return rc;
+}
+
+extern "C" int s3hc_store_mode_frame(s3hc_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
+                                     size_t* out_len) {
+    return host_encode(ctx, src, n, 1, S3HC_BLK_AUTO_LZ4FLEX, dst, cap, out_len);
+}
+
+// --------------------------------------------- host-buffer frame walker
+// Structure of concatenated frames in a host buffer, in decompress_data order
+// (compression.rs:474-494). Mirrors lz4_flex FrameInfo::read / FrameDecoder::read_more.
+struct HFrame {
+    size_t pos;          // frame start in src
+    uint32_t flg, bmax;
+    uint32_t blk0, nblk;
+    uint64_t out_off;    // slot-layout output offset (device)
+    uint64_t content_size;
+    uint32_t want;       // content checksum
+};
+struct HWalk {
+    std::vector<HFrame> frames;
+    std::vector<DecBlock> blocks;
+    std::vector<uint32_t> blk_cs_want;  // block checksums (FLG 0x10)
+    std::vector<uint8_t> blk_has_cs;
+    int tail_status = S3HC_OK;   // structural error after the last complete frame
+    bool stopped_empty = false;  // a frame with no blocks ended the walk (Ok(0) => break)
+    size_t end = 0;              // bytes consumed by complete frames
+    uint64_t slot_total = 0;
+};
+
+static int parse_header_h(const uint8_t* p, size_t avail, uint32_t* flg, uint32_t* bmax, size_t* hdr, uint64_t* csize) {
+    if (avail < 4) return S3HC_CORRUPT;
+    uint32_t magic = rd32h(p);
+    if (magic == 0x184C2102u || (magic & 0xFFFFFFF0u) == 0x184D2A50u) return S3HC_UNSUPPORTED;
+    if (magic != kMagic || avail < 7) return S3HC_CORRUPT;
+    uint32_t f = p[4], bd = p[5];
+    size_t need = 7 + ((f & 0x08) ? 8 : 0) + ((f & 0x01) ? 4 : 0);
+    if (avail < need) return S3HC_CORRUPT;
+    if ((f & 0xC0) != 0x40 || (f & 0x02) || (bd & 0x8F)) return S3HC_CORRUPT;
+    uint32_t code = (bd >> 4) & 7;
+    if (code < 4) return S3HC_CORRUPT;
+    if ((uint8_t)(hdr_xxh32(p + 4, need - 5) >> 8) != p[need - 1]) return S3HC_CORRUPT;
+    if (f & 0x01) return S3HC_UNSUPPORTED;
+    *flg = f;
+    *bmax = 1u << (16 + 2 * (code - 4));
+    *hdr = need;
+    *csize = (f & 0x08) ? ((uint64_t)rd32h(p + 6) | ((uint64_t)rd32h(p + 10) << 32)) : 0;
+    return S3HC_OK;
+}
+
+// Walk frames from src; `stream_mode` = stream_range_data semantics (an incomplete final
+// frame is left for later instead of being an error; an empty frame does not stop).
+static void walk_frames(const uint8_t* src, size_t n, HWalk& W, bool allow_incomplete, bool stop_on_empty) {
+    const bool stream_mode = allow_incomplete;
+    size_t pos = 0;
+    while (pos < n) {
+        HFrame F{};
+        size_t hdr;
+        int rc = parse_header_h(src + pos, n - pos, &F.flg, &F.bmax, &hdr, &F.content_size);
+        if (rc) {
+            if (stream_mode && rc == S3HC_CORRUPT && n - pos < 19) break;  // maybe just incomplete
+            W.tail_status = rc;
+            return;
+        }
+        F.pos = pos;
+        F.blk0 = (uint32_t)W.blocks.size();
+        F.out_off = W.slot_total;
+        const bool linked = !(F.flg & 0x20);
+        size_t ip = pos + hdr;
+        uint64_t slot = 0;
+        int st = S3HC_OK;
+        bool complete = false;
+        std::vector<DecBlock> fb;
+        std::vector<uint32_t> fcs;
+        std::vector<uint8_t> fhas;
+        for (;;) {
+            if (n - ip < 4) { st = S3HC_CORRUPT; break; }
+            uint32_t w = rd32h(src + ip);
+            ip += 4;
+            if (w == 0) {
+                if (F.flg & 0x04) {
+                    if (n - ip < 4) { st = S3HC_CORRUPT; break; }
+                    F.want = rd32h(src + ip);
+                    ip += 4;
+                }
+                complete = true;
+                break;
+            }
+            uint32_t len = w & 0x7FFFFFFFu;
+            if (len > F.bmax) { st = S3HC_CORRUPT; break; }
+            size_t need = (size_t)len + ((F.flg & 0x10) ? 4 : 0);
+            if (n - ip < need) { st = S3HC_CORRUPT; break; }
+            DecBlock D{};
+            D.src_off = ip;
+            D.dst_off = F.out_off + slot;
+            D.csize = len;
+            D.limit = (w & kStoredBit) ? len : F.bmax;
+            D.cap = D.limit;
+            D.flags = ((w & kStoredBit) ? DB_STORED : 0u) | (linked ? DB_LINKED : 0u);
+            D.frame = (uint32_t)W.frames.size();
+            fb.push_back(D);
+            fhas.push_back((F.flg & 0x10) ? 1 : 0);
+            fcs.push_back((F.flg & 0x10) ? rd32h(src + ip + len) : 0);
+            slot += D.limit;
+            ip += need;
+        }
+        if (!complete) {
+            if (stream_mode && st == S3HC_CORRUPT) break;  // wait for more bytes
+            // Blocks before the failure still decode (their errors come first in order).
+            W.tail_status = st;
+        }
+        F.nblk = (uint32_t)fb.size();
+        W.blocks.insert(W.blocks.end(), fb.begin(), fb.end());
+        W.blk_cs_want.insert(W.blk_cs_want.end(), fcs.begin(), fcs.end());
+        W.blk_has_cs.insert(W.blk_has_cs.end(), fhas.begin(), fhas.end());
+        W.slot_total += slot;
+        W.frames.push_back(F);
+        if (!complete) return;
+        pos = ip;
+        W.end = pos;
+        if (F.nblk == 0 && stop_on_empty) {  // empty frame: read_to_end == Ok(0) => break
+            W.stopped_empty = true;
+            return;
+        }
+    }
+}
+
+extern "C" int s3hc_decompressed_bound(const uint8_t* src, size_t n, size_t* bound) {
+    if ((!src && n) || !bound) return fail(S3HC_INVALID_ARG, "bad arguments");
+    HWalk W;
+    walk_frames(src, n, W, false, true);
+    uint64_t b = 0;
+    for (auto& D : W.blocks) b += D.limit;
+    *bound = b;
+    return S3HC_OK;
+}
+
+// Decode the frames of W (already walked) from a host buffer; append decoded bytes to
+// `out` (host) in frame order. Applies the decompress_data loop rules unless stream_mode.
+// Returns the first error in frame order (or W.tail_status).
+static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bool stream_mode,
+                       std::vector<uint8_t>* vout, uint8_t* dst, size_t cap, size_t* out_len) {
+    hipStream_t st = ctx->stream;
+    const size_t nb = W.blocks.size(), nf = W.frames.size();
+    std::vector<uint32_t> bo(nb), cs_got(nb);
+    std::vector<int32_t> bs(nb);
+    if (nb) {
+        HIPCHK(ctx->d_in.ensure(n + 64));
+        HIPCHK(hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
+        HIPCHK(ctx->d_out.ensure(W.slot_total + 64));
+        std::vector<DecUnit> units;
+        for (auto& F : W.frames) {
+            if (!F.nblk) continue;
+            if (!(F.flg & 0x20)) units.push_back(DecUnit{F.blk0, F.nblk});
+            else for (uint32_t k = 0; k < F.nblk; ++k) units.push_back(DecUnit{F.blk0 + k, 1});
+        }
+        HIPCHK(upload(ctx->d_blocks, W.blocks, st));
+        HIPCHK(upload(ctx->d_units, units, st));
+        HIPCHK(ctx->d_blk_out.ensure(nb * 4));
+        HIPCHK(ctx->d_blk_status.ensure(nb * 4));
+        HIPCHK(launch_decode_units(ctx->d_in.as<uint8_t>(), ctx->d_out.as<uint8_t>(), ctx->d_blocks.as<DecBlock>(),
+                                   ctx->d_units.as<DecUnit>(), (uint32_t)units.size(), ctx->d_blk_out.as<uint32_t>(),
+                                   ctx->d_blk_status.as<int32_t>(), st));
+        // block checksums (FLG bit 4) over the compressed payloads
+        bool any_cs = false;
+        for (auto h : W.blk_has_cs) any_cs |= h != 0;
+        if (any_cs) {
+            std::vector<uint64_t> ro(nb);
+            std::vector<uint32_t> rl(nb);
+            for (size_t i = 0; i < nb; ++i) { ro[i] = W.blocks[i].src_off; rl[i] = W.blocks[i].csize; }
+            HIPCHK(upload(ctx->d_rng_off, ro, st));
+            HIPCHK(upload(ctx->d_rng_len, rl, st));
+            HIPCHK(ctx->d_hash.ensure(nb * 4));
+            HIPCHK(launch_xxh32(ctx->d_in.as<uint8_t>(), ctx->d_rng_off.as<uint64_t>(), ctx->d_rng_len.as<uint32_t>(),
+                                (uint32_t)nb, ctx->d_hash.as<uint32_t>(), st));
+            HIPCHK(hipMemcpyAsync(cs_got.data(), ctx->d_hash.p, nb * 4, hipMemcpyDeviceToHost, st));
+        }
+        HIPCHK(hipMemcpyAsync(bo.data(), ctx->d_blk_out.p, nb * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(bs.data(), ctx->d_blk_status.p, nb * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    // Resolve frames in order (FrameDecoder reads frames sequentially): the first failure in
+    // stream order wins — a block's checksum/decode error, then at its EndMark the frame's
+    // content size and content checksum, then the next frame; a frame yielding 0 bytes ends
+    // the loop (Ok(0) => break) and nothing after it is looked at.
+    int err_status = S3HC_OK;
+    size_t use_frames = nf;    // frames whose output is delivered / checksummed
+    bool stopped = false;
+    std::vector<uint64_t> fout(nf, 0);
+    bool need_compact = false;
+    for (size_t f = 0; f < nf; ++f) {
+        const HFrame& F = W.frames[f];
+        uint64_t tot = 0;
+        int fs = S3HC_OK;
+        for (uint32_t k = 0; k < F.nblk; ++k) {
+            const uint32_t b = F.blk0 + k;
+            if (W.blk_has_cs[b] && cs_got[b] != W.blk_cs_want[b]) { fs = S3HC_CHECKSUM; break; }
+            if (bs[b] != S3HC_OK) { fs = bs[b]; break; }
+            if ((F.flg & 0x20) && k + 1 < F.nblk && bo[b] != W.blocks[b].limit) need_compact = true;
+            tot += bo[b];
+        }
+        if (fs == S3HC_OK && f + 1 == nf && W.tail_status != S3HC_OK) fs = W.tail_status;  // incomplete frame
+        if (fs != S3HC_OK) { err_status = fs; use_frames = f; break; }
+        fout[f] = tot;
+        if (!stream_mode && tot == 0) { use_frames = f + 1; stopped = true; break; }
+    }
+    if (err_status == S3HC_OK && !stopped && W.tail_status != S3HC_OK && nf == W.frames.size()) {
+        // a header-level failure after every walked frame (bad magic, truncated header, ...)
+        err_status = W.tail_status;
+    }
+    // Compact independent frames whose non-final blocks were short (rare) so each frame's
+    // output is contiguous before its content checksum is computed.
+    uint64_t total = 0;
+    for (size_t f = 0; f < use_frames; ++f) total += fout[f];
+    DevBuf compact;
+    const uint8_t* dev_out = ctx->d_out.as<uint8_t>();
+    std::vector<uint64_t> fpos(use_frames);
+    if (need_compact) {
+        HIPCHK(compact.ensure(total + 64));
+        uint64_t o = 0;
+        for (size_t f = 0; f < use_frames; ++f) {
+            const HFrame& F = W.frames[f];
+            fpos[f] = o;
+            const bool linked = !(F.flg & 0x20);
+            uint64_t lpos = F.out_off;  // linked units decode contiguously from the frame start
+            for (uint32_t k = 0; k < F.nblk; ++k) {
+                const uint32_t b = F.blk0 + k;
+                const uint64_t from = linked ? lpos : W.blocks[b].dst_off;
+                if (bo[b]) HIPCHK(hipMemcpyAsync(compact.as<uint8_t>() + o, dev_out + from, bo[b],
+                                                 hipMemcpyDeviceToDevice, st));
+                o += bo[b];
+                lpos += bo[b];
+            }
+        }
+        dev_out = compact.as<uint8_t>();
+    } else {
+        for (size_t f = 0; f < use_frames; ++f) fpos[f] = W.frames[f].out_off;
+    }
+    // EndMark checks of every delivered frame, in order: content size, content checksum (GPU xxh32)
+    {
+        std::vector<uint64_t> ro;
+        std::vector<uint32_t> rl;
+        std::vector<size_t> which;
+        for (size_t f = 0; f < use_frames; ++f) {
+            if (W.frames[f].flg & 0x04) {
+                ro.push_back(fpos[f]);
+                rl.push_back((uint32_t)fout[f]);
+                which.push_back(f);
+            }
+        }
+        std::vector<uint32_t> got(ro.size());
+        if (!ro.empty()) {
+            HIPCHK(upload(ctx->d_rng_off, ro, st));
+            HIPCHK(upload(ctx->d_rng_len, rl, st));
+            HIPCHK(ctx->d_hash.ensure(ro.size() * 4));
+            HIPCHK(launch_xxh32(dev_out, ctx->d_rng_off.as<uint64_t>(), ctx->d_rng_len.as<uint32_t>(),
+                                (uint32_t)ro.size(), ctx->d_hash.as<uint32_t>(), st));
+            HIPCHK(hipMemcpyAsync(got.data(), ctx->d_hash.p, ro.size() * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
+        size_t wi = 0;
+        for (size_t f = 0; f < use_frames; ++f) {
+            const HFrame& F = W.frames[f];
+            if ((F.flg & 0x08) && fout[f] != F.content_size) return fail(S3HC_CORRUPT, "content size mismatch");
+            if (F.flg & 0x04) {
+                if (got[wi] != F.want) return fail(S3HC_CHECKSUM, "content checksum mismatch");
+                wi++;
+            }
+        }
+    }
+    if (err_status != S3HC_OK) return fail(err_status, "frame decode failed");
+    // Deliver
+    uint8_t* hdst = dst;
+    if (vout) {
+        size_t o0 = vout->size();
+        vout->resize(o0 + total);
+        hdst = vout->data() + o0;
+    } else if (total > cap) {
+        *out_len = total;
+        return fail(S3HC_DST_TOO_SMALL, "dst capacity below decoded size");
+    }
+    uint64_t o = 0;
+    for (size_t f = 0; f < use_frames; ++f) {
+        if (fout[f]) HIPCHK(hipMemcpyAsync(hdst + o, dev_out + fpos[f], fout[f], hipMemcpyDeviceToHost, st));
+        o += fout[f];
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    if (out_len) *out_len = total;
+    return S3HC_OK;
+}
+
+extern "C" int s3hc_decompress_frames(s3hc_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
+                                      size_t* out_len) {
+    if (!ctx || (!src && n) || !out_len) return fail(S3HC_INVALID_ARG, "bad arguments");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    *out_len = 0;
+    HWalk W;
+    walk_frames(src, n, W, false, true);
+    return decode_walk(ctx, src, n, W, false, nullptr, dst, cap, out_len);
+}
+
+// ------------------------------------------------------ streaming decoder
+struct s3hc_stream {
+    s3hc_ctx* ctx;
+    std::vector<uint8_t> in;    // undecoded input (starts at a frame boundary)
+    std::vector<uint8_t> out;   // decoded, not yet read
+    size_t out_pos = 0;
+    bool finished = false;
+    int error = S3HC_OK;
+    uint64_t total = 0;
+};
+
+extern "C" int s3hc_stream_open(s3hc_ctx* ctx, s3hc_stream** out) {
+    if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
+    *out = new s3hc_stream{ctx};
+    return S3HC_OK;
+}
+extern "C" int s3hc_stream_feed(s3hc_stream* s, const uint8_t* src, size_t n) {
+    if (!s || (!src && n)) return fail(S3HC_INVALID_ARG, "bad arguments");
+    if (s->finished) return fail(S3HC_INVALID_ARG, "stream already finished");
+    s->in.insert(s->in.end(), src, src + n);
+    return S3HC_OK;
+}
+extern "C" int s3hc_stream_finish(s3hc_stream* s) {
+    if (!s) return fail(S3HC_INVALID_ARG, "bad arguments");
+    s->finished = true;
+    return S3HC_OK;
+}
+// Decode every complete frame buffered so far (stream_range_data: one FrameDecoder per frame).
+static int stream_pump(s3hc_stream* s) {
+    if (s->error) return s->error;
+    if (s->in.empty()) return S3HC_OK;
+    std::lock_guard<std::mutex> g(s->ctx->mu);
+    HIPCHK(hipSetDevice(s->ctx->device));
+    HWalk W;
+    walk_frames(s->in.data(), s->in.size(), W, !s->finished, false);
+    if (s->finished && W.tail_status == S3HC_OK && W.end != s->in.size() && W.frames.empty())
+        W.tail_status = S3HC_CORRUPT;
+    if (W.frames.empty() && W.tail_status == S3HC_OK) return S3HC_OK;
+    if (s->out_pos == s->out.size()) { s->out.clear(); s->out_pos = 0; }
+    size_t before = s->out.size();
+    int rc = decode_walk(s->ctx, s->in.data(), s->in.size(), W, true, &s->out, nullptr, 0, nullptr);
+    if (rc) {
+        s->out.resize(before);
+        s->error = rc;
+        return rc;
+    }
+    s->total += s->out.size() - before;
+    s->in.erase(s->in.begin(), s->in.begin() + W.end);
+    if (s->finished && !s->in.empty()) {  // trailing bytes that never formed a frame
+        s->error = S3HC_CORRUPT;
+        return fail(S3HC_CORRUPT, "truncated frame at end of stream");
+    }
+    return S3HC_OK;
+}
+extern "C" int s3hc_stream_read(s3hc_stream* s, uint8_t* dst, size_t cap, size_t* n) {
+    if (!s || !n || (!dst && cap)) return fail(S3HC_INVALID_ARG, "bad arguments");
+    *n = 0;
+    if (s->out_pos == s->out.size()) {
+        int rc = stream_pump(s);
+        if (rc) return rc;
+    }
+    size_t k = std::min(cap, s->out.size() - s->out_pos);
+    if (k) memcpy(dst, s->out.data() + s->out_pos, k);
+    s->out_pos += k;
+    *n = k;
+    return S3HC_OK;
+}
+extern "C" uint64_t s3hc_stream_total(const s3hc_stream* s) { return s ? s->total : 0; }
+extern "C" void s3hc_stream_close(s3hc_stream* s) { delete s; }
+
+// ----------------------------------------------- device memory plumbing
+// Thin helpers so callers (tests, bench) can stage device-resident batches without a
+// second HIP runtime in the process.
+extern "C" int s3hc_dev_alloc(s3hc_ctx* ctx, size_t n, void** out) {
+    if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMalloc(out, n ? n : 16));
+    return S3HC_OK;
+}
+extern "C" int s3hc_dev_free(s3hc_ctx* ctx, void* p) {
+    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    if (p) HIPCHK(hipFree(p));
+    return S3HC_OK;
+}
+// kind: 1 host->device, 2 device->host, 3 device->device. Synchronous w.r.t. the host.
+extern "C" int s3hc_memcpy(s3hc_ctx* ctx, void* dst, const void* src, size_t n, int kind) {
+    if (!ctx || kind < 1 || kind > 3) return fail(S3HC_INVALID_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    if (n) HIPCHK(hipMemcpyAsync(dst, src, n, k, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return S3HC_OK;
+}
+extern "C" int s3hc_memset(s3hc_ctx* ctx, void* dst, int v, size_t n) {
+    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    if (n) HIPCHK(hipMemsetAsync(dst, v, n, ctx->stream));
+    return S3HC_OK;
+}
+extern "C" int s3hc_sync(s3hc_ctx* ctx) {
+    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return S3HC_OK;
+}

@@ -1,0 +1,430 @@
+"""Python binding of libs3hc_lz4.so (the MI355X LZ4 frame engine) over its C ABI.
+
+Mirrors the reference's codec surface (src/compression.rs): ``CompressionHandler`` with
+``compress_with_metadata`` / ``compress_with_algorithm`` / ``decompress_data`` /
+``decompress_with_algorithm`` / ``encode_store_mode_frame`` / ``get_stats`` and
+``is_denylisted_extension``, plus the device-resident batch API used by bench.py.
+
+There is no CPU fallback: if the shared library is missing this module raises at import
+time, and if no HIP device is present ``Engine()`` raises ``CodecError(S3HC_DEVICE)``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libs3hc_lz4.so")
+
+S3HC_OK, S3HC_CORRUPT, S3HC_CHECKSUM, S3HC_DST_TOO_SMALL = 0, 1, 2, 3
+S3HC_UNSUPPORTED, S3HC_DEVICE, S3HC_INVALID_ARG = 4, 5, 6
+STATUS_NAMES = {0: "OK", 1: "CORRUPT", 2: "CHECKSUM", 3: "DST_TOO_SMALL", 4: "UNSUPPORTED", 5: "DEVICE", 6: "INVALID_ARG"}
+BLK_AUTO_LZ4FLEX, BLK_64K_PER_FRAME = 0, 1
+ALG_LZ4, ALG_NONE = 0, 1
+
+
+class CodecError(Exception):
+    """ProxyError::CompressionError equivalent (src/error.rs:22-23)."""
+
+    def __init__(self, status: int, message: str = ""):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {message}")
+        self.status = status
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", _HERE, "-j4"], check=True)
+    return LIB_PATH
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built (run __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u8p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p
+    szp, ip = ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int)
+    u64, u32, i32 = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "s3hc_create": (i32, [ctypes.POINTER(vp), i32]),
+        "s3hc_destroy": (None, [vp]),
+        "s3hc_last_error": (ctypes.c_char_p, []),
+        "s3hc_version": (ctypes.c_char_p, []),
+        "s3hc_frame_bound": (sz, [sz]),
+        "s3hc_compress_frame": (i32, [vp, u8p, sz, i32, u8p, sz, szp, ip]),
+        "s3hc_store_mode_frame": (i32, [vp, u8p, sz, u8p, sz, szp]),
+        "s3hc_decompressed_bound": (i32, [u8p, sz, szp]),
+        "s3hc_decompress_frames": (i32, [vp, u8p, sz, u8p, sz, szp]),
+        "s3hc_stream_open": (i32, [vp, ctypes.POINTER(vp)]),
+        "s3hc_stream_feed": (i32, [vp, u8p, sz]),
+        "s3hc_stream_finish": (i32, [vp]),
+        "s3hc_stream_read": (i32, [vp, u8p, sz, szp]),
+        "s3hc_stream_total": (u64, [vp]),
+        "s3hc_stream_close": (None, [vp]),
+        "s3hc_plan_encode": (i32, [vp, vp, vp, vp, u32, ctypes.POINTER(vp)]),
+        "s3hc_encode_dev": (i32, [vp, vp, vp, vp, u64, vp, vp, vp]),
+        "s3hc_plan_dst_bound": (u64, [vp]),
+        "s3hc_plan_decode": (i32, [vp, vp, vp, vp, vp, u32, ctypes.POINTER(vp)]),
+        "s3hc_decode_dev": (i32, [vp, vp, vp, vp, vp, vp, vp]),
+        "s3hc_plan_free": (None, [vp]),
+        "s3hc_last_kernel_ms": (ctypes.c_float, [vp, ctypes.c_char_p]),
+        "s3hc_set_timing": (None, [vp, i32]),
+        "s3hc_handler_new": (vp, [vp, sz, i32]),
+        "s3hc_handler_new_with_shared_stats": (vp, [sz, i32, vp]),
+        "s3hc_handler_clone": (vp, [vp]),
+        "s3hc_handler_free": (None, [vp]),
+        "s3hc_handler_is_compression_enabled": (i32, [vp]),
+        "s3hc_handler_compress_with_metadata": (i32, [vp, u8p, sz, ctypes.c_char_p, i32, u8p, sz, szp, ip, ip]),
+        "s3hc_handler_compress_with_algorithm": (i32, [vp, u8p, sz, i32, u8p, sz, szp, ip]),
+        "s3hc_handler_decompress_with_algorithm": (i32, [vp, u8p, sz, i32, u8p, sz, szp]),
+        "s3hc_handler_stats": (None, [vp, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_float)]),
+        "s3hc_handler_record_batch_bytes": (None, [vp, u64, u64]),
+        "s3hc_handler_record_object": (None, [vp, i32]),
+        "s3hc_is_denylisted_extension": (i32, [ctypes.c_char_p]),
+        "s3hc_dev_alloc": (i32, [vp, sz, ctypes.POINTER(vp)]),
+        "s3hc_dev_free": (i32, [vp, vp]),
+        "s3hc_memcpy": (i32, [vp, vp, vp, sz, i32]),
+        "s3hc_memset": (i32, [vp, vp, i32, sz]),
+        "s3hc_sync": (i32, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
+lib = _load()
+
+
+def _ptr(b) -> ctypes.c_void_p:
+    if isinstance(b, (bytes, bytearray, memoryview)):
+        b = bytes(b)
+        return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), b
+    raise TypeError(type(b))
+
+
+def _check(rc: int):
+    if rc != S3HC_OK:
+        raise CodecError(rc, (lib.s3hc_last_error() or b"").decode(errors="replace"))
+
+
+def is_denylisted_extension(path: str) -> bool:
+    """CompressionHandler::is_denylisted_extension (compression.rs:252-255)."""
+    return bool(lib.s3hc_is_denylisted_extension(path.encode()))
+
+
+def frame_bound(n: int) -> int:
+    return lib.s3hc_frame_bound(n)
+
+
+class Engine:
+    """One s3hc context on one GPU."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib.s3hc_create(ctypes.byref(h), device))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib.s3hc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- whole-buffer codec on host buffers
+    def compress_frame(self, data, policy: int = BLK_AUTO_LZ4FLEX) -> bytes:
+        p, keep = _ptr(data)
+        cap = frame_bound(len(keep))
+        out = ctypes.create_string_buffer(cap)
+        n, wc = ctypes.c_size_t(), ctypes.c_int()
+        _check(lib.s3hc_compress_frame(self.h, p, len(keep), policy, out, cap, ctypes.byref(n), ctypes.byref(wc)))
+        return out.raw[: n.value]
+
+    def store_mode_frame(self, data) -> bytes:
+        p, keep = _ptr(data)
+        cap = frame_bound(len(keep)) + 4 * (len(keep) // (4 << 20) + 1)
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t()
+        _check(lib.s3hc_store_mode_frame(self.h, p, len(keep), out, cap, ctypes.byref(n)))
+        return out.raw[: n.value]
+
+    def decompress_frames(self, data, cap: int | None = None) -> bytes:
+        p, keep = _ptr(data)
+        if cap is None:
+            b = ctypes.c_size_t()
+            _check(lib.s3hc_decompressed_bound(p, len(keep), ctypes.byref(b)))
+            cap = b.value
+        out = ctypes.create_string_buffer(max(cap, 1))
+        n = ctypes.c_size_t()
+        _check(lib.s3hc_decompress_frames(self.h, p, len(keep), out, cap, ctypes.byref(n)))
+        return out.raw[: n.value]
+
+    def decompress_status(self, data) -> tuple[int, bytes]:
+        try:
+            return S3HC_OK, self.decompress_frames(data)
+        except CodecError as e:
+            return e.status, b""
+
+    def stream(self) -> "FrameStream":
+        return FrameStream(self)
+
+    # ---- timing of the last *_dev call
+    def set_timing(self, on: bool):
+        lib.s3hc_set_timing(self.h, 1 if on else 0)
+
+    def kernel_ms(self, name: str) -> float:
+        return lib.s3hc_last_kernel_ms(self.h, name.encode())
+
+    def sync(self):
+        _check(lib.s3hc_sync(self.h))
+
+    def alloc(self, nbytes: int) -> "DeviceBuffer":
+        return DeviceBuffer(self, nbytes)
+
+    def upload(self, data) -> "DeviceBuffer":
+        b = DeviceBuffer(self, len(data))
+        b.write(data)
+        return b
+
+    # ---- device-resident batches (DeviceBuffer or any object with data_ptr()/numel())
+    def plan_encode(self, src_off, lengths, modes=None) -> "Plan":
+        n = len(src_off)
+        a_off = (ctypes.c_uint64 * n)(*src_off)
+        a_len = (ctypes.c_uint32 * n)(*lengths)
+        a_mode = (ctypes.c_uint8 * n)(*(modes if modes is not None else [0] * n))
+        h = ctypes.c_void_p()
+        _check(lib.s3hc_plan_encode(self.h, a_off, a_len, a_mode, n, ctypes.byref(h)))
+        return Plan(h, n)
+
+    def encode_dev(self, plan: "Plan", d_src, d_dst, d_item_off, d_item_len, stream=None):
+        _check(lib.s3hc_encode_dev(self.h, plan.h, d_src.data_ptr(), d_dst.data_ptr(), d_dst.numel(),
+                                   d_item_off.data_ptr(), d_item_len.data_ptr(), stream))
+
+    def plan_decode(self, frame_off, frame_len, dst_off, dst_cap) -> "Plan":
+        n = len(frame_off)
+        h = ctypes.c_void_p()
+        _check(lib.s3hc_plan_decode(self.h, (ctypes.c_uint64 * n)(*frame_off), (ctypes.c_uint32 * n)(*frame_len),
+                                    (ctypes.c_uint64 * n)(*dst_off), (ctypes.c_uint32 * n)(*dst_cap), n,
+                                    ctypes.byref(h)))
+        return Plan(h, n)
+
+    def decode_dev(self, plan: "Plan", d_src, d_dst, d_out_len, d_status, stream=None):
+        _check(lib.s3hc_decode_dev(self.h, plan.h, d_src.data_ptr(), d_dst.data_ptr(), d_out_len.data_ptr(),
+                                   d_status.data_ptr(), stream))
+
+
+class DeviceBuffer:
+    """HBM buffer owned by the engine's HIP runtime (data_ptr()/numel() like a tensor)."""
+
+    def __init__(self, eng: Engine, nbytes: int):
+        self.eng, self.nbytes = eng, int(nbytes)
+        p = ctypes.c_void_p()
+        _check(lib.s3hc_dev_alloc(eng.h, self.nbytes, ctypes.byref(p)))
+        self.ptr = p
+
+    def data_ptr(self) -> int:
+        return self.ptr.value
+
+    def numel(self) -> int:
+        return self.nbytes
+
+    def write(self, data, offset: int = 0):
+        p, keep = _ptr(data)
+        assert offset + len(keep) <= self.nbytes
+        _check(lib.s3hc_memcpy(self.eng.h, ctypes.c_void_p(self.ptr.value + offset), p, len(keep), 1))
+
+    def read(self, n: int | None = None, offset: int = 0) -> bytes:
+        n = self.nbytes - offset if n is None else n
+        out = ctypes.create_string_buffer(max(n, 1))
+        _check(lib.s3hc_memcpy(self.eng.h, out, ctypes.c_void_p(self.ptr.value + offset), n, 2))
+        return out.raw[:n]
+
+    def fill(self, value: int = 0):
+        _check(lib.s3hc_memset(self.eng.h, self.ptr, value, self.nbytes))
+
+    def u32(self, n: int) -> list:
+        import array
+        a = array.array("I")
+        a.frombytes(self.read(4 * n))
+        return list(a)
+
+    def i32(self, n: int) -> list:
+        import array
+        a = array.array("i")
+        a.frombytes(self.read(4 * n))
+        return list(a)
+
+    def u64(self, n: int) -> list:
+        import array
+        a = array.array("Q")
+        a.frombytes(self.read(8 * n))
+        return list(a)
+
+    def free(self):
+        if self.ptr:
+            lib.s3hc_dev_free(self.eng.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            if self.ptr and self.eng.h:
+                self.free()
+        except Exception:
+            pass
+
+
+class Plan:
+    def __init__(self, h, n):
+        self.h, self.n = h, n
+
+    @property
+    def dst_bound(self) -> int:
+        return lib.s3hc_plan_dst_bound(self.h)
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib.s3hc_plan_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class FrameStream:
+    """stream_range_data (disk_cache.rs:3850-3935): feed compressed bytes, read decoded chunks."""
+
+    def __init__(self, eng: Engine):
+        h = ctypes.c_void_p()
+        _check(lib.s3hc_stream_open(eng.h, ctypes.byref(h)))
+        self.h = h
+
+    def feed(self, data):
+        p, keep = _ptr(data)
+        _check(lib.s3hc_stream_feed(self.h, p, len(keep)))
+
+    def finish(self):
+        _check(lib.s3hc_stream_finish(self.h))
+
+    def read(self, cap: int = 1 << 20) -> bytes:
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t()
+        _check(lib.s3hc_stream_read(self.h, out, cap, ctypes.byref(n)))
+        return out.raw[: n.value]
+
+    @property
+    def total(self) -> int:
+        return lib.s3hc_stream_total(self.h)
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib.s3hc_stream_close(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+@dataclass
+class CompressionResult:  # compression.rs:159-166
+    data: bytes
+    algorithm: int
+    original_size: int
+    compressed_size: int
+    was_compressed: bool
+
+
+@dataclass
+class CompressionStats:  # compression.rs:53-76
+    total_objects_compressed: int
+    total_objects_uncompressed: int
+    total_bytes_before: int
+    total_bytes_after: int
+    compression_failures: int
+    decompression_failures: int
+    average_compression_ratio: float
+
+
+class CompressionHandler:
+    """Mirror of src/compression.rs CompressionHandler over the C++ handler in the library."""
+
+    def __init__(self, engine: Engine, compression_threshold: int, compression_enabled: bool, _h=None):
+        self.engine = engine
+        self.h = _h if _h is not None else lib.s3hc_handler_new(engine.h, compression_threshold,
+                                                                1 if compression_enabled else 0)
+
+    @classmethod
+    def new_with_shared_stats(cls, threshold: int, enabled: bool, source: "CompressionHandler"):
+        return cls(source.engine, threshold, enabled, lib.s3hc_handler_new_with_shared_stats(
+            threshold, 1 if enabled else 0, source.h))
+
+    def clone(self) -> "CompressionHandler":
+        return CompressionHandler(self.engine, 0, True, lib.s3hc_handler_clone(self.h))
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib.s3hc_handler_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def is_compression_enabled(self) -> bool:
+        return bool(lib.s3hc_handler_is_compression_enabled(self.h))
+
+    @staticmethod
+    def is_denylisted_extension(path: str) -> bool:
+        return is_denylisted_extension(path)
+
+    @staticmethod
+    def encode_store_mode_frame(engine: Engine, data) -> bytes:
+        return engine.store_mode_frame(data)
+
+    def compress_with_metadata(self, data, path: str, should_compress: bool) -> CompressionResult:
+        p, keep = _ptr(data)
+        cap = frame_bound(len(keep)) + 4 * (len(keep) // (4 << 20) + 1) + 64
+        out = ctypes.create_string_buffer(cap)
+        n, alg, wc = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_int()
+        _check(lib.s3hc_handler_compress_with_metadata(self.h, p, len(keep), path.encode(), 1 if should_compress else 0,
+                                                       out, cap, ctypes.byref(n), ctypes.byref(alg), ctypes.byref(wc)))
+        return CompressionResult(out.raw[: n.value], alg.value, len(keep), n.value, bool(wc.value))
+
+    def compress_with_algorithm(self, data, algorithm: int = ALG_LZ4) -> CompressionResult:
+        p, keep = _ptr(data)
+        cap = frame_bound(len(keep)) + 64
+        out = ctypes.create_string_buffer(cap)
+        n, wc = ctypes.c_size_t(), ctypes.c_int()
+        _check(lib.s3hc_handler_compress_with_algorithm(self.h, p, len(keep), algorithm, out, cap, ctypes.byref(n),
+                                                        ctypes.byref(wc)))
+        return CompressionResult(out.raw[: n.value], algorithm, len(keep), n.value, bool(wc.value))
+
+    def decompress_with_algorithm(self, data, algorithm: int = ALG_LZ4) -> bytes:
+        p, keep = _ptr(data)
+        b = ctypes.c_size_t()
+        lib.s3hc_decompressed_bound(p, len(keep), ctypes.byref(b))
+        cap = max(b.value, len(keep), 1)
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t()
+        _check(lib.s3hc_handler_decompress_with_algorithm(self.h, p, len(keep), algorithm, out, cap, ctypes.byref(n)))
+        return out.raw[: n.value]
+
+    def decompress_data(self, data) -> bytes:
+        return self.decompress_with_algorithm(data, ALG_LZ4)
+
+    def get_stats(self) -> CompressionStats:
+        arr = (ctypes.c_uint64 * 6)()
+        r = ctypes.c_float()
+        lib.s3hc_handler_stats(self.h, arr, ctypes.byref(r))
+        return CompressionStats(*list(arr), r.value)
+
+    def record_batch_bytes(self, before: int, after: int):
+        lib.s3hc_handler_record_batch_bytes(self.h, before, after)
+
+    def record_object(self, compressed: bool):
+        lib.s3hc_handler_record_object(self.h, 1 if compressed else 0)
