@@ -109,10 +109,15 @@ int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* plan, const uint8_t* d_src, uint8_
                     uint32_t* d_out_len, int32_t* d_status, void* stream);
 void s3hc_plan_free(s3hc_plan* plan);
 
-/* Time of the last s3hc_*_dev call per kernel (ms, HIP events on the launch stream),
- * for roofline accounting. name = "enc_parse", "enc_emit", "decode", "xxh32", ... */
-float s3hc_last_kernel_ms(const s3hc_ctx* ctx, const char* name);
+/* Per-kernel timing for roofline accounting: with timing on, every *_dev launch is bracketed
+ * by HIP events on its stream (no host sync). s3hc_timing_collect resolves them into per-name
+ * totals: s3hc_last_kernel_ms = summed ms, s3hc_kernel_count = launches.
+ * Names: "xxh32", "enc_parse", "enc_sizes", "enc_emit", "dec_plan", "decode", "dec_finish". */
 void s3hc_set_timing(s3hc_ctx* ctx, int enabled);
+int s3hc_timing_collect(s3hc_ctx* ctx);
+void s3hc_timing_reset(s3hc_ctx* ctx);
+float s3hc_last_kernel_ms(const s3hc_ctx* ctx, const char* name);
+int s3hc_kernel_count(const s3hc_ctx* ctx, const char* name);
 
 /* ---- device memory plumbing (lets callers stage batches in HBM without a second HIP
  * runtime in the process). kind: 1 H2D, 2 D2H, 3 D2D; s3hc_memcpy is host-synchronous. */

@@ -114,12 +114,29 @@ template <class T> static hipError_t upload(DevBuf& b, const std::vector<T>& v, 
 }
 
 // --------------------------------------------------------------- context
+struct TimedSpan {
+    std::string name;
+    hipEvent_t a, b;
+};
 struct s3hc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
     bool timing = false;
     std::map<std::string, float> kernel_ms;
+    std::map<std::string, int> kernel_n;
+    std::vector<TimedSpan> pending;
+    std::vector<hipEvent_t> event_pool;
+    hipEvent_t take_event() {
+        if (event_pool.empty()) {
+            hipEvent_t e;
+            (void)hipEventCreate(&e);
+            return e;
+        }
+        hipEvent_t e = event_pool.back();
+        event_pool.pop_back();
+        return e;
+    }
     // scratch for host-buffer calls
     DevBuf d_in, d_out;
     s3hc_plan* host_plan = nullptr;
@@ -127,39 +144,15 @@ struct s3hc_ctx {
     ~s3hc_ctx();
 };
 
-// Per-kernel event timing (enabled by s3hc_set_timing; used by bench.py for roofline).
+// Per-kernel event timing (s3hc_set_timing). Events come from a pool and are only resolved
+// by s3hc_timing_collect(), so timing adds no host synchronisation inside a timed region.
 struct KTimer {
     s3hc_ctx* ctx;
     hipStream_t st;
-    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> ev;
     explicit KTimer(s3hc_ctx* c, hipStream_t s) : ctx(c), st(s) {}
-    void begin(const char* name) {
-        if (!ctx->timing) return;
-        hipEvent_t a, b;
-        (void)hipEventCreate(&a);
-        (void)hipEventCreate(&b);
-        (void)hipEventRecord(a, st);
-        ev.push_back({name, {a, b}});
-    }
-    void end() {
-        if (!ctx->timing || ev.empty()) return;
-        (void)hipEventRecord(ev.back().second.second, st);
-    }
-    ~KTimer() {
-        if (ev.empty()) return;
-        (void)hipEventSynchronize(ev.back().second.second);
-        std::map<std::string, float> acc;
-        for (auto& e : ev) {
-            float ms = 0.f;
-            (void)hipEventElapsedTime(&ms, e.second.first, e.second.second);
-            acc[e.first] += ms;
-            (void)hipEventDestroy(e.second.first);
-            (void)hipEventDestroy(e.second.second);
-        }
-        ctx->kernel_ms = acc;
-    }
+    void begin(const char* name);
+    void end();
 };
-
 // ------------------------------------------------------------------ plans
 struct s3hc_plan {
     bool is_encode = true;
@@ -180,7 +173,20 @@ struct s3hc_plan {
     DevBuf d_nblk, d_fstatus, d_blk_base, d_fwant, d_dblocks, d_units, d_blk_out, d_blk_status, d_got;
 };
 
+void KTimer::begin(const char* name) {
+    if (!ctx->timing) return;
+    TimedSpan t{name, ctx->take_event(), ctx->take_event()};
+    (void)hipEventRecord(t.a, st);
+    ctx->pending.push_back(t);
+}
+void KTimer::end() {
+    if (!ctx->timing || ctx->pending.empty()) return;
+    (void)hipEventRecord(ctx->pending.back().b, st);
+}
+
 s3hc_ctx::~s3hc_ctx() {
+    for (auto& t : pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
+    for (auto e : event_pool) (void)hipEventDestroy(e);
     delete host_plan;
     if (stream) (void)hipStreamDestroy(stream);
 }
@@ -313,10 +319,38 @@ extern "C" void s3hc_destroy(s3hc_ctx* ctx) {
     delete ctx;
 }
 extern "C" void s3hc_set_timing(s3hc_ctx* ctx, int enabled) { if (ctx) ctx->timing = enabled != 0; }
+// Resolve recorded spans into per-name totals (ms) and launch counts; clears the spans.
+extern "C" int s3hc_timing_collect(s3hc_ctx* ctx) {
+    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    for (auto& t : ctx->pending) {
+        HIPCHK(hipEventSynchronize(t.b));
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, t.a, t.b));
+        ctx->kernel_ms[t.name] += ms;
+        ctx->kernel_n[t.name] += 1;
+        ctx->event_pool.push_back(t.a);
+        ctx->event_pool.push_back(t.b);
+    }
+    ctx->pending.clear();
+    return S3HC_OK;
+}
+extern "C" void s3hc_timing_reset(s3hc_ctx* ctx) {
+    if (!ctx) return;
+    s3hc_timing_collect(ctx);
+    ctx->kernel_ms.clear();
+    ctx->kernel_n.clear();
+}
 extern "C" float s3hc_last_kernel_ms(const s3hc_ctx* ctx, const char* name) {
     if (!ctx || !name) return -1.f;
     auto it = ctx->kernel_ms.find(name);
     return it == ctx->kernel_ms.end() ? -1.f : it->second;
+}
+extern "C" int s3hc_kernel_count(const s3hc_ctx* ctx, const char* name) {
+    if (!ctx || !name) return 0;
+    auto it = ctx->kernel_n.find(name);
+    return it == ctx->kernel_n.end() ? 0 : it->second;
 }
 
 extern "C" size_t s3hc_frame_bound(size_t n) {
@@ -495,6 +529,7 @@ struct HWalk {
     std::vector<uint32_t> blk_cs_want;  // block checksums (FLG 0x10)
     std::vector<uint8_t> blk_has_cs;
     int tail_status = S3HC_OK;   // structural error after the last complete frame
+    bool last_incomplete = false; // tail_status belongs to the last frame in `frames` (truncated/bad block)
     bool stopped_empty = false;  // a frame with no blocks ended the walk (Ok(0) => break)
     size_t end = 0;              // bytes consumed by complete frames
     uint64_t slot_total = 0;
@@ -580,6 +615,7 @@ static void walk_frames(const uint8_t* src, size_t n, HWalk& W, bool allow_incom
             if (stream_mode && st == S3HC_CORRUPT) break;  // wait for more bytes
             // Blocks before the failure still decode (their errors come first in order).
             W.tail_status = st;
+            W.last_incomplete = true;
         }
         F.nblk = (uint32_t)fb.size();
         W.blocks.insert(W.blocks.end(), fb.begin(), fb.end());
@@ -671,12 +707,12 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
             if ((F.flg & 0x20) && k + 1 < F.nblk && bo[b] != W.blocks[b].limit) need_compact = true;
             tot += bo[b];
         }
-        if (fs == S3HC_OK && f + 1 == nf && W.tail_status != S3HC_OK) fs = W.tail_status;  // incomplete frame
+        if (fs == S3HC_OK && f + 1 == nf && W.last_incomplete) fs = W.tail_status;  // incomplete frame
         if (fs != S3HC_OK) { err_status = fs; use_frames = f; break; }
         fout[f] = tot;
         if (!stream_mode && tot == 0) { use_frames = f + 1; stopped = true; break; }
     }
-    if (err_status == S3HC_OK && !stopped && W.tail_status != S3HC_OK && nf == W.frames.size()) {
+    if (err_status == S3HC_OK && !stopped && W.tail_status != S3HC_OK && !W.last_incomplete) {
         // a header-level failure after every walked frame (bad magic, truncated header, ...)
         err_status = W.tail_status;
     }

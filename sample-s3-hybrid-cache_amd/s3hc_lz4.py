@@ -70,6 +70,9 @@ def _load():
         "s3hc_plan_free": (None, [vp]),
         "s3hc_last_kernel_ms": (ctypes.c_float, [vp, ctypes.c_char_p]),
         "s3hc_set_timing": (None, [vp, i32]),
+        "s3hc_timing_collect": (i32, [vp]),
+        "s3hc_timing_reset": (None, [vp]),
+        "s3hc_kernel_count": (i32, [vp, ctypes.c_char_p]),
         "s3hc_handler_new": (vp, [vp, sz, i32]),
         "s3hc_handler_new_with_shared_stats": (vp, [sz, i32, vp]),
         "s3hc_handler_clone": (vp, [vp]),
@@ -179,8 +182,18 @@ class Engine:
     def set_timing(self, on: bool):
         lib.s3hc_set_timing(self.h, 1 if on else 0)
 
-    def kernel_ms(self, name: str) -> float:
-        return lib.s3hc_last_kernel_ms(self.h, name.encode())
+    def timing_reset(self):
+        lib.s3hc_timing_reset(self.h)
+
+    def timing(self) -> dict:
+        """{kernel name: (total ms, launches)} since the last reset."""
+        _check(lib.s3hc_timing_collect(self.h))
+        out = {}
+        for name in ("xxh32", "enc_parse", "enc_sizes", "enc_emit", "dec_plan", "decode", "dec_finish"):
+            n = lib.s3hc_kernel_count(self.h, name.encode())
+            if n:
+                out[name] = (lib.s3hc_last_kernel_ms(self.h, name.encode()), n)
+        return out
 
     def sync(self):
         _check(lib.s3hc_sync(self.h))
