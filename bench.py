@@ -41,6 +41,7 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--blocks", type=int, default=4096, help="64 KiB blocks per GPU (config 2: 4096)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--skip-check", action="store_true", help="diagnostic builds only: skip output checks")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall seconds of the CPU baseline sample")
     return ap.parse_args()
 
@@ -174,9 +175,10 @@ def main():
         step()
     eng.sync()
     # correctness gate on the warmed-up state (outside the timed region)
-    st = d_ost.i32(nb)
-    assert st == [0] * nb, f"decode status {set(st)}"
-    assert d_out.read(2 * block) == data[: 2 * block]
+    if not args.skip_check:
+        st = d_ost.i32(nb)
+        assert st == [0] * nb, f"decode status {set(st)}"
+        assert d_out.read(2 * block) == data[: 2 * block]
 
     eng.timing_reset()
     eng.set_timing(True)
@@ -193,9 +195,9 @@ def main():
     kt = eng.timing()
 
     # full-output check after the timed steps
-    assert d_ost.i32(nb) == [0] * nb
-    out_ok = d_out.read() == data
-    assert out_ok, "decoded batch differs from the input"
+    if not args.skip_check:
+        assert d_ost.i32(nb) == [0] * nb
+        assert d_out.read() == data, "decoded batch differs from the input"
 
     total_u = allsum(pg, float(nb * block)) * args.steps
     value = total_u / elapsed / GiB

@@ -69,32 +69,37 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
 }
 
 // Wave-cooperative copy of n bytes global -> global, any alignment of either side.
+// Loads for up to 4 KiB are issued before the stores.
 __device__ void wave_copy_global(uint8_t* dst, const uint8_t* src, uint32_t n, int lane) {
     uintptr_t da = (uintptr_t)dst;
     uint32_t head = (uint32_t)((16 - (da & 15)) & 15);
     if (head > n) head = n;
     if ((uint32_t)lane < head) dst[lane] = src[lane];
-    uint32_t body = (n - head) & ~15u;
+    const uint32_t nv = (n - head) >> 4;
     const uint8_t* s = src + head;
     uint8_t* d = dst + head;
-    if ((((uintptr_t)s) & 3) == 0) {
-        for (uint32_t c = (uint32_t)lane * 16; c < body; c += 64 * 16) {
-            const uint32_t* sw = (const uint32_t*)(s + c);
-            uint4 v = make_uint4(sw[0], sw[1], sw[2], sw[3]);
-            *(uint4*)(d + c) = v;
+    const uintptr_t sa = (uintptr_t)s;
+    const uint32_t sh = (uint32_t)(sa & 3);
+    const uint32_t* sw = (const uint32_t*)(sa & ~(uintptr_t)3);
+    for (uint32_t base = 0; base < nv; base += 64 * 2) {
+        const uint32_t ja = base + lane, jb = base + lane + 64;
+        const uint32_t ka = ja < nv ? ja : nv - 1, kb = jb < nv ? jb : nv - 1;
+        uint4 va, vb;
+        if (sh == 0) {
+            va = make_uint4(sw[4 * ka], sw[4 * ka + 1], sw[4 * ka + 2], sw[4 * ka + 3]);
+            vb = make_uint4(sw[4 * kb], sw[4 * kb + 1], sw[4 * kb + 2], sw[4 * kb + 3]);
+        } else {
+            const uint32_t a0 = sw[4 * ka], a1 = sw[4 * ka + 1], a2 = sw[4 * ka + 2], a3 = sw[4 * ka + 3], a4 = sw[4 * ka + 4];
+            const uint32_t b0 = sw[4 * kb], b1 = sw[4 * kb + 1], b2 = sw[4 * kb + 2], b3 = sw[4 * kb + 3], b4 = sw[4 * kb + 4];
+            va = make_uint4(__builtin_amdgcn_alignbyte(a1, a0, sh), __builtin_amdgcn_alignbyte(a2, a1, sh),
+                            __builtin_amdgcn_alignbyte(a3, a2, sh), __builtin_amdgcn_alignbyte(a4, a3, sh));
+            vb = make_uint4(__builtin_amdgcn_alignbyte(b1, b0, sh), __builtin_amdgcn_alignbyte(b2, b1, sh),
+                            __builtin_amdgcn_alignbyte(b3, b2, sh), __builtin_amdgcn_alignbyte(b4, b3, sh));
         }
-    } else {
-        uintptr_t sa = (uintptr_t)s;
-        uint32_t sh = (uint32_t)(sa & 3);
-        for (uint32_t c = (uint32_t)lane * 16; c < body; c += 64 * 16) {
-            const uint32_t* sw = (const uint32_t*)((sa + c) & ~(uintptr_t)3);
-            uint32_t w0 = sw[0], w1 = sw[1], w2 = sw[2], w3 = sw[3], w4 = sw[4];
-            uint4 v = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                                 __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
-            *(uint4*)(d + c) = v;
-        }
+        if (ja < nv) *(uint4*)(d + 16 * ja) = va;
+        if (jb < nv) *(uint4*)(d + 16 * jb) = vb;
     }
-    for (uint32_t t = head + body + (uint32_t)lane; t < n; t += 64) dst[t] = src[t];
+    for (uint32_t t = head + 16 * nv + (uint32_t)lane; t < n; t += 64) dst[t] = src[t];
 }
 
 // Wave-cooperative store of n bytes from (contiguous) LDS to global, any global alignment.
@@ -142,12 +147,13 @@ __global__ __launch_bounds__(256) void k_xxh32_ranges(const uint8_t* __restrict_
     uint32_t s = 0;
     if ((((uintptr_t)p) & 3) == 0) {
         const uint32_t* w = (const uint32_t*)q;
-        for (; s + 8 <= ns; s += 8) {
-            uint32_t v[8];
+        // 32 loads in flight per lane: the chain (add, rotate, multiply) is the only serial part
+        for (; s + 32 <= ns; s += 32) {
+            uint32_t v[32];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = w[4 * (s + k)];
+            for (int k = 0; k < 32; ++k) v[k] = w[4 * (s + k)];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) acc = xround(acc, v[k]);
+            for (int k = 0; k < 32; ++k) acc = xround(acc, v[k]);
         }
         for (; s < ns; ++s) acc = xround(acc, w[4 * s]);
     } else {
@@ -483,26 +489,108 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
 namespace enc {
 constexpr uint32_t kIn = kPrewarm + kSeg + 128;         // staged input bytes (+ read-ahead pad)
 constexpr uint32_t kTbl = 1u << kHashLog;
-constexpr uint32_t kWaveLds = kIn + kTbl * 2;
-constexpr int kWaves = 4;
-constexpr uint16_t kEmpty = 0xFFFF;
+constexpr uint32_t kSub = 512;                          // positions per candidate sub-block
+constexpr uint32_t kWaveLds = kIn + kTbl * 2 + kSub * 4;
+constexpr int kWaves = 1;
+constexpr uint32_t kEmpty = 0xFFFFu;
 }  // namespace enc
 
 __device__ __forceinline__ uint32_t ext_bytes(uint32_t n) { return n >= 15 ? (n - 15) / 255 + 1 : 0; }
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
+__device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t l) {
+    return (uint64_t)rdl((uint32_t)v, l) | ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32);
+}
 
-// Stage block bytes [lo, hi) into lds (lds[x - lo]); any alignment.
+// Stage block bytes [lo, hi) into lds (lds[x - lo]); any alignment. Every lane issues all of
+// its loads (8 x 16 B per pass) before the first LDS store, so staging costs one HBM round trip
+// per 8 KiB instead of one per dword.
 __device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* lds, int lane) {
     const uint32_t n = hi - lo;
-    for (uint32_t i = 4u * lane; i < n; i += 256) *(uint32_t*)(lds + i) = gld32u(blk + lo + i, n - i);
+    const uint8_t* g = blk + lo;
+    const uint32_t nv = n >> 4;  // whole 16-byte vectors
+    if (nv && (((uintptr_t)g) & 15) == 0) {
+        const uint4* sv = (const uint4*)g;
+        for (uint32_t base = 0; base < nv; base += 64 * 8) {
+            // loads are unconditional (clamped index) so the group stays in registers
+            uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+#define S3HC_LD(q, vq) { const uint32_t j = base + lane + 64 * q; vq = sv[j < nv ? j : nv - 1]; }
+            S3HC_LD(0, v0) S3HC_LD(1, v1) S3HC_LD(2, v2) S3HC_LD(3, v3)
+            S3HC_LD(4, v4) S3HC_LD(5, v5) S3HC_LD(6, v6) S3HC_LD(7, v7)
+#undef S3HC_LD
+#define S3HC_ST(q, vq) { const uint32_t j = base + lane + 64 * q; if (j < nv) *(uint4*)(lds + 16 * j) = vq; }
+            S3HC_ST(0, v0) S3HC_ST(1, v1) S3HC_ST(2, v2) S3HC_ST(3, v3)
+            S3HC_ST(4, v4) S3HC_ST(5, v5) S3HC_ST(6, v6) S3HC_ST(7, v7)
+#undef S3HC_ST
+        }
+    } else if (nv) {
+        const uintptr_t a = (uintptr_t)g & ~(uintptr_t)3;
+        const uint32_t sh = (uint32_t)((uintptr_t)g & 3);
+        const uint32_t* sw = (const uint32_t*)a;
+        for (uint32_t base = 0; base < nv; base += 64 * 2) {
+            const uint32_t ja = base + lane, jb = base + lane + 64;
+            const uint32_t ka = ja < nv ? ja : nv - 1, kb = jb < nv ? jb : nv - 1;
+            const uint32_t a0 = sw[4 * ka], a1 = sw[4 * ka + 1], a2 = sw[4 * ka + 2], a3 = sw[4 * ka + 3];
+            const uint32_t a4 = sh ? sw[4 * ka + 4] : 0u;  // holds valid bytes only when sh != 0
+            const uint32_t b0 = sw[4 * kb], b1 = sw[4 * kb + 1], b2 = sw[4 * kb + 2], b3 = sw[4 * kb + 3];
+            const uint32_t b4 = sh ? sw[4 * kb + 4] : 0u;
+            if (ja < nv)
+                *(uint4*)(lds + 16 * ja) = make_uint4(__builtin_amdgcn_alignbyte(a1, a0, sh), __builtin_amdgcn_alignbyte(a2, a1, sh),
+                                                      __builtin_amdgcn_alignbyte(a3, a2, sh), __builtin_amdgcn_alignbyte(a4, a3, sh));
+            if (jb < nv)
+                *(uint4*)(lds + 16 * jb) = make_uint4(__builtin_amdgcn_alignbyte(b1, b0, sh), __builtin_amdgcn_alignbyte(b2, b1, sh),
+                                                      __builtin_amdgcn_alignbyte(b3, b2, sh), __builtin_amdgcn_alignbyte(b4, b3, sh));
+        }
+    }
+    for (uint32_t t = 16 * nv + lane; t < n; t += 64) lds[t] = g[t];
     wave_sync();
 }
 
-__global__ __launch_bounds__(256) void k_enc_parse(const uint8_t* __restrict__ src,
+// Lane-parallel post-processing of up to 64 walk hops held one per lane (hop j in lane j):
+// clip each backward extension at the previous match end, form the LZ4 sequence record
+// (literal length, match length, offset), add up encoded sizes, store the records.
+__device__ __forceinline__ void enc_flush_group(int lane, uint32_t cnt, uint32_t g0, uint32_t gls, uint32_t hP,
+                                                uint32_t hW, uint32_t hL, uint2* myrec, uint32_t& body,
+                                                uint32_t& ll0) {
+    const bool act = (uint32_t)lane < cnt;
+    const uint32_t endj = hP + hL;                        // this hop's match end
+    uint32_t prev = __shfl_up(endj, 1);
+    if (lane == 0) prev = gls;
+    uint32_t nb = (hW >> 29) & 7u;
+    if (nb > hP - prev) nb = hP - prev;
+    const uint32_t p = hP - nb;
+    const uint32_t ll = p - prev;
+    const uint32_t len = nb + hL;
+    const uint32_t off = (hW >> 9) & 0xFFFFu;
+    const uint32_t gj = g0 + lane;
+    uint32_t sz = act ? (gj == 0 ? 0u : 1 + ext_bytes(ll)) + ll + 2 + ext_bytes(len - 4) : 0u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) sz += __shfl_xor(sz, d);
+    body += sz;
+    if (g0 == 0) ll0 = rdl(ll, 0);
+    if (act) myrec[gj] = make_uint2(ll | (len << 16), off);
+}
+
+// Match finding for one 4 KiB segment per wave, in alternating phases per kSub-position
+// sub-block:
+//   candidates (parallel, 64 positions per step): every position P is probed exactly once —
+//     4-byte hash into the wave's LDS table (most recent earlier position with that hash),
+//     verified against the input, with a fallback to distances 1..4 (runs and short periods
+//     inside a probe step); then every position of the step enters the table. For verified
+//     positions the same step measures the match: forward up to kFwd bytes, backward up to
+//     4 bytes. A second pass writes for EVERY position x a descriptor of the first match at or
+//     after x: distance to it, its offset, forward length and backward length (one u32).
+//   greedy walk (scalar, one LDS read per hop): read the descriptor at the current position,
+//     jump to the match, extend it wave-wide only if it reached kFwd bytes, continue from its
+//     end. Hops are parked one per lane; every 64 hops a lane-parallel pass turns them into
+//     LZ4 sequence records (enc_flush_group).
+// Matches end inside the segment, so segments are independent; k_enc_sizes stitches them.
+__global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ src,
                                                    const EncBlock* __restrict__ blocks,
                                                    const uint32_t* __restrict__ seg_block, uint32_t nseg,
                                                    uint2* __restrict__ recs, SegSummary* __restrict__ summ) {
     using namespace enc;
+    constexpr uint32_t kFwd = 19;  // forward bytes measured in the parallel phase (4 verified + 15)
+    static_assert(kSub <= 512, "descriptor keeps the hop distance in 9 bits");
     __shared__ __attribute__((aligned(16))) uint8_t smem[kWaves * kWaveLds];
     const int lane = lane_id();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -513,6 +601,8 @@ __global__ __launch_bounds__(256) void k_enc_parse(const uint8_t* __restrict__ s
     if (B.flags & (EB_STORE | EB_EMPTY)) return;
     uint8_t* inb = smem + wv * kWaveLds;
     uint16_t* tbl = (uint16_t*)(inb + kIn);
+    uint32_t* info = (uint32_t*)(tbl + kTbl);   // per position: off | lenf-4 << 16 | nb << 24 (0 = none)
+    uint32_t* nd = info;  // descriptors overwrite info in place: chunk c reads info only at >= c
     const uint32_t U = B.len;
     const uint32_t k = s - B.seg0;
     const uint32_t seg_lo = k * kSeg;
@@ -523,8 +613,8 @@ __global__ __launch_bounds__(256) void k_enc_parse(const uint8_t* __restrict__ s
     stage_in(bin, pw_lo, st_hi, inb, lane);
     for (uint32_t t = lane; t < kTbl / 2; t += 64) ((uint32_t*)tbl)[t] = 0xFFFFFFFFu;
     wave_sync();
-    // Largest match end, largest match start (LZ4: last 5 bytes literal, last match starts
-    // >= 12 bytes before the block end; segment matches end inside the segment).
+    // Largest match end / start (LZ4: the last 5 bytes are literals and the last match starts
+    // at least 12 bytes before the block end; segment matches end inside the segment).
     const uint32_t blk_end_lim = U >= 5 ? U - 5 : 0;
     const uint32_t end_lim = seg_hi < blk_end_lim ? seg_hi : blk_end_lim;
     int64_t smax = (int64_t)end_lim - 4;
@@ -533,103 +623,155 @@ __global__ __launch_bounds__(256) void k_enc_parse(const uint8_t* __restrict__ s
     for (uint32_t x = pw_lo + lane; x + 4 <= seg_lo; x += 64) tbl[hash4(lds32u(inb, x - pw_lo))] = (uint16_t)(x - pw_lo);
     wave_sync();
 
-    uint32_t lit_start = seg_lo;
-    uint32_t W = seg_lo;
+    const uint32_t* dw = (const uint32_t*)inb;
+    uint32_t lit_start = seg_lo;   // greedy position: end of the last match
+    uint32_t gls = seg_lo;         // lit_start before the first hop of the current group
     uint32_t nseq = 0, body = 0, ll0 = 0;
-    uint32_t rx = 0, ry = 0;
+    uint32_t hP = 0, hW = 0, hL = 0;  // parked hops (lane j = hop j of the group)
     uint2* myrec = recs + (size_t)s * kMaxSeqPerSeg;
-    while ((int64_t)W <= smax) {
-        const uint32_t P = W + lane;
-        const bool valid = (int64_t)P <= smax;
-        const uint32_t v = lds32u(inb, P - pw_lo);
-        const uint32_t h = hash4(v);
-        const uint32_t c16 = tbl[h];
-        uint32_t c = pw_lo + c16;
-        bool good = valid && c16 != kEmpty && c < P && lds32u(inb, c - pw_lo) == v;
-        // short-period repeats inside the probe window (runs, 2-4 byte patterns)
-        const uint32_t v1 = __shfl_up(v, 1), v2 = __shfl_up(v, 2), v3 = __shfl_up(v, 3), v4 = __shfl_up(v, 4);
-        if (!good && valid) {
-            if (lane >= 1 && v1 == v) { good = true; c = P - 1; }
-            else if (lane >= 2 && v2 == v) { good = true; c = P - 2; }
-            else if (lane >= 3 && v3 == v) { good = true; c = P - 3; }
-            else if (lane >= 4 && v4 == v) { good = true; c = P - 4; }
-        }
-        const uint64_t mask = __ballot(good);
-        // Insert only the positions the parse has passed (lanes up to the first match):
-        // later lanes are probed again by the next window, and inserting them now would
-        // shadow their own older candidates.
-        const uint32_t f = mask ? (uint32_t)__builtin_ctzll(mask) : 63u;
-        if (valid && (uint32_t)lane <= f) tbl[h] = (uint16_t)(P - pw_lo);
-        if (mask == 0) {
-            W += 64;
-            continue;
-        }
-        uint32_t p = W + f;
-        uint32_t cc = rdl(c, f);
-        // backward extension into the pending literals
-        {
-            const uint32_t lim = (p - lit_start) < (cc - pw_lo) ? (p - lit_start) : (cc - pw_lo);
-            uint32_t nb = 0;
-            while (nb < lim) {
-                const uint32_t kk = nb + lane;
-                const bool eq = kk < lim && inb[p - 1 - kk - pw_lo] == inb[cc - 1 - kk - pw_lo];
-                const uint64_t m = __ballot(!eq);
-                if (m == 0) { nb += 64; continue; }
-                nb += (uint32_t)__builtin_ctzll(m);
-                break;
+    uint32_t pend = smax < (int64_t)seg_lo ? seg_lo : (uint32_t)(smax + 1);  // probe [seg_lo, pend)
+#if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 1  // diagnostic builds only: staging + prewarm
+    if (dw[lane] == 0x12345678u) pend = 0;
+    pend = seg_lo;
+#endif
+    for (uint32_t sb = seg_lo; sb < pend; sb += kSub) {
+        const uint32_t sb_end = sb + kSub < pend ? sb + kSub : pend;
+        // ---- candidates + match measurements for [sb, sb_end)
+        uint64_t mymask = 0;
+        for (uint32_t x0 = sb; x0 < sb_end; x0 += 64) {
+            const uint32_t P = x0 + lane;
+            const bool valid = P < sb_end;
+            const uint32_t i = P - pw_lo;
+            const uint32_t a = i >> 2, sh = i & 3;
+            const uint32_t w0 = dw[a], w1 = dw[a + 1], wp = a ? dw[a - 1] : 0u;
+            const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            const uint32_t vm4 = __builtin_amdgcn_alignbyte(w0, wp, sh);  // bytes [P-4, P)
+            const uint32_t h = hash4(v);
+            const uint32_t c16 = tbl[h];
+            uint32_t c = pw_lo + c16;
+            bool good = valid && c16 != kEmpty && c < P && lds32u(inb, c16) == v;
+            if (!good && valid) {
+                if (i >= 1 && __builtin_amdgcn_alignbyte(v, vm4, 3) == v) { good = true; c = P - 1; }
+                else if (i >= 2 && __builtin_amdgcn_alignbyte(v, vm4, 2) == v) { good = true; c = P - 2; }
+                else if (i >= 3 && __builtin_amdgcn_alignbyte(v, vm4, 1) == v) { good = true; c = P - 3; }
+                else if (i >= 4 && vm4 == v) { good = true; c = P - 4; }
             }
-            if (nb > lim) nb = lim;
-            p -= nb;
-            cc -= nb;
-            // forward extension
-            const uint32_t maxlen = end_lim - p;
-            uint32_t len = nb + 4;
-            for (;;) {
-                const uint32_t rel = len + 4u * lane;
-                uint32_t eqb;
-                if (rel >= maxlen) {
-                    eqb = 0;
-                } else {
-                    uint32_t ia = p + rel - pw_lo, ib = cc + rel - pw_lo;
-                    if (ia > kIn - 8) ia = kIn - 8;
-                    const uint32_t x = lds32u(inb, ia), y = lds32u(inb, ib);
-                    eqb = x == y ? 4u : (uint32_t)__builtin_ctz(x ^ y) >> 3;
-                    if (eqb > maxlen - rel) eqb = maxlen - rel;
+            if (valid) tbl[h] = (uint16_t)i;
+            uint32_t word = 0;
+            if (good) {
+                const uint32_t ci = c - pw_lo;
+                // forward: bytes [P+4, P+20) against [c+4, c+20)
+                const uint32_t pa = (i + 4) >> 2, ps = (i + 4) & 3;
+                const uint32_t ca = (ci + 4) >> 2, cs = (ci + 4) & 3;
+                const uint32_t x0w = dw[pa], x1w = dw[pa + 1], x2w = dw[pa + 2], x3w = dw[pa + 3], x4w = dw[pa + 4];
+                const uint32_t y0w = dw[ca], y1w = dw[ca + 1], y2w = dw[ca + 2], y3w = dw[ca + 3], y4w = dw[ca + 4];
+                const uint32_t d0 = __builtin_amdgcn_alignbyte(x1w, x0w, ps) ^ __builtin_amdgcn_alignbyte(y1w, y0w, cs);
+                const uint32_t d1 = __builtin_amdgcn_alignbyte(x2w, x1w, ps) ^ __builtin_amdgcn_alignbyte(y2w, y1w, cs);
+                const uint32_t d2 = __builtin_amdgcn_alignbyte(x3w, x2w, ps) ^ __builtin_amdgcn_alignbyte(y3w, y2w, cs);
+                const uint32_t d3 = __builtin_amdgcn_alignbyte(x4w, x3w, ps) ^ __builtin_amdgcn_alignbyte(y4w, y3w, cs);
+                uint32_t len = d0 ? 4 + (__builtin_ctz(d0) >> 3)
+                             : d1 ? 8 + (__builtin_ctz(d1) >> 3)
+                             : d2 ? 12 + (__builtin_ctz(d2) >> 3)
+                             : d3 ? 16 + (__builtin_ctz(d3) >> 3) : 20u;
+                if (len > kFwd) len = kFwd;
+                const uint32_t maxf = end_lim - P;  // >= 4 for P <= smax
+                if (len > maxf) len = maxf;
+                // backward: up to 4 bytes before P and c (c-4 .. c-1 must be staged)
+                uint32_t nb = 0;
+                if (ci >= 1) {
+                    const uint32_t cm4 = ci >= 4 ? lds32u(inb, ci - 4) : (lds32u(inb, 0) << (8 * (4 - ci)));
+                    const uint32_t dx = vm4 ^ cm4;
+                    nb = dx ? (uint32_t)__builtin_clz(dx) >> 3 : 4u;
+                    const uint32_t lim = ci < i ? ci : i;
+                    if (nb > lim) nb = lim;
                 }
-                const uint64_t m = __ballot(eqb != 4u);
-                if (m == 0) { len += 256; continue; }
-                const uint32_t g = (uint32_t)__builtin_ctzll(m);
-                len += 4u * g + rdl(eqb, g);
-                break;
+                word = (P - c) | ((len - 4) << 16) | (nb << 24);
             }
-            const uint32_t ll = p - lit_start;
-            const uint32_t off = p - cc;
-            if (nseq == 0) {
-                ll0 = ll;
-                body += ll + 2 + ext_bytes(len - 4);
-            } else {
-                body += 1 + ext_bytes(ll) + ll + 2 + ext_bytes(len - 4);
+            if (valid) info[P - sb] = word;
+            const uint64_t m = __ballot(good);
+            if ((uint32_t)lane == ((x0 - sb) >> 6)) mymask = m;
+        }
+        wave_sync();
+#if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 2  // + candidate pass
+        if (mymask == 12345ull) body += 1;
+        continue;
+#endif
+        // ---- next-match descriptors: nd[x] = dist(x -> next match P) | off << 9 | (lenf-4) << 25 | nb << 29
+        {
+            const uint32_t nch = (sb_end - sb + 63) >> 6;
+            // first match position of chunk c or any later chunk (relative to sb), lane c
+            const uint32_t firstc = mymask ? (uint32_t)(lane * 64) + (uint32_t)__builtin_ctzll(mymask) : 0xFFFFu;
+            uint32_t later = 0xFFFFu;  // first match in the chunks after this lane's chunk
+            uint32_t run = 0xFFFFu;
+            for (int c2 = (int)nch - 1; c2 >= 0; --c2) {
+                if (lane == c2) later = run;
+                const uint32_t f2 = rdl(firstc, (uint32_t)c2);
+                if (f2 != 0xFFFFu) run = f2;
             }
-            if ((uint32_t)lane == (nseq & 63)) {
-                rx = ll | (len << 16);
-                ry = off;
+            for (uint32_t ck = 0; ck < nch; ++ck) {
+                const uint32_t xr = ck * 64 + lane;  // x - sb
+                if (sb + xr >= sb_end) break;
+                const uint64_t mk = rdl64(mymask, ck) & (~0ull << lane);
+                const uint32_t lat = rdl(later, ck);
+                const uint32_t pr = mk ? ck * 64 + (uint32_t)__builtin_ctzll(mk) : lat;
+                uint32_t d = 0;
+                if (pr != 0xFFFFu) {
+                    const uint32_t w = info[pr];
+                    d = (pr - xr) | ((w & 0xFFFFu) << 9) | (((w >> 16) & 15u) << 25) | ((w >> 24) << 29);
+                }
+                nd[xr] = d;
+            }
+        }
+        wave_sync();
+#if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 3  // + descriptor pass
+        if (nd[lane] == 12345u) body += 1;
+        continue;
+#endif
+        // ---- greedy walk through [sb, sb_end)
+        for (;;) {
+            const uint32_t x = lit_start > sb ? lit_start : sb;
+            if (x >= sb_end) break;
+            const uint32_t d = nd[x - sb];
+            if (((d >> 9) & 0xFFFFu) == 0) break;  // no match left in this sub-block
+            const uint32_t P = x + (d & 511u);
+            uint32_t lenf = 4 + ((d >> 25) & 15u);
+            if (lenf == kFwd) {  // long match: wave-wide forward extension
+                const uint32_t maxf = end_lim - P;
+                const uint32_t c = P - ((d >> 9) & 0xFFFFu);
+                while (lenf < maxf) {
+                    const uint32_t rel = lenf + 4u * lane;
+                    uint32_t e2;
+                    if (rel >= maxf) {
+                        e2 = 0;
+                    } else {
+                        uint32_t ia = P + rel - pw_lo;
+                        if (ia > kIn - 8) ia = kIn - 8;
+                        const uint32_t xa = lds32u(inb, ia), ya = lds32u(inb, c + rel - pw_lo);
+                        e2 = xa == ya ? 4u : (uint32_t)__builtin_ctz(xa ^ ya) >> 3;
+                        if (e2 > maxf - rel) e2 = maxf - rel;
+                    }
+                    const uint64_t m2 = __ballot(e2 != 4u);
+                    if (m2 == 0) { lenf += 256; continue; }
+                    const uint32_t g = (uint32_t)__builtin_ctzll(m2);
+                    lenf += 4u * g + rdl(e2, g);
+                    break;
+                }
+            }
+            const uint32_t j = nseq & 63;
+            if ((uint32_t)lane == j) {
+                hP = P;
+                hW = d;
+                hL = lenf;
             }
             nseq++;
-            if ((nseq & 63) == 0) {
-                myrec[nseq - 64 + lane] = make_uint2(rx, ry);
+            lit_start = P + lenf;
+            if (j == 63) {
+                enc_flush_group(lane, 64, nseq - 64, gls, hP, hW, hL, myrec, body, ll0);
+                gls = lit_start;
             }
-            lit_start = p + len;
-            W = lit_start;
-            if (lane == 0) {  // as lz4_flex: remember the position two bytes before the match end
-                const uint32_t x = lit_start - 2;
-                tbl[hash4(lds32u(inb, x - pw_lo))] = (uint16_t)(x - pw_lo);
-            }
-            wave_sync();
         }
     }
-    if (nseq & 63) {
-        if ((uint32_t)lane < (nseq & 63)) myrec[(nseq & ~63u) + lane] = make_uint2(rx, ry);
-    }
+    if (nseq & 63) enc_flush_group(lane, nseq & 63, nseq & ~63u, gls, hP, hW, hL, myrec, body, ll0);
     if (lane == 0) {
         SegSummary S;
         S.nseq = nseq;

@@ -16,7 +16,7 @@ import subprocess
 from dataclasses import dataclass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libs3hc_lz4.so")
+LIB_PATH = os.environ.get("S3HC_LIB_PATH") or os.path.join(_HERE, "libs3hc_lz4.so")  # override: diagnostic builds only
 
 S3HC_OK, S3HC_CORRUPT, S3HC_CHECKSUM, S3HC_DST_TOO_SMALL = 0, 1, 2, 3
 S3HC_UNSUPPORTED, S3HC_DEVICE, S3HC_INVALID_ARG = 4, 5, 6
