@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "sample-s3-hybrid-cache_amd")]
 
 import s3hc_lz4 as S  # noqa: E402
+import shard  # noqa: E402
 import synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.3 measured)
@@ -39,50 +40,13 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--blocks", type=int, default=4096, help="64 KiB blocks per GPU (config 2: 4096)")
+    ap.add_argument("--blocks", type=int, default=4096, help="64 KiB blocks per GPU (config 2: 4096; weak scaling)")
+    ap.add_argument("--total-blocks", type=int, default=0,
+                    help="strong scaling instead: split this many blocks over the ranks (config 5: 1048576)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--skip-check", action="store_true", help="diagnostic builds only: skip output checks")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall seconds of the CPU baseline sample")
     return ap.parse_args()
-
-
-def dist_setup(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    pg = None
-    if world > 1:
-        import torch.distributed as dist  # gloo on CPU: barrier + max reduction only
-
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        pg = dist
-    return world, rank, local, pg
-
-
-def barrier(pg):
-    if pg is not None:
-        pg.barrier()
-
-
-def allmax(pg, x: float) -> float:
-    if pg is None:
-        return x
-    import torch
-
-    t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.MAX)
-    return float(t.item())
-
-
-def allsum(pg, x: float) -> float:
-    if pg is None:
-        return x
-    import torch
-
-    t = torch.tensor([x], dtype=torch.float64)
-    pg.all_reduce(t, op=pg.ReduceOp.SUM)
-    return float(t.item())
 
 
 def cpu_baseline(data: bytes, block: int, seconds: float):
@@ -100,12 +64,13 @@ def cpu_baseline(data: bytes, block: int, seconds: float):
     base = ctypes.addressof(buf)
     cap = O.lib().or_frame_bound(block)
 
-    def work(lo, hi):
+    def work(lo, count):
         fr = ctypes.create_string_buffer(cap)
         out = ctypes.create_string_buffer(block)
         n = ctypes.c_size_t()
         te = td = 0.0
-        for i in range(lo, hi):
+        for k in range(count):
+            i = (lo + k) % nb
             t0 = time.perf_counter()
             L.or_lz4flex_compress_frame(base + i * block, block, fr, cap, ctypes.byref(n))
             t1 = time.perf_counter()
@@ -115,17 +80,17 @@ def cpu_baseline(data: bytes, block: int, seconds: float):
             assert rc == 0 and m.value == block
             te += t1 - t0
             td += t2 - t1
-        return te, td, hi - lo
+        return te, td, count
 
-    # single thread: how many blocks per second
+    # single thread: seconds per block (encode + decode)
     te, td, k = work(0, min(nb, 64))
     per_blk = (te + td) / k
-    # all threads: contiguous block ranges per thread (one request per blocking thread)
-    per_thread = max(1, min(nb // threads, int(seconds / per_blk)))
+    # all threads, each on its own contiguous block range (one request per blocking thread),
+    # sized to ~`seconds` of wall time
+    per_thread = max(1, int(seconds / per_blk))
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
-        futs = [ex.submit(work, (t * per_thread) % max(1, nb - per_thread), (t * per_thread) % max(1, nb - per_thread) + per_thread)
-                for t in range(threads)]
+        futs = [ex.submit(work, (t * nb) // threads, per_thread) for t in range(threads)]
         res = [f.result() for f in futs]
     wall = time.perf_counter() - t0
     blocks = sum(r[2] for r in res)
@@ -134,8 +99,9 @@ def cpu_baseline(data: bytes, block: int, seconds: float):
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{blocks} x 64 KiB blocks of the same log-text batch, lz4_flex-faithful encode + decode_data per block, "
-                  f"{threads} threads over contiguous block ranges, {wall:.2f} s wall",
+        "sample": f"{blocks} x 64 KiB blocks of the same log-text batch (lz4_flex-faithful frame encode + decompress_data "
+                  f"per block, oracle/ C port -O3), {threads} threads over contiguous block ranges, {wall:.2f} s wall "
+                  f"= {wall * threads:.1f} CPU-s",
         "single_thread_gibps": round(block / per_blk / GiB, 4),
         "single_thread_encode_gibps": round(k * block / te / GiB, 4),
         "single_thread_decode_gibps": round(k * block / td / GiB, 4),
@@ -145,10 +111,15 @@ def cpu_baseline(data: bytes, block: int, seconds: float):
 
 def main():
     args = parse_args()
-    world, rank, local, pg = dist_setup(args)
+    g = shard.Group()
+    world, rank, local = g.world, g.rank, g.local
     block = 65536
-    nb = args.blocks
-    eng = S.Engine(local)
+    if args.total_blocks:
+        lo, hi = shard.shard_range(args.total_blocks, world, rank)
+        nb = hi - lo
+    else:
+        nb = args.blocks
+    eng = S.Engine(local % max(1, S.device_count()))  # one process per GPU (shared GPU only in CPU-box rehearsals)
 
     # ---- synthetic batch, resident in HBM before timing (distinct data per rank)
     data = synth.log_text(nb * block, synth.SEED_BASE + 1 + 1000 * rank)
@@ -182,16 +153,16 @@ def main():
 
     eng.timing_reset()
     eng.set_timing(True)
-    barrier(pg)
+    g.barrier()
     eng.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     eng.sync()
     t1 = time.perf_counter()
-    barrier(pg)
+    g.barrier()
     eng.set_timing(False)
-    elapsed = allmax(pg, t1 - t0)
+    elapsed = g.max(t1 - t0)
     kt = eng.timing()
 
     # full-output check after the timed steps
@@ -199,7 +170,7 @@ def main():
         assert d_ost.i32(nb) == [0] * nb
         assert d_out.read() == data, "decoded batch differs from the input"
 
-    total_u = allsum(pg, float(nb * block)) * args.steps
+    total_u = g.sum(float(nb * block)) * args.steps
     value = total_u / elapsed / GiB
 
     # ---- roofline for the dominant kernel
@@ -236,12 +207,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.total_blocks else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic S3 access-log text (SURVEY.md §8d config 2), seeded, distinct per rank",
             "config": {
-                "workload": "config2: 4096 x 64 KiB log-text blocks per GPU, LZ4 frame encode + decode, device-resident",
+                "workload": (f"config5: {args.total_blocks} x 64 KiB log-text blocks split over {world} GPUs" if args.total_blocks
+                             else f"config2: {nb} x 64 KiB log-text blocks per GPU") + ", LZ4 frame encode + decode, device-resident",
                 "blocks_per_gpu": nb, "block_bytes": block, "frame": "FLG 0x64 BD 0x40 (lz4_flex Auto), xxh32 content checksum",
                 "compression_ratio": round(comp_bytes / (nb * block), 4), "parallelism": f"shard{world}",
             },
@@ -250,8 +222,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
-    if pg is not None:
-        pg.destroy_process_group()
+    g.close()
 
 
 if __name__ == "__main__":

@@ -46,6 +46,7 @@ typedef struct s3hc_plan s3hc_plan;
 /* One context per device; internally locked, safe to share between threads (the
  * reference calls the codec from many spawn_blocking threads, http_proxy.rs:11608). */
 int s3hc_create(s3hc_ctx** out, int device);
+int s3hc_device_count(void);
 void s3hc_destroy(s3hc_ctx* ctx);
 const char* s3hc_last_error(void);
 const char* s3hc_version(void);

@@ -312,6 +312,10 @@ extern "C" int s3hc_create(s3hc_ctx** out, int device) {
     *out = c.release();
     return S3HC_OK;
 }
+extern "C" int s3hc_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
 extern "C" void s3hc_destroy(s3hc_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);

@@ -49,6 +49,7 @@ def _load():
     sig = {
         "s3hc_create": (i32, [ctypes.POINTER(vp), i32]),
         "s3hc_destroy": (None, [vp]),
+        "s3hc_device_count": (i32, []),
         "s3hc_last_error": (ctypes.c_char_p, []),
         "s3hc_version": (ctypes.c_char_p, []),
         "s3hc_frame_bound": (sz, [sz]),
@@ -116,6 +117,10 @@ def _check(rc: int):
 def is_denylisted_extension(path: str) -> bool:
     """CompressionHandler::is_denylisted_extension (compression.rs:252-255)."""
     return bool(lib.s3hc_is_denylisted_extension(path.encode()))
+
+
+def device_count() -> int:
+    return lib.s3hc_device_count()
 
 
 def frame_bound(n: int) -> int:

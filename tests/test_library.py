@@ -1,0 +1,75 @@
+"""CPU-side checks of the product library: it builds, loads, exports every symbol the C
+header declares, and fails loudly (S3HC_DEVICE) without a GPU instead of falling back."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "s3hc_lz4.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(s3hc_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_header_symbols():
+    import s3hc_lz4 as S
+
+    lib = ctypes.CDLL(S.LIB_PATH)
+    names = declared_functions()
+    assert len(names) >= 40
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_no_oracle_in_product():
+    import s3hc_lz4 as S
+
+    data = open(S.LIB_PATH, "rb").read()
+    assert b"or_decompress_data" not in data and b"lz4_oracle" not in data
+
+
+def test_create_without_gpu_fails_loudly():
+    import s3hc_lz4 as S
+
+    h = ctypes.c_void_p()
+    rc = S.lib.s3hc_create(ctypes.byref(h), 0)
+    if rc == S.S3HC_OK:
+        S.lib.s3hc_destroy(h)
+        pytest.skip("a GPU is present")
+    assert rc == S.S3HC_DEVICE
+    assert b"no HIP device" in S.lib.s3hc_last_error()
+
+
+@pytest.mark.parametrize("path,want", [
+    ("file.txt", False), ("path/to/file.json", False), ("bucket/folder/image.jpg", True), ("file.tar.gz", True),
+    ("noextension", False), ("", False), ("bucket/images/photo.JPG", True), ("deep/nested/path/archive.zip", True),
+    ("clip.mp4", True), ("doc.pdf", True), ("index.html", False), ("x.woff2", True), ("a.db", True),
+])
+def test_denylist(path, want):
+    # compression.rs:750-846 (extension extraction + denylist)
+    import s3hc_lz4 as S
+
+    assert S.is_denylisted_extension(path) is want
+
+
+def test_decompressed_bound_host_walk(oracle):
+    import s3hc_lz4 as S
+
+    for data in (b"", b"x" * 10, bytes(i % 251 for i in range(300_000))):
+        f = oracle.lz4flex_compress_frame(data) + oracle.store_mode_frame(data)
+        b = ctypes.c_size_t()
+        assert S.lib.s3hc_decompressed_bound(f, len(f), ctypes.byref(b)) == 0
+        assert b.value >= 2 * len(data)
+        assert b.value == oracle.decompressed_bound(f)
+
+
+def test_frame_bound():
+    import s3hc_lz4 as S
+
+    for n in (0, 1, 65535, 65536, 65537, 1 << 20, 5 << 20):
+        assert S.frame_bound(n) >= n + 4 * (n // 65536 + 1) + 15
