@@ -58,15 +58,32 @@ __device__ __forceinline__ uint32_t gld32u(const uint8_t* p, uint32_t avail) {
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
-    }
-    return x - v;
+// DPP lane moves (GFX9 row_shr / row_bcast): lanes without a source read 0.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, 0xF, false);
 }
+// Inclusive wave-wide sum / max (Hillis-Steele inside 16-lane rows, then row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += dpp0<0x111, 0xF>(x);
+    x += dpp0<0x112, 0xF>(x);
+    x += dpp0<0x114, 0xF>(x);
+    x += dpp0<0x118, 0xF>(x);
+    x += dpp0<0x142, 0xA>(x);
+    x += dpp0<0x143, 0xC>(x);
+    return x;
+}
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = umax32(x, dpp0<0x111, 0xF>(x));
+    x = umax32(x, dpp0<0x112, 0xF>(x));
+    x = umax32(x, dpp0<0x114, 0xF>(x));
+    x = umax32(x, dpp0<0x118, 0xF>(x));
+    x = umax32(x, dpp0<0x142, 0xA>(x));
+    x = umax32(x, dpp0<0x143, 0xC>(x));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int) { return wave_incl_sum(v) - v; }
 
 // Wave-cooperative copy of n bytes global -> global, any alignment of either side.
 // Loads for up to 4 KiB are issued before the stores.
@@ -189,7 +206,8 @@ constexpr uint32_t kStage = 512;   // compressed bytes staged per wave
 constexpr uint32_t kRing = 4096;   // recent output kept in LDS per wave (match sources)
 constexpr uint32_t kMask = kRing - 1;
 constexpr uint32_t kFlush = 1024;  // ring -> HBM flush granule
-constexpr uint32_t kWaveLds = kRing + kStage + 64;
+constexpr uint32_t kWin = 1024;    // output bytes executed per window (byte-parallel)
+constexpr uint32_t kWaveLds = kRing + kStage + (kWin + 64) + 2 * kWin;
 constexpr int kWaves = 4;
 enum : uint32_t { F_ERR = 1, F_LAST = 2, F_LONG = 4, F_MORE = 8 };
 }  // namespace dec
@@ -197,6 +215,8 @@ enum : uint32_t { F_ERR = 1, F_LAST = 2, F_LONG = 4, F_MORE = 8 };
 struct DecWave {
     uint8_t* ring;
     uint8_t* stage;
+    uint8_t* marks;      // kWin + 64 bytes: sequence start marks of the current window
+    uint16_t* refs;      // kWin entries: in-window match source of each output byte
     uint8_t* out;        // unit output base in HBM
     uint32_t upos;       // bytes produced in this unit
     uint32_t flushed;    // bytes of the unit already written to HBM
@@ -302,6 +322,115 @@ __device__ __forceinline__ int dec_ext_scan(const uint8_t* in, uint32_t C, uint3
     }
 }
 
+// One sequence executed wave-wide (literal run, then match unless `last`), with the lz4_flex
+// bound checks in stream order. Used for sequences too long for a window.
+__device__ __forceinline__ int dec_seq(DecWave& w, const uint8_t* in, uint32_t lit, uint32_t ll, bool last,
+                                       uint32_t off, uint32_t ml, uint32_t st_lo, uint32_t bstart,
+                                       uint32_t limit, uint32_t cap, uint32_t hist) {
+    const uint32_t produced = w.upos - bstart;
+    if (ll > limit - produced) return S3HC_CORRUPT;
+    if (ll > cap - produced) return S3HC_DST_TOO_SMALL;
+    dec_literals(w, in, lit, ll, st_lo, lit >= st_lo && lit + ll <= st_lo + dec::kStage);
+    if (last) return S3HC_OK;
+    const uint32_t have = w.upos - bstart;
+    if (off == 0 || off > have + hist) return S3HC_CORRUPT;
+    if (ml > limit - have) return S3HC_CORRUPT;
+    if (ml > cap - have) return S3HC_DST_TOO_SMALL;
+    dec_match(w, off, ml);
+    return S3HC_OK;
+}
+
+// Executes the window's member sequences (lanes set in `members`, S output bytes in total,
+// S <= kWin) byte-parallel: every output byte finds its sequence (start marks + max-scan),
+// literal bytes and match bytes whose source precedes the window are written at once, and
+// match bytes whose source lies inside the window follow the source chain (refs) to a byte
+// written in the first pass. A fixed handful of LDS round trips per window instead of two per
+// sequence.
+__device__ int dec_window(DecWave& w, uint64_t members, uint32_t S, uint32_t flags, uint32_t lit, uint32_t ll,
+                          uint32_t off, uint32_t ml, uint32_t st_lo, uint32_t bstart, uint32_t limit,
+                          uint32_t cap, uint32_t hist) {
+    using namespace dec;
+    const int lane = w.lane;
+    const bool isM = (members >> lane) & 1ull;
+    const bool last = (flags & F_LAST) != 0;
+    const uint32_t sl = isM ? ll + (last ? 0u : ml) : 0u;
+    const uint32_t orel = wave_excl_scan(sl, lane);
+    // bound checks, lane-parallel; the first failing member in stream order decides
+    {
+        const uint32_t produced = w.upos - bstart + orel;
+        int st = S3HC_OK;
+        if (isM) {
+            if (ll > limit - produced) st = S3HC_CORRUPT;
+            else if (ll > cap - produced) st = S3HC_DST_TOO_SMALL;
+            else if (!last) {
+                const uint32_t have = produced + ll;
+                if (off == 0 || off > have + hist) st = S3HC_CORRUPT;
+                else if (ml > limit - have) st = S3HC_CORRUPT;
+                else if (ml > cap - have) st = S3HC_DST_TOO_SMALL;
+            }
+        }
+        const uint64_t bad = __ballot(st != S3HC_OK);
+        if (bad) return (int)rdl((uint32_t)st, (uint32_t)__builtin_ctzll(bad));
+    }
+    uint8_t* marks = w.marks;
+    uint16_t* refs = w.refs;
+    for (uint32_t k = lane; k < ((S + 3) >> 2); k += 64) ((uint32_t*)marks)[k] = 0u;
+    wave_sync();
+    if (isM && sl) marks[orel] = (uint8_t)(lane + 1);
+    wave_sync();
+    const uint32_t pkA = orel | (ll << 16);
+    const uint32_t pkB = off | ((lit - st_lo) << 16);
+    const uint32_t upos = w.upos;
+    uint32_t carry = 0;
+    bool pend = false;
+    for (uint32_t b = 0; b < S; b += 64) {
+        const uint32_t t = b + lane;
+        const bool v = t < S;
+        uint32_t mk = wave_incl_max(v ? (uint32_t)marks[t] : 0u);
+        mk = mk > carry ? mk : carry;
+        carry = rdl(mk, 63);
+        const int m = (int)mk - 1;
+        const uint32_t A = __shfl(pkA, m), B = __shfl(pkB, m);
+        if (v) {
+            const uint32_t mo = A & 0xFFFFu, mll = A >> 16, moff = B & 0xFFFFu, mlit = B >> 16;
+            const uint32_t x = upos + t;
+            const uint32_t dd = t - mo;
+            uint32_t ref = 0xFFFFu;
+            uint32_t val = 0;
+            if (dd < mll) {
+                val = w.stage[mlit + dd];
+            } else {
+                uint32_t e = dd - mll;
+                const uint32_t ms = x - e;  // match start
+                if (e >= moff) e %= moff;   // overlapping match: period moff
+                const uint32_t y = ms - moff + e;
+                if (y >= upos) { ref = y - upos; pend = true; }
+                else if (y + (kRing - S) >= upos) val = w.ring[y & kMask];
+                else val = w.out[y];        // older than the ring: already in HBM
+            }
+            if (ref == 0xFFFFu) w.ring[x & kMask] = (uint8_t)val;
+            refs[t] = (uint16_t)ref;
+        }
+    }
+    if (__ballot(pend)) {
+        wave_sync();
+        for (uint32_t b = 0; b < S; b += 64) {
+            const uint32_t t = b + lane;
+            if (t < S) {
+                uint32_t z = refs[t];
+                if (z != 0xFFFFu) {
+                    for (uint32_t r = refs[z]; r != 0xFFFFu; r = refs[z]) z = r;
+                    w.ring[(upos + t) & kMask] = w.ring[(upos + z) & kMask];
+                }
+            }
+        }
+    }
+    wave_sync();
+    w.upos = upos + S;
+    dec_maybe_flush(w);
+    return S3HC_OK;
+}
+
 // Decode one compressed block of C bytes. hist = bytes of earlier unit output matches may use.
 // Output overflowing `limit` is corruption (lz4_flex: output sink bounded by the block size);
 // overflowing only `cap` is DST_TOO_SMALL.
@@ -317,21 +446,24 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
             st_lo = q & ~3u;
             dec_stage(in, C, st_lo, w.stage, lane);
         }
-        // ---- speculative parse: lane assumes a token at qq = q + lane
+        // ---- speculative parse: lane assumes a token at qq = q + lane. Two LDS round trips:
+        // token + up to two length bytes, then offset + up to two match-length bytes.
         const uint32_t qq = q + lane;
         const uint32_t i = qq - st_lo;
         uint32_t flags = 0, nxt = 0, lit = 0, ll = 0, off = 0, ml = 0;
         {
-            const uint32_t t = w.stage[i];
+            const uint32_t w0 = lds32u(w.stage, i);
+            const uint32_t t = w0 & 0xFFu;
             uint32_t j = i + 1;
             ll = t >> 4;
             if (ll == 15) {
-                uint32_t e = w.stage[j++];
-                ll += e;
-                if (e == 255) {
-                    e = w.stage[j++];
-                    ll += e;
-                    if (e == 255) flags |= F_LONG;
+                const uint32_t e1 = (w0 >> 8) & 0xFFu, e2 = (w0 >> 16) & 0xFFu;
+                ll += e1;
+                j++;
+                if (e1 == 255) {
+                    ll += e2;
+                    j++;
+                    if (e2 == 255) flags |= F_LONG;
                 }
             }
             lit = st_lo + j;
@@ -340,32 +472,31 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
             } else {
                 const uint32_t mp = lit + ll;
                 if (mp == C) {
-                    flags |= F_LAST;
+                    flags |= (mp - st_lo > kStage) ? F_MORE : F_LAST;
                     nxt = C;
                 } else if (C - mp < 2) {
                     flags |= F_ERR;
                 } else if (mp - st_lo + 4 > kStage) {
                     flags |= F_MORE;
                 } else {
-                    const uint32_t mi = mp - st_lo;
-                    off = (uint32_t)w.stage[mi] | ((uint32_t)w.stage[mi + 1] << 8);
+                    const uint32_t w1 = lds32u(w.stage, mp - st_lo);
+                    off = w1 & 0xFFFFu;
                     uint32_t k = mp + 2;
                     ml = (t & 15) + 4;
                     if ((t & 15) == 15) {
+                        const uint32_t e1 = (w1 >> 16) & 0xFFu, e2 = w1 >> 24;
                         if (k >= C) {
                             flags |= F_ERR;
                         } else {
-                            uint32_t e = w.stage[k - st_lo];
                             k++;
-                            ml += e;
-                            if (e == 255) {
+                            ml += e1;
+                            if (e1 == 255) {
                                 if (k >= C) {
                                     flags |= F_ERR;
                                 } else {
-                                    e = w.stage[k - st_lo];
                                     k++;
-                                    ml += e;
-                                    if (e == 255) flags |= F_LONG;
+                                    ml += e2;
+                                    if (e2 == 255) flags |= F_LONG;
                                 }
                             }
                         }
@@ -374,39 +505,43 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
                 }
             }
         }
-        // ---- walk the true token chain through the window (scalar)
+        const uint32_t sl = ll + ((flags & F_LAST) ? 0u : ml);
+        // chain word: flags | sequence output length | next token position (window-relative)
+        const uint32_t pk = flags | ((sl & 0xFFFu) << 4) | ((nxt - q) << 16);
+        // ---- walk the true token chain through the window (scalar), up to kWin output bytes
         uint64_t members = 0;
-        uint32_t cur = q;
-        int stop = 0;  // 0 window exhausted, 1 last sequence, 2 error, 3 slow path at cur
+        uint32_t l = 0, S = 0;
+        int stop = 0;  // 0 window exhausted, 1 last sequence, 2 error, 3 slow path at l, 4 long sequence
         for (;;) {
-            uint32_t l = cur - q;
             if (l >= 64) break;
-            uint32_t f = rdl(flags, l);
-            if (f & (F_LONG | F_MORE)) { stop = 3; break; }
-            if (f & F_ERR) { stop = 2; break; }
+            const uint32_t pw = rdl(pk, l);
+            if (pw & (F_LONG | F_MORE)) { stop = 3; break; }
+            if (pw & F_ERR) { stop = 2; break; }
+            const uint32_t s = (pw >> 4) & 0xFFFu;
+            if (S + s > kWin) {
+                if (members == 0) stop = 4;
+                break;
+            }
+            S += s;
             members |= 1ull << l;
-            if (f & F_LAST) { stop = 1; break; }
-            cur = rdl(nxt, l);
+            if (pw & F_LAST) { stop = 1; break; }
+            l = pw >> 16;
         }
-        // ---- execute the chain in order
-        while (members) {
-            const uint32_t l = (uint32_t)__builtin_ctzll(members);
-            members &= members - 1;
-            const uint32_t mlit = rdl(lit, l), mll = rdl(ll, l), mf = rdl(flags, l);
-            const uint32_t produced = w.upos - bstart;
-            if (mll > limit - produced) return S3HC_CORRUPT;
-            if (mll > cap - produced) return S3HC_DST_TOO_SMALL;
-            dec_literals(w, in, mlit, mll, st_lo, mlit >= st_lo && mlit + mll <= st_lo + kStage);
-            if (mf & F_LAST) break;
-            const uint32_t moff = rdl(off, l), mml = rdl(ml, l);
-            const uint32_t have = w.upos - bstart;
-            if (moff == 0 || moff > have + hist) return S3HC_CORRUPT;
-            if (mml > limit - have) return S3HC_CORRUPT;
-            if (mml > cap - have) return S3HC_DST_TOO_SMALL;
-            dec_match(w, moff, mml);
+        uint32_t cur = q + l;
+        if (members) {
+            const int rc = dec_window(w, members, S, flags, lit, ll, off, ml, st_lo, bstart, limit, cap, hist);
+            if (rc) return rc;
         }
         if (stop == 1) return S3HC_OK;
         if (stop == 2) return S3HC_CORRUPT;
+        if (stop == 4) {
+            const uint32_t f = rdl(flags, l);
+            const int rc = dec_seq(w, in, rdl(lit, l), rdl(ll, l), (f & F_LAST) != 0, rdl(off, l), rdl(ml, l),
+                                   st_lo, bstart, limit, cap, hist);
+            if (rc) return rc;
+            if (f & F_LAST) return S3HC_OK;
+            cur = rdl(nxt, l);
+        }
         if (stop == 3) {
             // Slow path: this sequence has long length runs or reaches past the stage.
             uint32_t pos = cur;
@@ -417,21 +552,17 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
             if (sll > C - pos) return S3HC_CORRUPT;
             const uint32_t slit = pos;
             pos += sll;
+            if (pos == C) return dec_seq(w, in, slit, sll, true, 0, 0, st_lo, bstart, limit, cap, hist);
             const uint32_t produced = w.upos - bstart;
             if (sll > limit - produced) return S3HC_CORRUPT;
             if (sll > cap - produced) return S3HC_DST_TOO_SMALL;
-            dec_literals(w, in, slit, sll, st_lo, slit >= st_lo && slit + sll <= st_lo + kStage);
-            if (pos == C) return S3HC_OK;
             if (C - pos < 2) return S3HC_CORRUPT;
             const uint32_t soff = (uint32_t)in[pos] | ((uint32_t)in[pos + 1] << 8);
             pos += 2;
             uint32_t sml = (t & 15) + 4;
             if ((t & 15) == 15 && dec_ext_scan(in, C, pos, sml, lane)) return S3HC_CORRUPT;
-            const uint32_t have = w.upos - bstart;
-            if (soff == 0 || soff > have + hist) return S3HC_CORRUPT;
-            if (sml > limit - have) return S3HC_CORRUPT;
-            if (sml > cap - have) return S3HC_DST_TOO_SMALL;
-            dec_match(w, soff, sml);
+            const int rc = dec_seq(w, in, slit, sll, false, soff, sml, st_lo, bstart, limit, cap, hist);
+            if (rc) return rc;
             cur = pos;
         }
         q = cur;
@@ -453,6 +584,8 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     DecWave w;
     w.ring = smem + wv * dec::kWaveLds;
     w.stage = w.ring + dec::kRing;
+    w.marks = w.stage + dec::kStage;
+    w.refs = (uint16_t*)(w.marks + dec::kWin + 64);
     w.out = dst + blk[U.first].dst_off;
     w.upos = 0;
     w.flushed = 0;
