@@ -41,6 +41,18 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Phase timers for diagnostic builds only (S3HC_DIAG_LEVEL 10): per-wave s_memtime sums into
+// g_prof, read back with s3hc_diag_prof. Compiled out of the shipped library.
+#if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 10
+#define S3HC_PROF 1
+__device__ unsigned long long g_prof[32];
+#define PROF_NOW() __builtin_amdgcn_s_memtime()
+#define PROF_ADD(arr, k, v) (arr)[k] += (v)
+#else
+#define PROF_NOW() 0ull
+#define PROF_ADD(arr, k, v) ((void)(v))
+#endif
+
 // 4 bytes at any LDS byte offset: two aligned dword reads + v_alignbyte.
 __device__ __forceinline__ uint32_t lds32u(const uint8_t* lds, uint32_t i) {
     const uint32_t* w = (const uint32_t*)(lds + (i & ~3u));
@@ -218,6 +230,9 @@ struct DecWave {
     uint8_t* marks;      // kWin + 64 bytes: sequence start marks of the current window
     uint16_t* refs;      // kWin entries: in-window match source of each output byte
     uint8_t* out;        // unit output base in HBM
+#ifdef S3HC_PROF
+    uint64_t pr[16];
+#endif
     uint32_t upos;       // bytes produced in this unit
     uint32_t flushed;    // bytes of the unit already written to HBM
     int lane;
@@ -340,95 +355,80 @@ __device__ __forceinline__ int dec_seq(DecWave& w, const uint8_t* in, uint32_t l
     return S3HC_OK;
 }
 
-// Executes the window's member sequences (lanes set in `members`, S output bytes in total,
-// S <= kWin) byte-parallel: every output byte finds its sequence (start marks + max-scan),
-// literal bytes and match bytes whose source precedes the window are written at once, and
-// match bytes whose source lies inside the window follow the source chain (refs) to a byte
+// Byte-parallel execution of one window's sequences (lanes in `members`; S output bytes,
+// S <= kWin). Every output byte t finds its sequence (start marks + max-scan), literal bytes
+// and match bytes whose source precedes the window are written at once, and match bytes whose
+// source lies inside the window then follow the chain of in-window sources (refs) to a byte
 // written in the first pass. A fixed handful of LDS round trips per window instead of two per
-// sequence.
-__device__ int dec_window(DecWave& w, uint64_t members, uint32_t S, uint32_t flags, uint32_t lit, uint32_t ll,
-                          uint32_t off, uint32_t ml, uint32_t st_lo, uint32_t bstart, uint32_t limit,
-                          uint32_t cap, uint32_t hist) {
+// sequence, and almost no scalar work.
+__device__ __forceinline__ void dec_window_exec(DecWave& w, bool isM, uint32_t S, uint32_t orel, uint32_t sl,
+                                                uint32_t lit, uint32_t ll, uint32_t off, uint32_t st_lo) {
     using namespace dec;
     const int lane = w.lane;
-    const bool isM = (members >> lane) & 1ull;
-    const bool last = (flags & F_LAST) != 0;
-    const uint32_t sl = isM ? ll + (last ? 0u : ml) : 0u;
-    const uint32_t orel = wave_excl_scan(sl, lane);
-    // bound checks, lane-parallel; the first failing member in stream order decides
-    {
-        const uint32_t produced = w.upos - bstart + orel;
-        int st = S3HC_OK;
-        if (isM) {
-            if (ll > limit - produced) st = S3HC_CORRUPT;
-            else if (ll > cap - produced) st = S3HC_DST_TOO_SMALL;
-            else if (!last) {
-                const uint32_t have = produced + ll;
-                if (off == 0 || off > have + hist) st = S3HC_CORRUPT;
-                else if (ml > limit - have) st = S3HC_CORRUPT;
-                else if (ml > cap - have) st = S3HC_DST_TOO_SMALL;
-            }
-        }
-        const uint64_t bad = __ballot(st != S3HC_OK);
-        if (bad) return (int)rdl((uint32_t)st, (uint32_t)__builtin_ctzll(bad));
-    }
     uint8_t* marks = w.marks;
     uint16_t* refs = w.refs;
-    for (uint32_t k = lane; k < ((S + 3) >> 2); k += 64) ((uint32_t*)marks)[k] = 0u;
+    *(uint4*)(marks + 16 * lane) = make_uint4(0, 0, 0, 0);  // clears [0, kWin)
     wave_sync();
     if (isM && sl) marks[orel] = (uint8_t)(lane + 1);
     wave_sync();
     const uint32_t pkA = orel | (ll << 16);
     const uint32_t pkB = off | ((lit - st_lo) << 16);
     const uint32_t upos = w.upos;
-    uint32_t carry = 0;
-    bool pend = false;
+    uint32_t carry = 0, pendv = 0;
     for (uint32_t b = 0; b < S; b += 64) {
+        // lanes t >= S only compute (their reads stay inside this wave's LDS) and never write;
+        // they sit above every valid lane, so they do not disturb the scan
         const uint32_t t = b + lane;
-        const bool v = t < S;
-        uint32_t mk = wave_incl_max(v ? (uint32_t)marks[t] : 0u);
+        uint32_t mk = wave_incl_max((uint32_t)marks[t]);
         mk = mk > carry ? mk : carry;
         carry = rdl(mk, 63);
         const int m = (int)mk - 1;
         const uint32_t A = __shfl(pkA, m), B = __shfl(pkB, m);
-        if (v) {
-            const uint32_t mo = A & 0xFFFFu, mll = A >> 16, moff = B & 0xFFFFu, mlit = B >> 16;
-            const uint32_t x = upos + t;
-            const uint32_t dd = t - mo;
-            uint32_t ref = 0xFFFFu;
-            uint32_t val = 0;
-            if (dd < mll) {
-                val = w.stage[mlit + dd];
-            } else {
-                uint32_t e = dd - mll;
-                const uint32_t ms = x - e;  // match start
-                if (e >= moff) e %= moff;   // overlapping match: period moff
-                const uint32_t y = ms - moff + e;
-                if (y >= upos) { ref = y - upos; pend = true; }
-                else if (y + (kRing - S) >= upos) val = w.ring[y & kMask];
-                else val = w.out[y];        // older than the ring: already in HBM
-            }
-            if (ref == 0xFFFFu) w.ring[x & kMask] = (uint8_t)val;
-            refs[t] = (uint16_t)ref;
+        const uint32_t mo = A & 0xFFFFu, mll = A >> 16, moff = B & 0xFFFFu, mlit = B >> 16;
+        const uint32_t x = upos + t;
+        const uint32_t dd = t - mo;
+        const bool isLit = dd < mll;
+        uint32_t e = dd - mll;          // position inside the match
+        const uint32_t ms = x - e;      // match start
+        const bool wrap = !isLit && e >= moff && t < S;
+        if (__ballot(wrap)) e = wrap ? e % moff : e;  // overlapping match: period moff
+        const uint32_t y = ms - moff + e;
+        const uint8_t lv = w.stage[(mlit + dd) & (kStage - 1)];
+        const uint8_t rv = w.ring[y & kMask];
+        uint32_t val = isLit ? lv : rv;
+        const uint32_t ry = y - upos;  // < S when the source is inside the window
+        const bool pnd = !isLit && ry < S;
+        const bool old = !isLit && !pnd && y + (kRing - S) < upos && t < S;
+        if (__ballot(old)) val = old ? (uint32_t)w.out[y] : val;  // older than the ring: in HBM
+        if (t < S) {
+            w.ring[x & kMask] = (uint8_t)val;
+            refs[t] = (uint16_t)(pnd ? ry : 0xFFFFu);
         }
+        pendv |= (pnd && t < S) ? 1u : 0u;
     }
-    if (__ballot(pend)) {
+    if (__ballot(pendv)) {
         wave_sync();
         for (uint32_t b = 0; b < S; b += 64) {
             const uint32_t t = b + lane;
-            if (t < S) {
-                uint32_t z = refs[t];
-                if (z != 0xFFFFu) {
-                    for (uint32_t r = refs[z]; r != 0xFFFFu; r = refs[z]) z = r;
-                    w.ring[(upos + t) & kMask] = w.ring[(upos + z) & kMask];
-                }
+            const uint32_t z0 = t < S ? (uint32_t)refs[t] : 0xFFFFu;
+            const bool pl = z0 != 0xFFFFu;
+            if (!__ballot(pl)) continue;
+            uint32_t z = pl ? z0 : 0u;
+            for (;;) {
+                const uint32_t r = refs[z];
+                const bool more = pl && r != 0xFFFFu;
+                if (!__ballot(more)) break;
+                z = more ? r : z;
             }
+            const uint8_t v = w.ring[(upos + z) & kMask];
+            if (pl) w.ring[(upos + t) & kMask] = v;
         }
     }
     wave_sync();
     w.upos = upos + S;
+    const uint64_t tf = PROF_NOW();
     dec_maybe_flush(w);
-    return S3HC_OK;
+    PROF_ADD(w.pr, 10, PROF_NOW() - tf);
 }
 
 // Decode one compressed block of C bytes. hist = bytes of earlier unit output matches may use.
@@ -444,103 +444,116 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
         if (q >= C) return S3HC_CORRUPT;  // a token was expected
         if (st_lo == 0xFFFFFFFFu || q < st_lo || q + 192 > st_lo + kStage) {
             st_lo = q & ~3u;
+            const uint64_t t0 = PROF_NOW();
             dec_stage(in, C, st_lo, w.stage, lane);
+            PROF_ADD(w.pr, 0, PROF_NOW() - t0);
+            PROF_ADD(w.pr, 9, 1);
         }
-        // ---- speculative parse: lane assumes a token at qq = q + lane. Two LDS round trips:
-        // token + up to two length bytes, then offset + up to two match-length bytes.
+        const uint64_t tp0 = PROF_NOW();
+        // ---- speculative parse: lane assumes a token at qq = q + lane. Two LDS round trips
+        // (token + up to two length bytes; offset + up to two match-length bytes), no branches.
         const uint32_t qq = q + lane;
         const uint32_t i = qq - st_lo;
-        uint32_t flags = 0, nxt = 0, lit = 0, ll = 0, off = 0, ml = 0;
+        uint32_t flags, nxt, lit, ll, off, ml;
         {
             const uint32_t w0 = lds32u(w.stage, i);
-            const uint32_t t = w0 & 0xFFu;
-            uint32_t j = i + 1;
-            ll = t >> 4;
-            if (ll == 15) {
-                const uint32_t e1 = (w0 >> 8) & 0xFFu, e2 = (w0 >> 16) & 0xFFu;
-                ll += e1;
-                j++;
-                if (e1 == 255) {
-                    ll += e2;
-                    j++;
-                    if (e2 == 255) flags |= F_LONG;
-                }
-            }
-            lit = st_lo + j;
-            if (qq >= C || lit > C || ll > C - lit) {
-                flags |= F_ERR;
-            } else {
-                const uint32_t mp = lit + ll;
-                if (mp == C) {
-                    flags |= (mp - st_lo > kStage) ? F_MORE : F_LAST;
-                    nxt = C;
-                } else if (C - mp < 2) {
-                    flags |= F_ERR;
-                } else if (mp - st_lo + 4 > kStage) {
-                    flags |= F_MORE;
-                } else {
-                    const uint32_t w1 = lds32u(w.stage, mp - st_lo);
-                    off = w1 & 0xFFFFu;
-                    uint32_t k = mp + 2;
-                    ml = (t & 15) + 4;
-                    if ((t & 15) == 15) {
-                        const uint32_t e1 = (w1 >> 16) & 0xFFu, e2 = w1 >> 24;
-                        if (k >= C) {
-                            flags |= F_ERR;
-                        } else {
-                            k++;
-                            ml += e1;
-                            if (e1 == 255) {
-                                if (k >= C) {
-                                    flags |= F_ERR;
-                                } else {
-                                    k++;
-                                    ml += e2;
-                                    if (e2 == 255) flags |= F_LONG;
-                                }
-                            }
-                        }
-                    }
-                    nxt = k;
-                }
-            }
+            const uint32_t t = w0 & 0xFFu, L = t >> 4, M = t & 15u;
+            const uint32_t e1 = (w0 >> 8) & 0xFFu, e2 = (w0 >> 16) & 0xFFu;
+            const uint32_t x1 = L == 15u ? 1u : 0u, x2 = (L == 15u && e1 == 255u) ? 1u : 0u;
+            ll = L + (x1 ? e1 : 0u) + (x2 ? e2 : 0u);
+            lit = qq + 1u + x1 + x2;
+            const uint32_t mp = lit + ll;
+            const uint32_t mi = mp - st_lo;
+            const uint32_t w1 = lds32u(w.stage, mi < kStage ? mi : kStage);
+            off = w1 & 0xFFFFu;
+            const uint32_t f1 = (w1 >> 16) & 0xFFu, f2 = w1 >> 24;
+            const uint32_t y1 = M == 15u ? 1u : 0u, y2 = (M == 15u && f1 == 255u) ? 1u : 0u;
+            ml = M + 4u + (y1 ? f1 : 0u) + (y2 ? f2 : 0u);
+            nxt = mp + 2u + y1 + y2;
+            // precedence (lowest first): long match run, ext byte past the end, offset past the
+            // stage, offset cut off, last sequence, bad literal run
+            uint32_t fm = (y2 && f2 == 255u) ? F_LONG : 0u;
+            fm = (nxt > C) ? F_ERR : fm;
+            fm = (mi + 4 > kStage) ? F_MORE : fm;
+            fm = (C - mp < 2) ? F_ERR : fm;
+            fm = (mp == C) ? (mi > kStage ? F_MORE : F_LAST) : fm;
+            fm = (qq >= C || lit > C || ll > C - lit) ? F_ERR : fm;
+            flags = fm | ((x2 && e2 == 255u) ? F_LONG : 0u);
         }
-        const uint32_t sl = ll + ((flags & F_LAST) ? 0u : ml);
-        // chain word: flags | sequence output length | next token position (window-relative)
-        const uint32_t pk = flags | ((sl & 0xFFFu) << 4) | ((nxt - q) << 16);
-        // ---- walk the true token chain through the window (scalar), up to kWin output bytes
+        // ---- walk the true token chain through the window (scalar, one readlane per hop)
+        const bool term = (flags & (F_ERR | F_LONG | F_MORE | F_LAST)) != 0;
+        const uint32_t nx = term ? 64u : (nxt - q < 64u ? nxt - q : 64u);
         uint64_t members = 0;
-        uint32_t l = 0, S = 0;
-        int stop = 0;  // 0 window exhausted, 1 last sequence, 2 error, 3 slow path at l, 4 long sequence
-        for (;;) {
-            if (l >= 64) break;
-            const uint32_t pw = rdl(pk, l);
-            if (pw & (F_LONG | F_MORE)) { stop = 3; break; }
-            if (pw & F_ERR) { stop = 2; break; }
-            const uint32_t s = (pw >> 4) & 0xFFFu;
-            if (S + s > kWin) {
-                if (members == 0) stop = 4;
-                break;
-            }
-            S += s;
+        uint32_t l = 0, lastl;
+        do {
+            lastl = l;
             members |= 1ull << l;
-            if (pw & F_LAST) { stop = 1; break; }
-            l = pw >> 16;
+            l = rdl(nx, l);
+        } while (l < 64u);
+        int stop = 0;  // 0 window exhausted, 1 last sequence, 2 error, 3 slow path at cur, 4 long sequence
+        uint32_t cur;
+        {
+            const uint32_t fl = rdl(flags, lastl);
+            if (fl & (F_LONG | F_MORE | F_ERR)) {
+                members &= ~(1ull << lastl);
+                stop = (fl & (F_LONG | F_MORE)) ? 3 : 2;
+                cur = q + lastl;
+            } else if (fl & F_LAST) {
+                stop = 1;
+                cur = C;
+            } else {
+                cur = rdl(nxt, lastl);
+            }
         }
-        uint32_t cur = q + l;
+        const uint64_t tp1 = PROF_NOW();
+        PROF_ADD(w.pr, 1, tp1 - tp0);
         if (members) {
-            const int rc = dec_window(w, members, S, flags, lit, ll, off, ml, st_lo, bstart, limit, cap, hist);
-            if (rc) return rc;
+            bool isM = (members >> lane) & 1ull;
+            const uint32_t sl = isM ? ll + ((flags & F_LAST) ? 0u : ml) : 0u;
+            const uint32_t orel = wave_excl_scan(sl, lane);
+            uint32_t S = rdl(orel + sl, 63);
+            // output budget: the members that fit in kWin run now, the rest next window
+            const uint64_t cut = __ballot(isM && orel + sl > kWin);
+            if (cut) {
+                const uint32_t c = (uint32_t)__builtin_ctzll(cut);
+                members &= (1ull << c) - 1ull;
+                isM = isM && (uint32_t)lane < c;
+                S = rdl(orel, c);
+                stop = members ? 0 : 4;
+                cur = q + c;
+            }
+            if (members) {
+                // lz4_flex bound checks, lane-parallel; the first failing member decides
+                const uint32_t produced = w.upos - bstart + orel;
+                const bool lastm = (flags & F_LAST) != 0;
+                const uint32_t have = produced + ll;
+                int st = S3HC_OK;
+                st = (!lastm && ml > cap - have) ? S3HC_DST_TOO_SMALL : st;
+                st = (!lastm && ml > limit - have) ? S3HC_CORRUPT : st;
+                st = (!lastm && (off == 0 || off > have + hist)) ? S3HC_CORRUPT : st;
+                st = (ll > cap - produced) ? S3HC_DST_TOO_SMALL : st;
+                st = (ll > limit - produced) ? S3HC_CORRUPT : st;
+                const uint64_t bad = __ballot(isM && st != S3HC_OK);
+                if (bad) return (int)rdl((uint32_t)st, (uint32_t)__builtin_ctzll(bad));
+                dec_window_exec(w, isM, S, orel, sl, lit, ll, off, st_lo);
+                PROF_ADD(w.pr, 2, PROF_NOW() - tp1);
+                PROF_ADD(w.pr, 5, 1);
+                PROF_ADD(w.pr, 6, __builtin_popcountll(members));
+                PROF_ADD(w.pr, 7, (S + 63) / 64);
+                PROF_ADD(w.pr, 11, S);
+            }
         }
+        const uint64_t tp2 = PROF_NOW();
         if (stop == 1) return S3HC_OK;
         if (stop == 2) return S3HC_CORRUPT;
         if (stop == 4) {
-            const uint32_t f = rdl(flags, l);
-            const int rc = dec_seq(w, in, rdl(lit, l), rdl(ll, l), (f & F_LAST) != 0, rdl(off, l), rdl(ml, l),
+            const uint32_t c = cur - q;
+            const uint32_t f = rdl(flags, c);
+            const int rc = dec_seq(w, in, rdl(lit, c), rdl(ll, c), (f & F_LAST) != 0, rdl(off, c), rdl(ml, c),
                                    st_lo, bstart, limit, cap, hist);
             if (rc) return rc;
             if (f & F_LAST) return S3HC_OK;
-            cur = rdl(nxt, l);
+            cur = rdl(nxt, c);
         }
         if (stop == 3) {
             // Slow path: this sequence has long length runs or reaches past the stage.
@@ -565,6 +578,7 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
             if (rc) return rc;
             cur = pos;
         }
+        PROF_ADD(w.pr, 3, PROF_NOW() - tp2);
         q = cur;
     }
 }
@@ -591,6 +605,10 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     w.flushed = 0;
     w.lane = lane;
     int status = S3HC_OK;
+#ifdef S3HC_PROF
+    for (int k = 0; k < 16; ++k) w.pr[k] = 0;
+    const uint64_t tk0 = PROF_NOW();
+#endif
     for (uint32_t b = 0; b < U.n; ++b) {
         const DecBlock B = blk[U.first + b];
         const uint32_t start = w.upos;
@@ -616,6 +634,11 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
         }
     }
     dec_final_flush(w);
+#ifdef S3HC_PROF
+    w.pr[4] = PROF_NOW() - tk0;
+    if (lane == 0)
+        for (int k = 0; k < 16; ++k) atomicAdd(&g_prof[k], (unsigned long long)w.pr[k]);
+#endif
 }
 
 // ================================================================== encode
@@ -732,6 +755,10 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
     const uint32_t b = seg_block[s];
     const EncBlock B = blocks[b];
     if (B.flags & (EB_STORE | EB_EMPTY)) return;
+#ifdef S3HC_PROF
+    uint64_t epr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t tk0 = PROF_NOW();
+#endif
     uint8_t* inb = smem + wv * kWaveLds;
     uint16_t* tbl = (uint16_t*)(inb + kIn);
     uint32_t* info = (uint32_t*)(tbl + kTbl);   // per position: off | lenf-4 << 16 | nb << 24 (0 = none)
@@ -755,6 +782,9 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
     // prewarm the table with the window before the segment
     for (uint32_t x = pw_lo + lane; x + 4 <= seg_lo; x += 64) tbl[hash4(lds32u(inb, x - pw_lo))] = (uint16_t)(x - pw_lo);
     wave_sync();
+#ifdef S3HC_PROF
+    epr[0] = PROF_NOW() - tk0;
+#endif
 
     const uint32_t* dw = (const uint32_t*)inb;
     uint32_t lit_start = seg_lo;   // greedy position: end of the last match
@@ -769,6 +799,8 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
 #endif
     for (uint32_t sb = seg_lo; sb < pend; sb += kSub) {
         const uint32_t sb_end = sb + kSub < pend ? sb + kSub : pend;
+        const uint64_t tc0 = PROF_NOW();
+        PROF_ADD(epr, 6, 1);
         // ---- candidates + match measurements for [sb, sb_end)
         uint64_t mymask = 0;
         for (uint32_t x0 = sb; x0 < sb_end; x0 += 64) {
@@ -825,6 +857,8 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
             if ((uint32_t)lane == ((x0 - sb) >> 6)) mymask = m;
         }
         wave_sync();
+        const uint64_t tc1 = PROF_NOW();
+        PROF_ADD(epr, 1, tc1 - tc0);
 #if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 2  // + candidate pass
         if (mymask == 12345ull) body += 1;
         continue;
@@ -856,6 +890,8 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
             }
         }
         wave_sync();
+        const uint64_t tc2 = PROF_NOW();
+        PROF_ADD(epr, 2, tc2 - tc1);
 #if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 3  // + descriptor pass
         if (nd[lane] == 12345u) body += 1;
         continue;
@@ -899,12 +935,21 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
             nseq++;
             lit_start = P + lenf;
             if (j == 63) {
+                const uint64_t tf0 = PROF_NOW();
                 enc_flush_group(lane, 64, nseq - 64, gls, hP, hW, hL, myrec, body, ll0);
                 gls = lit_start;
+                PROF_ADD(epr, 4, PROF_NOW() - tf0);
             }
         }
+        PROF_ADD(epr, 3, PROF_NOW() - tc2);
     }
     if (nseq & 63) enc_flush_group(lane, nseq & 63, nseq & ~63u, gls, hP, hW, hL, myrec, body, ll0);
+#ifdef S3HC_PROF
+    epr[5] = PROF_NOW() - tk0;
+    epr[7] = nseq;
+    if (lane == 0)
+        for (int q = 0; q < 8; ++q) atomicAdd(&g_prof[16 + q], (unsigned long long)epr[q]);
+#endif
     if (lane == 0) {
         SegSummary S;
         S.nseq = nseq;
@@ -1394,3 +1439,16 @@ hipError_t launch_dframe_verify(const uint8_t* src, const uint64_t* frame_off, u
     return hipGetLastError();
 }
 }  // namespace s3hc
+
+#ifdef S3HC_PROF
+extern "C" int s3hc_diag_prof(unsigned long long* out, int n, int reset) {
+    if (n > 32) n = 32;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(s3hc::g_prof), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(s3hc::g_prof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
