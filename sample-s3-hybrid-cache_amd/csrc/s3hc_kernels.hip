@@ -374,55 +374,114 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, bool isM, uint32_t S
     const uint32_t pkA = orel | (ll << 16);
     const uint32_t pkB = off | ((lit - st_lo) << 16);
     const uint32_t upos = w.upos;
-    uint32_t carry = 0, pendv = 0;
-    for (uint32_t b = 0; b < S; b += 64) {
-        // lanes t >= S only compute (their reads stay inside this wave's LDS) and never write;
-        // they sit above every valid lane, so they do not disturb the scan
-        const uint32_t t = b + lane;
-        uint32_t mk = wave_incl_max((uint32_t)marks[t]);
-        mk = mk > carry ? mk : carry;
-        carry = rdl(mk, 63);
-        const int m = (int)mk - 1;
-        const uint32_t A = __shfl(pkA, m), B = __shfl(pkB, m);
-        const uint32_t mo = A & 0xFFFFu, mll = A >> 16, moff = B & 0xFFFFu, mlit = B >> 16;
-        const uint32_t x = upos + t;
-        const uint32_t dd = t - mo;
-        const bool isLit = dd < mll;
-        uint32_t e = dd - mll;          // position inside the match
-        const uint32_t ms = x - e;      // match start
-        const bool wrap = !isLit && e >= moff && t < S;
-        if (__ballot(wrap)) e = wrap ? e % moff : e;  // overlapping match: period moff
-        const uint32_t y = ms - moff + e;
-        const uint8_t lv = w.stage[(mlit + dd) & (kStage - 1)];
-        const uint8_t rv = w.ring[y & kMask];
-        uint32_t val = isLit ? lv : rv;
-        const uint32_t ry = y - upos;  // < S when the source is inside the window
-        const bool pnd = !isLit && ry < S;
-        const bool old = !isLit && !pnd && y + (kRing - S) < upos && t < S;
-        if (__ballot(old)) val = old ? (uint32_t)w.out[y] : val;  // older than the ring: in HBM
-        if (t < S) {
-            w.ring[x & kMask] = (uint8_t)val;
-            refs[t] = (uint16_t)(pnd ? ry : 0xFFFFu);
+    // Passes of 256 bytes: byte t = b + 64k + lane, k = 0..3, with every LDS read of the pass
+    // issued before its writes (four independent chunks per round trip).
+    uint32_t carry = 0;
+    for (uint32_t b = 0; b < S; b += 256) {
+        uint32_t mk[4], t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            t[k] = b + 64u * k + lane;
+            mk[k] = (uint32_t)marks[t[k]];
         }
-        pendv |= (pnd && t < S) ? 1u : 0u;
-    }
-    if (__ballot(pendv)) {
-        wave_sync();
-        for (uint32_t b = 0; b < S; b += 64) {
-            const uint32_t t = b + lane;
-            const uint32_t z0 = t < S ? (uint32_t)refs[t] : 0xFFFFu;
-            const bool pl = z0 != 0xFFFFu;
-            if (!__ballot(pl)) continue;
-            uint32_t z = pl ? z0 : 0u;
-            for (;;) {
-                const uint32_t r = refs[z];
-                const bool more = pl && r != 0xFFFFu;
-                if (!__ballot(more)) break;
-                z = more ? r : z;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mk[k] = wave_incl_max(mk[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // lanes t >= S only compute (their reads stay inside this wave's LDS) and never
+            // write; they sit above every valid byte, so they do not disturb the scan
+            const uint32_t top = rdl(mk[k], 63);
+            mk[k] = mk[k] > carry ? mk[k] : carry;
+            carry = top > carry ? top : carry;
+        }
+        uint32_t A[4], B[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            A[k] = __shfl(pkA, (int)mk[k] - 1);
+            B[k] = __shfl(pkB, (int)mk[k] - 1);
+        }
+        uint32_t y[4], val[4];
+        bool lit_[4], pnd[4], wrap[4];
+        bool anywrap = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t mo = A[k] & 0xFFFFu, mll = A[k] >> 16, moff = B[k] & 0xFFFFu;
+            const uint32_t dd = t[k] - mo;
+            lit_[k] = dd < mll;
+            const uint32_t e = dd - mll;  // position inside the match
+            wrap[k] = !lit_[k] && e >= moff && t[k] < S;
+            anywrap |= wrap[k];
+            y[k] = upos + t[k] - moff;    // non-overlapping source
+        }
+        if (__ballot(anywrap)) {          // overlapping matches: period moff
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (wrap[k]) {
+                    const uint32_t mo = A[k] & 0xFFFFu, mll = A[k] >> 16, moff = B[k] & 0xFFFFu;
+                    const uint32_t e = t[k] - mo - mll;
+                    y[k] = upos + mo + mll - moff + e % moff;
+                }
             }
-            const uint8_t v = w.ring[(upos + z) & kMask];
-            if (pl) w.ring[(upos + t) & kMask] = v;
         }
+        uint8_t lv[4], rv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t mo = A[k] & 0xFFFFu, mlit = B[k] >> 16;
+            lv[k] = w.stage[(mlit + t[k] - mo) & (kStage - 1)];
+            rv[k] = w.ring[y[k] & kMask];
+        }
+        bool anyold = false, anypnd = false;
+        bool old[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            val[k] = lit_[k] ? lv[k] : rv[k];
+            const bool ok = t[k] < S;
+            const uint32_t ry = y[k] - upos;  // < S: source inside the window
+            pnd[k] = ok && !lit_[k] && ry < S && ry >= b;  // earlier passes are final in the ring
+            old[k] = ok && !lit_[k] && ry >= S && y[k] + (kRing - S) < upos;
+            anyold |= old[k];
+            anypnd |= pnd[k];
+        }
+        if (__ballot(anyold)) {           // older than the ring: already in HBM
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (old[k]) val[k] = w.out[y[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (t[k] < S) {
+                w.ring[(upos + t[k]) & kMask] = (uint8_t)val[k];
+                refs[t[k]] = (uint16_t)(pnd[k] ? y[k] - upos : 0xFFFFu);
+            }
+        }
+        if (__ballot(anypnd)) {
+            // sources inside the window: follow refs through this pass's pending bytes (bytes
+            // of earlier passes and bytes with refs == 0xFFFF are final in the ring)
+            wave_sync();
+            uint32_t z[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z[k] = pnd[k] ? y[k] - upos : 0u;
+            for (;;) {
+                bool more = false;
+                uint32_t r[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) r[k] = refs[z[k]];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const bool mo = pnd[k] && z[k] >= b && r[k] != 0xFFFFu;
+                    z[k] = mo ? r[k] : z[k];
+                    more |= mo;
+                }
+                if (!__ballot(more)) break;
+            }
+            uint8_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = w.ring[(upos + z[k]) & kMask];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (pnd[k]) w.ring[(upos + t[k]) & kMask] = v[k];
+        }
+        wave_sync();
     }
     wave_sync();
     w.upos = upos + S;
