@@ -702,11 +702,11 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
 
 // ================================================================== encode
 namespace enc {
-constexpr uint32_t kIn = kPrewarm + kSeg + 128;         // staged input bytes (+ read-ahead pad)
+constexpr uint32_t kPad = 16;                               // front pad: reads at i-8 stay in bounds
+constexpr uint32_t kIn = kPad + kPrewarm + kSeg + 128;      // staged input bytes (+ read-ahead pad)
 constexpr uint32_t kTbl = 1u << kHashLog;
-constexpr uint32_t kSub = 512;                          // positions per candidate sub-block
-constexpr uint32_t kWaveLds = kIn + kTbl * 2 + kSub * 4;
-constexpr int kWaves = 1;
+constexpr uint32_t kSteps = 8;                              // 64-position steps per sub-block
+constexpr uint32_t kFwd = 19;                               // forward bytes measured per probe (4 + 15)
 constexpr uint32_t kEmpty = 0xFFFFu;
 }  // namespace enc
 
@@ -760,56 +760,58 @@ __device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* 
     wave_sync();
 }
 
-// Lane-parallel post-processing of up to 64 walk hops held one per lane (hop j in lane j):
-// clip each backward extension at the previous match end, form the LZ4 sequence record
-// (literal length, match length, offset), add up encoded sizes, store the records.
-__device__ __forceinline__ void enc_flush_group(int lane, uint32_t cnt, uint32_t g0, uint32_t gls, uint32_t hP,
-                                                uint32_t hW, uint32_t hL, uint2* myrec, uint32_t& body,
-                                                uint32_t& ll0) {
-    const bool act = (uint32_t)lane < cnt;
-    const uint32_t endj = hP + hL;                        // this hop's match end
-    uint32_t prev = __shfl_up(endj, 1);
-    if (lane == 0) prev = gls;
-    uint32_t nb = (hW >> 29) & 7u;
-    if (nb > hP - prev) nb = hP - prev;
-    const uint32_t p = hP - nb;
-    const uint32_t ll = p - prev;
-    const uint32_t len = nb + hL;
-    const uint32_t off = (hW >> 9) & 0xFFFFu;
-    const uint32_t gj = g0 + lane;
-    uint32_t sz = act ? (gj == 0 ? 0u : 1 + ext_bytes(ll)) + ll + 2 + ext_bytes(len - 4) : 0u;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) sz += __shfl_xor(sz, d);
-    body += sz;
-    if (g0 == 0) ll0 = rdl(ll, 0);
-    if (act) myrec[gj] = make_uint2(ll | (len << 16), off);
+// Lane-parallel LZ4 sequence records for the greedy hops of one 64-position chunk (bit j of
+// hm = a match taken at base + j; lane j holds that position's probe word and forward length):
+// clip each backward extension at the previous match end, form (literal length, match length,
+// offset), add up the encoded sizes, store the records.
+__device__ __forceinline__ void enc_chunk_records(int lane, uint64_t hm, uint32_t base, uint32_t word, uint32_t lenf,
+                                                  uint32_t& last_end, uint32_t& nseq, uint32_t& body,
+                                                  uint32_t& ll0, uint2* myrec) {
+    const bool hop = (hm >> lane) & 1ull;
+    const uint64_t below = hm & ((1ull << lane) - 1ull);
+    const uint32_t P = base + lane;
+    const uint32_t endj = P + lenf;
+    const uint32_t bh = (uint32_t)(below >> 32), bl = (uint32_t)below;
+    const int pl = bh ? 63 - __builtin_clz(bh) : (bl ? 31 - __builtin_clz(bl) : 0);
+    const uint32_t pe = __shfl(endj, pl);
+    const uint32_t prev = below ? pe : last_end;
+    uint32_t nb = (word >> 24) & 7u;
+    if (nb > P - prev) nb = P - prev;
+    const uint32_t ll = P - nb - prev;
+    const uint32_t len = nb + lenf;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0));
+    const uint32_t gj = nseq + rank;
+    const uint32_t sz = hop ? (gj == 0 ? 0u : 1u + ext_bytes(ll)) + ll + 2u + ext_bytes(len - 4) : 0u;
+    body += rdl(wave_incl_sum(sz), 63);
+    const uint32_t first = (uint32_t)__builtin_ctzll(hm);
+    if (nseq == 0) ll0 = rdl(ll, first);
+    if (hop) myrec[gj] = make_uint2(ll | (len << 16), word & 0xFFFFu);
+    last_end = rdl(endj, 63u - (uint32_t)__builtin_clzll(hm));
+    nseq += (uint32_t)__builtin_popcountll(hm);
 }
 
-// Match finding for one 4 KiB segment per wave, in alternating phases per kSub-position
-// sub-block:
-//   candidates (parallel, 64 positions per step): every position P is probed exactly once —
-//     4-byte hash into the wave's LDS table (most recent earlier position with that hash),
-//     verified against the input, with a fallback to distances 1..4 (runs and short periods
-//     inside a probe step); then every position of the step enters the table. For verified
-//     positions the same step measures the match: forward up to kFwd bytes, backward up to
-//     4 bytes. A second pass writes for EVERY position x a descriptor of the first match at or
-//     after x: distance to it, its offset, forward length and backward length (one u32).
-//   greedy walk (scalar, one LDS read per hop): read the descriptor at the current position,
-//     jump to the match, extend it wave-wide only if it reached kFwd bytes, continue from its
-//     end. Hops are parked one per lane; every 64 hops a lane-parallel pass turns them into
-//     LZ4 sequence records (enc_flush_group).
+// Match finding for one 4 KiB segment per wave (the segment's 4 KiB prefix window is staged
+// too and pre-inserted into the hash table). Per 512-position sub-block:
+//   A  table pass: every position hashes its 4 bytes, reads the per-wave LDS table (u16
+//      window positions; the most recent earlier position with that hash) and inserts
+//      itself; the eight 64-position steps go back to back (reads only wait at use).
+//      Distance 1..4 repeats are detected from the position's own bytes.
+//   B  measure pass: both candidates (table, short distance) are verified and measured in
+//      one LDS round trip per step — forward up to kFwd bytes, backward up to 4 — and the
+//      longer kept; a ballot gives the step's match mask, the probe word stays in a VGPR.
+//   C  greedy walk, per 64-position chunk, from registers: next match = lowest mask bit at
+//      or after the greedy position (s_ff1), its word by v_readlane, long matches extended
+//      wave-wide; the chunk's hops then become sequence records lane-parallel.
 // Matches end inside the segment, so segments are independent; k_enc_sizes stitches them.
 __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ src,
                                                    const EncBlock* __restrict__ blocks,
                                                    const uint32_t* __restrict__ seg_block, uint32_t nseg,
                                                    uint2* __restrict__ recs, SegSummary* __restrict__ summ) {
     using namespace enc;
-    constexpr uint32_t kFwd = 19;  // forward bytes measured in the parallel phase (4 verified + 15)
-    static_assert(kSub <= 512, "descriptor keeps the hop distance in 9 bits");
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kWaves * kWaveLds];
+    __shared__ __attribute__((aligned(16))) uint8_t inb_raw[kIn];
+    __shared__ __attribute__((aligned(16))) uint16_t tbl[kTbl + 8];  // slot kTbl: sink for idle lanes
     const int lane = lane_id();
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t s = blockIdx.x * kWaves + wv;
+    const uint32_t s = blockIdx.x;
     if (s >= nseg) return;
     const uint32_t b = seg_block[s];
     const EncBlock B = blocks[b];
@@ -818,10 +820,8 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
     uint64_t epr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t tk0 = PROF_NOW();
 #endif
-    uint8_t* inb = smem + wv * kWaveLds;
-    uint16_t* tbl = (uint16_t*)(inb + kIn);
-    uint32_t* info = (uint32_t*)(tbl + kTbl);   // per position: off | lenf-4 << 16 | nb << 24 (0 = none)
-    uint32_t* nd = info;  // descriptors overwrite info in place: chunk c reads info only at >= c
+    uint8_t* inb = inb_raw + kPad;               // inb[x - pw_lo] = block byte x
+    const uint32_t* dw = (const uint32_t*)inb;   // dw[-4 .. -1] is the pad
     const uint32_t U = B.len;
     const uint32_t k = s - B.seg0;
     const uint32_t seg_lo = k * kSeg;
@@ -829,9 +829,8 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
     const uint32_t pw_lo = seg_lo > kPrewarm ? seg_lo - kPrewarm : 0;
     const uint32_t st_hi = seg_hi + 64 < U ? seg_hi + 64 : U;
     const uint8_t* bin = src + B.src_off;
+    for (uint32_t t = lane; t < (kTbl + 8) / 8; t += 64) ((uint4*)tbl)[t] = make_uint4(~0u, ~0u, ~0u, ~0u);
     stage_in(bin, pw_lo, st_hi, inb, lane);
-    for (uint32_t t = lane; t < kTbl / 2; t += 64) ((uint32_t*)tbl)[t] = 0xFFFFFFFFu;
-    wave_sync();
     // Largest match end / start (LZ4: the last 5 bytes are literals and the last match starts
     // at least 12 bytes before the block end; segment matches end inside the segment).
     const uint32_t blk_end_lim = U >= 5 ? U - 5 : 0;
@@ -844,165 +843,137 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
 #ifdef S3HC_PROF
     epr[0] = PROF_NOW() - tk0;
 #endif
-
-    const uint32_t* dw = (const uint32_t*)inb;
-    uint32_t lit_start = seg_lo;   // greedy position: end of the last match
-    uint32_t gls = seg_lo;         // lit_start before the first hop of the current group
+    uint32_t x = seg_lo;         // greedy position: end of the last match
+    uint32_t last_end = seg_lo;  // end of the last recorded match (literal start)
     uint32_t nseq = 0, body = 0, ll0 = 0;
-    uint32_t hP = 0, hW = 0, hL = 0;  // parked hops (lane j = hop j of the group)
     uint2* myrec = recs + (size_t)s * kMaxSeqPerSeg;
-    uint32_t pend = smax < (int64_t)seg_lo ? seg_lo : (uint32_t)(smax + 1);  // probe [seg_lo, pend)
-#if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 1  // diagnostic builds only: staging + prewarm
-    if (dw[lane] == 0x12345678u) pend = 0;
-    pend = seg_lo;
-#endif
-    for (uint32_t sb = seg_lo; sb < pend; sb += kSub) {
-        const uint32_t sb_end = sb + kSub < pend ? sb + kSub : pend;
+    const uint32_t pend = smax < (int64_t)seg_lo ? seg_lo : (uint32_t)(smax + 1);  // probe [seg_lo, pend)
+    for (uint32_t sb = seg_lo; sb < pend; sb += 64 * kSteps) {
+        const uint32_t sb_end = sb + 64 * kSteps < pend ? sb + 64 * kSteps : pend;
         const uint64_t tc0 = PROF_NOW();
         PROF_ADD(epr, 6, 1);
-        // ---- candidates + match measurements for [sb, sb_end)
-        uint64_t mymask = 0;
-        for (uint32_t x0 = sb; x0 < sb_end; x0 += 64) {
-            const uint32_t P = x0 + lane;
-            const bool valid = P < sb_end;
+        // ---- A: table pass
+        uint32_t vv[kSteps], vm[kSteps], cc[kSteps];
+#pragma unroll
+        for (uint32_t q = 0; q < kSteps; ++q) {
+            const uint32_t P = sb + 64 * q + lane;
             const uint32_t i = P - pw_lo;
             const uint32_t a = i >> 2, sh = i & 3;
-            const uint32_t w0 = dw[a], w1 = dw[a + 1], wp = a ? dw[a - 1] : 0u;
-            const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            const uint32_t vm4 = __builtin_amdgcn_alignbyte(w0, wp, sh);  // bytes [P-4, P)
-            const uint32_t h = hash4(v);
-            const uint32_t c16 = tbl[h];
-            uint32_t c = pw_lo + c16;
-            bool good = valid && c16 != kEmpty && c < P && lds32u(inb, c16) == v;
-            if (!good && valid) {
-                if (i >= 1 && __builtin_amdgcn_alignbyte(v, vm4, 3) == v) { good = true; c = P - 1; }
-                else if (i >= 2 && __builtin_amdgcn_alignbyte(v, vm4, 2) == v) { good = true; c = P - 2; }
-                else if (i >= 3 && __builtin_amdgcn_alignbyte(v, vm4, 1) == v) { good = true; c = P - 3; }
-                else if (i >= 4 && vm4 == v) { good = true; c = P - 4; }
-            }
-            if (valid) tbl[h] = (uint16_t)i;
-            uint32_t word = 0;
-            if (good) {
-                const uint32_t ci = c - pw_lo;
-                // forward: bytes [P+4, P+20) against [c+4, c+20)
-                const uint32_t pa = (i + 4) >> 2, ps = (i + 4) & 3;
-                const uint32_t ca = (ci + 4) >> 2, cs = (ci + 4) & 3;
-                const uint32_t x0w = dw[pa], x1w = dw[pa + 1], x2w = dw[pa + 2], x3w = dw[pa + 3], x4w = dw[pa + 4];
-                const uint32_t y0w = dw[ca], y1w = dw[ca + 1], y2w = dw[ca + 2], y3w = dw[ca + 3], y4w = dw[ca + 4];
-                const uint32_t d0 = __builtin_amdgcn_alignbyte(x1w, x0w, ps) ^ __builtin_amdgcn_alignbyte(y1w, y0w, cs);
-                const uint32_t d1 = __builtin_amdgcn_alignbyte(x2w, x1w, ps) ^ __builtin_amdgcn_alignbyte(y2w, y1w, cs);
-                const uint32_t d2 = __builtin_amdgcn_alignbyte(x3w, x2w, ps) ^ __builtin_amdgcn_alignbyte(y3w, y2w, cs);
-                const uint32_t d3 = __builtin_amdgcn_alignbyte(x4w, x3w, ps) ^ __builtin_amdgcn_alignbyte(y4w, y3w, cs);
-                uint32_t len = d0 ? 4 + (__builtin_ctz(d0) >> 3)
-                             : d1 ? 8 + (__builtin_ctz(d1) >> 3)
-                             : d2 ? 12 + (__builtin_ctz(d2) >> 3)
-                             : d3 ? 16 + (__builtin_ctz(d3) >> 3) : 20u;
-                if (len > kFwd) len = kFwd;
-                const uint32_t maxf = end_lim - P;  // >= 4 for P <= smax
-                if (len > maxf) len = maxf;
-                // backward: up to 4 bytes before P and c (c-4 .. c-1 must be staged)
-                uint32_t nb = 0;
-                if (ci >= 1) {
-                    const uint32_t cm4 = ci >= 4 ? lds32u(inb, ci - 4) : (lds32u(inb, 0) << (8 * (4 - ci)));
-                    const uint32_t dx = vm4 ^ cm4;
-                    nb = dx ? (uint32_t)__builtin_clz(dx) >> 3 : 4u;
-                    const uint32_t lim = ci < i ? ci : i;
-                    if (nb > lim) nb = lim;
-                }
-                word = (P - c) | ((len - 4) << 16) | (nb << 24);
-            }
-            if (valid) info[P - sb] = word;
-            const uint64_t m = __ballot(good);
-            if ((uint32_t)lane == ((x0 - sb) >> 6)) mymask = m;
+            const uint32_t w0 = dw[a], w1 = dw[a + 1], wp = dw[(int)a - 1];
+            vv[q] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            vm[q] = __builtin_amdgcn_alignbyte(w0, wp, sh);  // bytes [P-4, P)
+            const uint32_t h = hash4(vv[q]);
+            cc[q] = tbl[h];
+            tbl[P < sb_end ? h : kTbl] = (uint16_t)i;
         }
-        wave_sync();
+        // ---- B: verify + measure both candidates
+        uint32_t word[kSteps], flen[kSteps];
+        uint64_t mm[kSteps];
+#pragma unroll
+        for (uint32_t q = 0; q < kSteps; ++q) {
+            const uint32_t P = sb + 64 * q + lane;
+            const bool valid = P < sb_end;
+            const uint32_t i = P - pw_lo;
+            const uint32_t v = vv[q], vm4 = vm[q];
+            const uint32_t df = (i >= 1 && __builtin_amdgcn_alignbyte(v, vm4, 3) == v) ? 1u
+                              : (i >= 2 && __builtin_amdgcn_alignbyte(v, vm4, 2) == v) ? 2u
+                              : (i >= 3 && __builtin_amdgcn_alignbyte(v, vm4, 1) == v) ? 3u
+                              : (i >= 4 && vm4 == v) ? 4u : 0u;
+            const uint32_t c16 = cc[q];
+            const bool tin = c16 != kEmpty && c16 < i;
+            const uint32_t ct = tin ? c16 : i, cf = i - df;
+            const uint32_t a = i >> 2, sh = i & 3;
+            const uint32_t ta = ct >> 2, ts = ct & 3, fa = cf >> 2, fs = cf & 3;
+            uint32_t O[5], T[7], F[7];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) O[j] = dw[a + 1 + j];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) T[j] = dw[(int)ta - 1 + j];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) F[j] = dw[(int)fa - 1 + j];
+            const uint32_t maxf = end_lim - P;  // >= 4 for P <= smax
+            // forward length against candidate dwords C (C[j] holds bytes c-4+4j .. c+4j)
+            auto fwd = [&](const uint32_t* C, uint32_t cs) -> uint32_t {
+                uint32_t len = 20u;
+#pragma unroll
+                for (int j = 3; j >= 0; --j) {
+                    const uint32_t dx = __builtin_amdgcn_alignbyte(O[j + 1], O[j], sh) ^
+                                        __builtin_amdgcn_alignbyte(C[j + 3], C[j + 2], cs);
+                    len = dx ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dx) >> 3) : len;
+                }
+                len = len > kFwd ? kFwd : len;
+                return len > maxf ? maxf : len;
+            };
+            auto bwd = [&](const uint32_t* C, uint32_t cs, uint32_t ci) -> uint32_t {
+                const uint32_t dx = vm4 ^ __builtin_amdgcn_alignbyte(C[1], C[0], cs);
+                uint32_t nb = dx ? (uint32_t)__builtin_clz(dx) >> 3 : 4u;
+                const uint32_t lim = ci < i ? ci : i;
+                return nb > lim ? lim : nb;
+            };
+            const bool gt = valid && tin && __builtin_amdgcn_alignbyte(T[2], T[1], ts) == v;
+            const bool gf = valid && df != 0;
+            const uint32_t lt = fwd(T, ts), lf = fwd(F, fs);
+            const bool ut = gt && (!gf || lt >= lf);
+            const uint32_t len = ut ? lt : lf;
+            const uint32_t nb = ut ? bwd(T, ts, ct) : bwd(F, fs, cf);
+            const uint32_t dist = i - (ut ? ct : cf);
+            const bool good = gt || gf;
+            word[q] = dist | ((len - 4) << 16) | (nb << 24);
+            flen[q] = len;
+            mm[q] = __ballot(good);
+        }
         const uint64_t tc1 = PROF_NOW();
         PROF_ADD(epr, 1, tc1 - tc0);
-#if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 2  // + candidate pass
-        if (mymask == 12345ull) body += 1;
-        continue;
-#endif
-        // ---- next-match descriptors: nd[x] = dist(x -> next match P) | off << 9 | (lenf-4) << 25 | nb << 29
-        {
-            const uint32_t nch = (sb_end - sb + 63) >> 6;
-            // first match position of chunk c or any later chunk (relative to sb), lane c
-            const uint32_t firstc = mymask ? (uint32_t)(lane * 64) + (uint32_t)__builtin_ctzll(mymask) : 0xFFFFu;
-            uint32_t later = 0xFFFFu;  // first match in the chunks after this lane's chunk
-            uint32_t run = 0xFFFFu;
-            for (int c2 = (int)nch - 1; c2 >= 0; --c2) {
-                if (lane == c2) later = run;
-                const uint32_t f2 = rdl(firstc, (uint32_t)c2);
-                if (f2 != 0xFFFFu) run = f2;
-            }
-            for (uint32_t ck = 0; ck < nch; ++ck) {
-                const uint32_t xr = ck * 64 + lane;  // x - sb
-                if (sb + xr >= sb_end) break;
-                const uint64_t mk = rdl64(mymask, ck) & (~0ull << lane);
-                const uint32_t lat = rdl(later, ck);
-                const uint32_t pr = mk ? ck * 64 + (uint32_t)__builtin_ctzll(mk) : lat;
-                uint32_t d = 0;
-                if (pr != 0xFFFFu) {
-                    const uint32_t w = info[pr];
-                    d = (pr - xr) | ((w & 0xFFFFu) << 9) | (((w >> 16) & 15u) << 25) | ((w >> 24) << 29);
-                }
-                nd[xr] = d;
-            }
-        }
-        wave_sync();
-        const uint64_t tc2 = PROF_NOW();
-        PROF_ADD(epr, 2, tc2 - tc1);
-#if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 3  // + descriptor pass
-        if (nd[lane] == 12345u) body += 1;
-        continue;
-#endif
-        // ---- greedy walk through [sb, sb_end)
-        for (;;) {
-            const uint32_t x = lit_start > sb ? lit_start : sb;
-            if (x >= sb_end) break;
-            const uint32_t d = nd[x - sb];
-            if (((d >> 9) & 0xFFFFu) == 0) break;  // no match left in this sub-block
-            const uint32_t P = x + (d & 511u);
-            uint32_t lenf = 4 + ((d >> 25) & 15u);
-            if (lenf == kFwd) {  // long match: wave-wide forward extension
-                const uint32_t maxf = end_lim - P;
-                const uint32_t c = P - ((d >> 9) & 0xFFFFu);
-                while (lenf < maxf) {
-                    const uint32_t rel = lenf + 4u * lane;
-                    uint32_t e2;
-                    if (rel >= maxf) {
-                        e2 = 0;
-                    } else {
-                        uint32_t ia = P + rel - pw_lo;
-                        if (ia > kIn - 8) ia = kIn - 8;
-                        const uint32_t xa = lds32u(inb, ia), ya = lds32u(inb, c + rel - pw_lo);
-                        e2 = xa == ya ? 4u : (uint32_t)__builtin_ctz(xa ^ ya) >> 3;
-                        if (e2 > maxf - rel) e2 = maxf - rel;
+        // ---- C: greedy walk per chunk, records per chunk
+#pragma unroll
+        for (uint32_t q = 0; q < kSteps; ++q) {
+            const uint32_t base = sb + 64 * q;
+            if (x >= base + 64 || !mm[q]) continue;
+            uint64_t hm = 0;
+            uint32_t lenv = flen[q];
+            for (;;) {
+                const uint32_t r = x > base ? x - base : 0u;
+                if (r >= 64) break;
+                const uint64_t av = mm[q] & (~0ull << r);
+                if (!av) break;
+                const uint32_t j = (uint32_t)__builtin_ctzll(av);
+                const uint32_t wj = rdl(word[q], j);
+                const uint32_t P = base + j;
+                uint32_t lenf = 4u + ((wj >> 16) & 15u);
+                if (lenf == kFwd) {  // long match: wave-wide forward extension
+                    const uint32_t maxf = end_lim - P;
+                    const uint32_t c = P - (wj & 0xFFFFu);
+                    while (lenf < maxf) {
+                        const uint32_t rel = lenf + 4u * lane;
+                        uint32_t e2;
+                        if (rel >= maxf) {
+                            e2 = 0;
+                        } else {
+                            uint32_t ia = P + rel - pw_lo;
+                            if (ia > kIn - kPad - 8) ia = kIn - kPad - 8;
+                            const uint32_t xa = lds32u(inb, ia), ya = lds32u(inb, c + rel - pw_lo);
+                            e2 = xa == ya ? 4u : (uint32_t)__builtin_ctz(xa ^ ya) >> 3;
+                            if (e2 > maxf - rel) e2 = maxf - rel;
+                        }
+                        const uint64_t m2 = __ballot(e2 != 4u);
+                        if (m2 == 0) { lenf += 256; continue; }
+                        const uint32_t g = (uint32_t)__builtin_ctzll(m2);
+                        lenf += 4u * g + rdl(e2, g);
+                        break;
                     }
-                    const uint64_t m2 = __ballot(e2 != 4u);
-                    if (m2 == 0) { lenf += 256; continue; }
-                    const uint32_t g = (uint32_t)__builtin_ctzll(m2);
-                    lenf += 4u * g + rdl(e2, g);
-                    break;
+                    lenv = (uint32_t)lane == j ? lenf : lenv;
                 }
+                hm |= 1ull << j;
+                x = P + lenf;
             }
-            const uint32_t j = nseq & 63;
-            if ((uint32_t)lane == j) {
-                hP = P;
-                hW = d;
-                hL = lenf;
-            }
-            nseq++;
-            lit_start = P + lenf;
-            if (j == 63) {
+            if (hm) {
                 const uint64_t tf0 = PROF_NOW();
-                enc_flush_group(lane, 64, nseq - 64, gls, hP, hW, hL, myrec, body, ll0);
-                gls = lit_start;
+                enc_chunk_records(lane, hm, base, word[q], lenv, last_end, nseq, body, ll0, myrec);
                 PROF_ADD(epr, 4, PROF_NOW() - tf0);
             }
         }
-        PROF_ADD(epr, 3, PROF_NOW() - tc2);
+        PROF_ADD(epr, 3, PROF_NOW() - tc1);
     }
-    if (nseq & 63) enc_flush_group(lane, nseq & 63, nseq & ~63u, gls, hP, hW, hL, myrec, body, ll0);
 #ifdef S3HC_PROF
     epr[5] = PROF_NOW() - tk0;
     epr[7] = nseq;
@@ -1014,7 +985,7 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
         S.nseq = nseq;
         S.ll0 = ll0;
         S.body = body;
-        S.trail = seg_hi - lit_start;
+        S.trail = seg_hi - x;
         summ[s] = S;
     }
 }
@@ -1434,7 +1405,7 @@ hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock*
 hipError_t launch_enc_parse(const uint8_t* src, const EncBlock* blocks, const uint32_t* seg_block, uint32_t nseg,
                             uint2* recs, SegSummary* summ, hipStream_t st) {
     if (!nseg) return hipSuccess;
-    hipLaunchKernelGGL(k_enc_parse, dim3(cdiv(nseg, enc::kWaves)), dim3(64 * enc::kWaves), 0, st, src, blocks,
+    hipLaunchKernelGGL(k_enc_parse, dim3(nseg), dim3(64), 0, st, src, blocks,
                        seg_block, nseg, recs, summ);
     return hipGetLastError();
 }
