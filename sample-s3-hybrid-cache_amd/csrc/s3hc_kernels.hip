@@ -214,19 +214,22 @@ __global__ __launch_bounds__(256) void k_xxh32_ranges(const uint8_t* __restrict_
 
 // ================================================================== decode
 namespace dec {
-constexpr uint32_t kStage = 512;   // compressed bytes staged per wave
+constexpr uint32_t kCring = 1024;  // compressed input ring per wave (aligned-address space)
+constexpr uint32_t kCmask = kCring - 1;
+constexpr uint32_t kChunk = 256;   // ring refill granule: one dword per lane
+constexpr uint32_t kAhead = 512;   // input kept staged ahead of the parse position
 constexpr uint32_t kRing = 4096;   // recent output kept in LDS per wave (match sources)
 constexpr uint32_t kMask = kRing - 1;
 constexpr uint32_t kFlush = 1024;  // ring -> HBM flush granule
 constexpr uint32_t kWin = 1024;    // output bytes executed per window (byte-parallel)
-constexpr uint32_t kWaveLds = kRing + kStage + (kWin + 64) + 2 * kWin;
+constexpr uint32_t kWaveLds = kRing + kCring + (kWin + 64) + 2 * kWin;
 constexpr int kWaves = 4;
 enum : uint32_t { F_ERR = 1, F_LAST = 2, F_LONG = 4, F_MORE = 8 };
 }  // namespace dec
 
 struct DecWave {
     uint8_t* ring;
-    uint8_t* stage;
+    uint8_t* cin;        // kCring bytes: compressed input, byte p of the block at (p + mis) & kCmask
     uint8_t* marks;      // kWin + 64 bytes: sequence start marks of the current window
     uint16_t* refs;      // kWin entries: in-window match source of each output byte
     uint8_t* out;        // unit output base in HBM
@@ -271,15 +274,15 @@ __device__ __forceinline__ void dec_final_flush(DecWave& w) {
     }
 }
 
-// Literal run [lit, lit+ll) of the block input -> output.
+// Literal run [lit, lit+ll) of the block input -> output (from the input ring when staged).
 __device__ __forceinline__ void dec_literals(DecWave& w, const uint8_t* in, uint32_t lit, uint32_t ll,
-                                             uint32_t st_lo, bool staged) {
+                                             uint32_t mis, bool staged) {
     for (uint32_t k0 = 0; k0 < ll; k0 += 64) {
         uint32_t piece = ll - k0 < 64 ? ll - k0 : 64;
         uint32_t base = w.upos;
         if ((uint32_t)w.lane < piece) {
             uint32_t k = k0 + w.lane;
-            uint8_t b = staged ? w.stage[lit + k - st_lo] : in[lit + k];
+            uint8_t b = staged ? w.cin[(lit + k + mis) & dec::kCmask] : in[lit + k];
             w.ring[(base + w.lane) & dec::kMask] = b;
         }
         w.upos = base + piece;
@@ -306,14 +309,11 @@ __device__ __forceinline__ void dec_match(DecWave& w, uint32_t off, uint32_t ml)
     }
 }
 
-// Stage [lo, lo+kStage) of the block input (bytes >= C left undefined).
-__device__ __forceinline__ void dec_stage(const uint8_t* in, uint32_t C, uint32_t lo, uint8_t* stage, int lane) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        uint32_t i = 8u * lane + 4u * k;
-        if (lo + i < C) *(uint32_t*)(stage + i) = gld32u(in + lo + i, C - lo - i);
-    }
-    wave_sync();
+// 4 bytes at aligned-space index i of the input ring (wraps).
+__device__ __forceinline__ uint32_t cin32(const uint8_t* cin, uint32_t i) {
+    const uint32_t* r = (const uint32_t*)cin;
+    const uint32_t a = i >> 2;
+    return __builtin_amdgcn_alignbyte(r[(a + 1) & (dec::kCring / 4 - 1)], r[a & (dec::kCring / 4 - 1)], i & 3u);
 }
 
 // Wave-cooperative LZ4 length-extension scan at pos (bytes of 255 continue the run).
@@ -340,12 +340,12 @@ __device__ __forceinline__ int dec_ext_scan(const uint8_t* in, uint32_t C, uint3
 // One sequence executed wave-wide (literal run, then match unless `last`), with the lz4_flex
 // bound checks in stream order. Used for sequences too long for a window.
 __device__ __forceinline__ int dec_seq(DecWave& w, const uint8_t* in, uint32_t lit, uint32_t ll, bool last,
-                                       uint32_t off, uint32_t ml, uint32_t st_lo, uint32_t bstart,
+                                       uint32_t off, uint32_t ml, uint32_t mis, uint32_t fill, uint32_t bstart,
                                        uint32_t limit, uint32_t cap, uint32_t hist) {
     const uint32_t produced = w.upos - bstart;
     if (ll > limit - produced) return S3HC_CORRUPT;
     if (ll > cap - produced) return S3HC_DST_TOO_SMALL;
-    dec_literals(w, in, lit, ll, st_lo, lit >= st_lo && lit + ll <= st_lo + dec::kStage);
+    dec_literals(w, in, lit, ll, mis, lit + ll + mis <= fill);  // lit >= the parse position
     if (last) return S3HC_OK;
     const uint32_t have = w.upos - bstart;
     if (off == 0 || off > have + hist) return S3HC_CORRUPT;
@@ -362,7 +362,7 @@ __device__ __forceinline__ int dec_seq(DecWave& w, const uint8_t* in, uint32_t l
 // written in the first pass. A fixed handful of LDS round trips per window instead of two per
 // sequence, and almost no scalar work.
 __device__ __forceinline__ void dec_window_exec(DecWave& w, bool isM, uint32_t S, uint32_t orel, uint32_t sl,
-                                                uint32_t lit, uint32_t ll, uint32_t off, uint32_t st_lo) {
+                                                uint32_t lit, uint32_t ll, uint32_t off, uint32_t mis) {
     using namespace dec;
     const int lane = w.lane;
     uint8_t* marks = w.marks;
@@ -372,7 +372,7 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, bool isM, uint32_t S
     if (isM && sl) marks[orel] = (uint8_t)(lane + 1);
     wave_sync();
     const uint32_t pkA = orel | (ll << 16);
-    const uint32_t pkB = off | ((lit - st_lo) << 16);
+    const uint32_t pkB = off | (((lit + mis) & kCmask) << 16);
     const uint32_t upos = w.upos;
     // Passes of 256 bytes: byte t = b + 64k + lane, k = 0..3, with every LDS read of the pass
     // issued before its writes (four independent chunks per round trip).
@@ -427,7 +427,7 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, bool isM, uint32_t S
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t mo = A[k] & 0xFFFFu, mlit = B[k] >> 16;
-            lv[k] = w.stage[(mlit + t[k] - mo) & (kStage - 1)];
+            lv[k] = w.cin[(mlit + t[k] - mo) & kCmask];
             rv[k] = w.ring[y[k] & kMask];
         }
         bool anyold = false, anypnd = false;
@@ -497,33 +497,58 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
     using namespace dec;
     const int lane = w.lane;
     const uint32_t bstart = w.upos;
+    if (C == 0) return S3HC_CORRUPT;
+    // Input ring: aligned dwords of the block (any alignment), one 256-byte chunk per lane-dword,
+    // kept kAhead bytes ahead of the parse; the next chunk's load is always in flight.
+    const uint32_t mis = (uint32_t)((uintptr_t)in & 3);
+    const uint32_t* aw = (const uint32_t*)((uintptr_t)in - mis);
+    const uint32_t kmax = (mis + C - 1) >> 2;  // last dword holding block bytes
+    const uint32_t fill_end = (mis + C + kChunk - 1) & ~(kChunk - 1);
+    uint32_t* cr = (uint32_t*)w.cin;
+    uint32_t fill;
+    uint32_t pf;
+    {
+        const uint32_t k0 = (uint32_t)lane, k1 = k0 + 64, k2 = k0 + 128;
+        const uint32_t d0 = aw[k0 < kmax ? k0 : kmax], d1 = aw[k1 < kmax ? k1 : kmax];
+        pf = aw[k2 < kmax ? k2 : kmax];
+        cr[k0] = d0;
+        cr[k1] = d1;
+        fill = 2 * kChunk;
+    }
     uint32_t q = 0;
-    uint32_t st_lo = 0xFFFFFFFFu;
     for (;;) {
         if (q >= C) return S3HC_CORRUPT;  // a token was expected
-        if (st_lo == 0xFFFFFFFFu || q < st_lo || q + 192 > st_lo + kStage) {
-            st_lo = q & ~3u;
-            const uint64_t t0 = PROF_NOW();
-            dec_stage(in, C, st_lo, w.stage, lane);
-            PROF_ADD(w.pr, 0, PROF_NOW() - t0);
-            PROF_ADD(w.pr, 9, 1);
+        {
+            const uint32_t want = q + mis + kAhead < fill_end ? q + mis + kAhead : fill_end;
+            if (fill < want) {
+                const uint64_t t0 = PROF_NOW();
+                do {
+                    cr[((fill >> 2) + lane) & (kCring / 4 - 1)] = pf;
+                    fill += kChunk;
+                    const uint32_t kn = (fill >> 2) + lane;
+                    pf = aw[kn < kmax ? kn : kmax];
+                } while (fill < want);
+                PROF_ADD(w.pr, 0, PROF_NOW() - t0);
+                PROF_ADD(w.pr, 9, 1);
+            }
+            wave_sync();
         }
         const uint64_t tp0 = PROF_NOW();
         // ---- speculative parse: lane assumes a token at qq = q + lane. Two LDS round trips
         // (token + up to two length bytes; offset + up to two match-length bytes), no branches.
         const uint32_t qq = q + lane;
-        const uint32_t i = qq - st_lo;
+        const uint32_t i = qq + mis;
         uint32_t flags, nxt, lit, ll, off, ml;
         {
-            const uint32_t w0 = lds32u(w.stage, i);
+            const uint32_t w0 = cin32(w.cin, i);
             const uint32_t t = w0 & 0xFFu, L = t >> 4, M = t & 15u;
             const uint32_t e1 = (w0 >> 8) & 0xFFu, e2 = (w0 >> 16) & 0xFFu;
             const uint32_t x1 = L == 15u ? 1u : 0u, x2 = (L == 15u && e1 == 255u) ? 1u : 0u;
             ll = L + (x1 ? e1 : 0u) + (x2 ? e2 : 0u);
             lit = qq + 1u + x1 + x2;
             const uint32_t mp = lit + ll;
-            const uint32_t mi = mp - st_lo;
-            const uint32_t w1 = lds32u(w.stage, mi < kStage ? mi : kStage);
+            const uint32_t mi = mp + mis;
+            const uint32_t w1 = cin32(w.cin, mi);
             off = w1 & 0xFFFFu;
             const uint32_t f1 = (w1 >> 16) & 0xFFu, f2 = w1 >> 24;
             const uint32_t y1 = M == 15u ? 1u : 0u, y2 = (M == 15u && f1 == 255u) ? 1u : 0u;
@@ -533,9 +558,9 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
             // stage, offset cut off, last sequence, bad literal run
             uint32_t fm = (y2 && f2 == 255u) ? F_LONG : 0u;
             fm = (nxt > C) ? F_ERR : fm;
-            fm = (mi + 4 > kStage) ? F_MORE : fm;
+            fm = (mi + 4 > fill) ? F_MORE : fm;
             fm = (C - mp < 2) ? F_ERR : fm;
-            fm = (mp == C) ? (mi > kStage ? F_MORE : F_LAST) : fm;
+            fm = (mp == C) ? (mi > fill ? F_MORE : F_LAST) : fm;
             fm = (qq >= C || lit > C || ll > C - lit) ? F_ERR : fm;
             flags = fm | ((x2 && e2 == 255u) ? F_LONG : 0u);
         }
@@ -594,7 +619,7 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
                 st = (ll > limit - produced) ? S3HC_CORRUPT : st;
                 const uint64_t bad = __ballot(isM && st != S3HC_OK);
                 if (bad) return (int)rdl((uint32_t)st, (uint32_t)__builtin_ctzll(bad));
-                dec_window_exec(w, isM, S, orel, sl, lit, ll, off, st_lo);
+                dec_window_exec(w, isM, S, orel, sl, lit, ll, off, mis);
                 PROF_ADD(w.pr, 2, PROF_NOW() - tp1);
                 PROF_ADD(w.pr, 5, 1);
                 PROF_ADD(w.pr, 6, __builtin_popcountll(members));
@@ -609,7 +634,7 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
             const uint32_t c = cur - q;
             const uint32_t f = rdl(flags, c);
             const int rc = dec_seq(w, in, rdl(lit, c), rdl(ll, c), (f & F_LAST) != 0, rdl(off, c), rdl(ml, c),
-                                   st_lo, bstart, limit, cap, hist);
+                                   mis, fill, bstart, limit, cap, hist);
             if (rc) return rc;
             if (f & F_LAST) return S3HC_OK;
             cur = rdl(nxt, c);
@@ -624,7 +649,7 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
             if (sll > C - pos) return S3HC_CORRUPT;
             const uint32_t slit = pos;
             pos += sll;
-            if (pos == C) return dec_seq(w, in, slit, sll, true, 0, 0, st_lo, bstart, limit, cap, hist);
+            if (pos == C) return dec_seq(w, in, slit, sll, true, 0, 0, mis, fill, bstart, limit, cap, hist);
             const uint32_t produced = w.upos - bstart;
             if (sll > limit - produced) return S3HC_CORRUPT;
             if (sll > cap - produced) return S3HC_DST_TOO_SMALL;
@@ -633,7 +658,7 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
             pos += 2;
             uint32_t sml = (t & 15) + 4;
             if ((t & 15) == 15 && dec_ext_scan(in, C, pos, sml, lane)) return S3HC_CORRUPT;
-            const int rc = dec_seq(w, in, slit, sll, false, soff, sml, st_lo, bstart, limit, cap, hist);
+            const int rc = dec_seq(w, in, slit, sll, false, soff, sml, mis, fill, bstart, limit, cap, hist);
             if (rc) return rc;
             cur = pos;
         }
@@ -656,8 +681,8 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     if (U.n == 0) return;
     DecWave w;
     w.ring = smem + wv * dec::kWaveLds;
-    w.stage = w.ring + dec::kRing;
-    w.marks = w.stage + dec::kStage;
+    w.cin = w.ring + dec::kRing;
+    w.marks = w.cin + dec::kCring;
     w.refs = (uint16_t*)(w.marks + dec::kWin + 64);
     w.out = dst + blk[U.first].dst_off;
     w.upos = 0;
@@ -710,7 +735,9 @@ constexpr uint32_t kFwd = 19;                               // forward bytes mea
 constexpr uint32_t kEmpty = 0xFFFFu;
 }  // namespace enc
 
-__device__ __forceinline__ uint32_t ext_bytes(uint32_t n) { return n >= 15 ? (n - 15) / 255 + 1 : 0; }
+// LZ4 length-extension bytes for a length field of n: (n - 15) / 255 + 1 for n >= 15, else 0
+// (branch-free form: (n + 240) / 255).
+__device__ __forceinline__ uint32_t ext_bytes(uint32_t n) { return (n + 240u) / 255u; }
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
 __device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t l) {
     return (uint64_t)rdl((uint32_t)v, l) | ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32);
@@ -772,7 +799,8 @@ __device__ __forceinline__ void enc_chunk_records(int lane, uint64_t hm, uint32_
     const uint32_t P = base + lane;
     const uint32_t endj = P + lenf;
     const uint32_t bh = (uint32_t)(below >> 32), bl = (uint32_t)below;
-    const int pl = bh ? 63 - __builtin_clz(bh) : (bl ? 31 - __builtin_clz(bl) : 0);
+    const int ph = 63 - __builtin_clz(bh | 1u), plo = 31 - __builtin_clz(bl | 1u);
+    const int pl = bh ? ph : plo;  // previous hop lane (any lane when there is none)
     const uint32_t pe = __shfl(endj, pl);
     const uint32_t prev = below ? pe : last_end;
     uint32_t nb = (word >> 24) & 7u;
@@ -781,7 +809,8 @@ __device__ __forceinline__ void enc_chunk_records(int lane, uint64_t hm, uint32_
     const uint32_t len = nb + lenf;
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0));
     const uint32_t gj = nseq + rank;
-    const uint32_t sz = hop ? (gj == 0 ? 0u : 1u + ext_bytes(ll)) + ll + 2u + ext_bytes(len - 4) : 0u;
+    const uint32_t tok = gj == 0 ? 0u : 1u + ext_bytes(ll);
+    const uint32_t sz = hop ? tok + ll + 2u + ext_bytes(len - 4) : 0u;
     body += rdl(wave_incl_sum(sz), 63);
     const uint32_t first = (uint32_t)__builtin_ctzll(hm);
     if (nseq == 0) ll0 = rdl(ll, first);
@@ -843,7 +872,7 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
 #ifdef S3HC_PROF
     epr[0] = PROF_NOW() - tk0;
 #endif
-    uint32_t x = seg_lo;         // greedy position: end of the last match
+    uint32_t x = seg_lo;         // greedy position (no match starts in [last_end, x))
     uint32_t last_end = seg_lo;  // end of the last recorded match (literal start)
     uint32_t nseq = 0, body = 0, ll0 = 0;
     uint2* myrec = recs + (size_t)s * kMaxSeqPerSeg;
@@ -931,18 +960,22 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
             if (x >= base + 64 || !mm[q]) continue;
             uint64_t hm = 0;
             uint32_t lenv = flen[q];
-            for (;;) {
-                const uint32_t r = x > base ? x - base : 0u;
-                if (r >= 64) break;
+            // per lane: greedy position after taking this lane's match (chunk-relative);
+            // 0x100 marks a match that reached kFwd and needs the wave-wide extension
+            const uint32_t nxr = (uint32_t)lane + lenv + (lenv == kFwd ? 0x100u : 0u);
+            uint32_t r = x > base ? x - base : 0u;
+            while (r < 64u) {
                 const uint64_t av = mm[q] & (~0ull << r);
                 if (!av) break;
                 const uint32_t j = (uint32_t)__builtin_ctzll(av);
-                const uint32_t wj = rdl(word[q], j);
-                const uint32_t P = base + j;
-                uint32_t lenf = 4u + ((wj >> 16) & 15u);
-                if (lenf == kFwd) {  // long match: wave-wide forward extension
+                hm |= 1ull << j;
+                r = rdl(nxr, j);
+                if (r & 0x100u) {  // long match: wave-wide forward extension
+                    const uint32_t wj = rdl(word[q], j);
+                    const uint32_t P = base + j;
                     const uint32_t maxf = end_lim - P;
                     const uint32_t c = P - (wj & 0xFFFFu);
+                    uint32_t lenf = kFwd;
                     while (lenf < maxf) {
                         const uint32_t rel = lenf + 4u * lane;
                         uint32_t e2;
@@ -962,10 +995,10 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
                         break;
                     }
                     lenv = (uint32_t)lane == j ? lenf : lenv;
+                    r = j + lenf;
                 }
-                hm |= 1ull << j;
-                x = P + lenf;
             }
+            x = base + r;
             if (hm) {
                 const uint64_t tf0 = PROF_NOW();
                 enc_chunk_records(lane, hm, base, word[q], lenv, last_end, nseq, body, ll0, myrec);
@@ -985,7 +1018,7 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
         S.nseq = nseq;
         S.ll0 = ll0;
         S.body = body;
-        S.trail = seg_hi - x;
+        S.trail = seg_hi - last_end;
         summ[s] = S;
     }
 }

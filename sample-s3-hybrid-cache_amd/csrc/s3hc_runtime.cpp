@@ -121,6 +121,8 @@ struct TimedSpan {
 struct s3hc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;          // content xxh32 beside the match finder
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::mutex mu;
     bool timing = false;
     std::map<std::string, float> kernel_ms;
@@ -188,6 +190,9 @@ s3hc_ctx::~s3hc_ctx() {
     for (auto& t : pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto e : event_pool) (void)hipEventDestroy(e);
     delete host_plan;
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -272,10 +277,17 @@ static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t
     const uint32_t nseg = (uint32_t)P->seg_block.size(), nb = (uint32_t)P->blocks.size();
     const uint32_t nf = (uint32_t)P->frame_blk0.size(), ni = (uint32_t)P->item_blk0.size();
     KTimer T(ctx, st);
-    T.begin("xxh32");
-    HIPCHK(launch_xxh32(d_src, P->d_frame_src_off.as<uint64_t>(), P->d_frame_src_len.as<uint32_t>(), nf,
-                        P->d_frame_hash.as<uint32_t>(), st));
-    T.end();
+    // content checksums run on the side stream, overlapping the match finder; emit joins
+    HIPCHK(hipEventRecord(ctx->ev_fork, st));
+    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    {
+        KTimer TS(ctx, ctx->side);
+        TS.begin("xxh32");
+        HIPCHK(launch_xxh32(d_src, P->d_frame_src_off.as<uint64_t>(), P->d_frame_src_len.as<uint32_t>(), nf,
+                            P->d_frame_hash.as<uint32_t>(), ctx->side));
+        TS.end();
+    }
+    HIPCHK(hipEventRecord(ctx->ev_join, ctx->side));
     T.begin("enc_parse");
     HIPCHK(launch_enc_parse(d_src, P->d_blocks.as<EncBlock>(), P->d_seg_block.as<uint32_t>(), nseg,
                             P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), st));
@@ -286,6 +298,7 @@ static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t
                             P->d_blk_carry.as<uint32_t>(), st));
     HIPCHK(launch_scan(P->d_blk_size.as<uint32_t>(), nb, P->d_blk_off.as<uint64_t>(), P->d_total.as<uint64_t>(), st));
     T.end();
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev_join, 0));
     T.begin("enc_emit");
     HIPCHK(launch_enc_emit(d_src, P->d_blocks.as<EncBlock>(), P->d_seg_block.as<uint32_t>(), nseg,
                            P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), P->d_place.as<SegPlace>(),
@@ -309,6 +322,9 @@ extern "C" int s3hc_create(s3hc_ctx** out, int device) {
     std::unique_ptr<s3hc_ctx> c(new s3hc_ctx);
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     *out = c.release();
     return S3HC_OK;
 }
