@@ -882,20 +882,22 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
         const uint64_t tc0 = PROF_NOW();
         PROF_ADD(epr, 6, 1);
         // ---- A: table pass
-        uint32_t vv[kSteps], vm[kSteps], cc[kSteps];
+        uint32_t vv[kSteps], vm[kSteps], vm8[kSteps], cc[kSteps];
 #pragma unroll
         for (uint32_t q = 0; q < kSteps; ++q) {
             const uint32_t P = sb + 64 * q + lane;
             const uint32_t i = P - pw_lo;
             const uint32_t a = i >> 2, sh = i & 3;
-            const uint32_t w0 = dw[a], w1 = dw[a + 1], wp = dw[(int)a - 1];
+            const uint32_t w0 = dw[a], w1 = dw[a + 1], wp = dw[(int)a - 1], wpp = dw[(int)a - 2];
             vv[q] = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            vm[q] = __builtin_amdgcn_alignbyte(w0, wp, sh);  // bytes [P-4, P)
+            vm[q] = __builtin_amdgcn_alignbyte(w0, wp, sh);    // bytes [P-4, P)
+            vm8[q] = __builtin_amdgcn_alignbyte(wp, wpp, sh);  // bytes [P-8, P-4)
             const uint32_t h = hash4(vv[q]);
             cc[q] = tbl[h];
             tbl[P < sb_end ? h : kTbl] = (uint16_t)i;
         }
-        // ---- B: verify + measure both candidates
+        // ---- B: verify + measure both candidates (table: one LDS round trip; distance 1..4:
+        // from the position's own bytes, no reads)
         uint32_t word[kSteps], flen[kSteps];
         uint64_t mm[kSteps];
 #pragma unroll
@@ -904,52 +906,54 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
             const bool valid = P < sb_end;
             const uint32_t i = P - pw_lo;
             const uint32_t v = vv[q], vm4 = vm[q];
-            const uint32_t df = (i >= 1 && __builtin_amdgcn_alignbyte(v, vm4, 3) == v) ? 1u
-                              : (i >= 2 && __builtin_amdgcn_alignbyte(v, vm4, 2) == v) ? 2u
-                              : (i >= 3 && __builtin_amdgcn_alignbyte(v, vm4, 1) == v) ? 3u
-                              : (i >= 4 && vm4 == v) ? 4u : 0u;
+            const bool r1 = (__builtin_amdgcn_alignbyte(v, vm4, 3) == v) & (i >= 1);
+            const bool r2 = (__builtin_amdgcn_alignbyte(v, vm4, 2) == v) & (i >= 2);
+            const bool r3 = (__builtin_amdgcn_alignbyte(v, vm4, 1) == v) & (i >= 3);
+            const bool r4 = (vm4 == v) & (i >= 4);
+            const uint32_t df = r1 ? 1u : (r2 ? 2u : (r3 ? 3u : (r4 ? 4u : 0u)));
             const uint32_t c16 = cc[q];
-            const bool tin = c16 != kEmpty && c16 < i;
-            const uint32_t ct = tin ? c16 : i, cf = i - df;
-            const uint32_t a = i >> 2, sh = i & 3;
-            const uint32_t ta = ct >> 2, ts = ct & 3, fa = cf >> 2, fs = cf & 3;
-            uint32_t O[5], T[7], F[7];
+            const bool tin = (c16 != kEmpty) & (c16 < i);
+            const uint32_t ct = tin ? c16 : i;
+            const uint32_t a = i >> 2, sh = i & 3, ta = ct >> 2, ts = ct & 3;
+            uint32_t O[5], T[7];
 #pragma unroll
             for (int j = 0; j < 5; ++j) O[j] = dw[a + 1 + j];
 #pragma unroll
             for (int j = 0; j < 7; ++j) T[j] = dw[(int)ta - 1 + j];
+            uint32_t Q[5];  // Q[k] = bytes [P+4k, P+4k+4)
+            Q[0] = v;
 #pragma unroll
-            for (int j = 0; j < 7; ++j) F[j] = dw[(int)fa - 1 + j];
+            for (int j = 0; j < 4; ++j) Q[j + 1] = __builtin_amdgcn_alignbyte(O[j + 1], O[j], sh);
             const uint32_t maxf = end_lim - P;  // >= 4 for P <= smax
-            // forward length against candidate dwords C (C[j] holds bytes c-4+4j .. c+4j)
-            auto fwd = [&](const uint32_t* C, uint32_t cs) -> uint32_t {
-                uint32_t len = 20u;
+            const uint32_t fs = (4u - df) & 3u;
+            uint32_t lt = 20u, lf = 20u;
 #pragma unroll
-                for (int j = 3; j >= 0; --j) {
-                    const uint32_t dx = __builtin_amdgcn_alignbyte(O[j + 1], O[j], sh) ^
-                                        __builtin_amdgcn_alignbyte(C[j + 3], C[j + 2], cs);
-                    len = dx ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dx) >> 3) : len;
-                }
-                len = len > kFwd ? kFwd : len;
-                return len > maxf ? maxf : len;
-            };
-            auto bwd = [&](const uint32_t* C, uint32_t cs, uint32_t ci) -> uint32_t {
-                const uint32_t dx = vm4 ^ __builtin_amdgcn_alignbyte(C[1], C[0], cs);
-                uint32_t nb = dx ? (uint32_t)__builtin_clz(dx) >> 3 : 4u;
-                const uint32_t lim = ci < i ? ci : i;
-                return nb > lim ? lim : nb;
-            };
-            const bool gt = valid && tin && __builtin_amdgcn_alignbyte(T[2], T[1], ts) == v;
-            const bool gf = valid && df != 0;
-            const uint32_t lt = fwd(T, ts), lf = fwd(F, fs);
-            const bool ut = gt && (!gf || lt >= lf);
+            for (int j = 3; j >= 0; --j) {
+                const uint32_t dt = Q[j + 1] ^ __builtin_amdgcn_alignbyte(T[j + 3], T[j + 2], ts);
+                const uint32_t dfw = Q[j + 1] ^ __builtin_amdgcn_alignbyte(Q[j + 1], Q[j], fs);
+                lt = dt ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dt) >> 3) : lt;
+                lf = dfw ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dfw) >> 3) : lf;
+            }
+            lt = lt > kFwd ? kFwd : lt;
+            lt = lt > maxf ? maxf : lt;
+            lf = lf > kFwd ? kFwd : lf;
+            lf = lf > maxf ? maxf : lf;
+            const uint32_t bt = vm4 ^ __builtin_amdgcn_alignbyte(T[1], T[0], ts);
+            const uint32_t bf = vm4 ^ __builtin_amdgcn_alignbyte(vm4, vm8[q], fs);
+            uint32_t nbt = bt ? (uint32_t)__builtin_clz(bt) >> 3 : 4u;
+            uint32_t nbf = bf ? (uint32_t)__builtin_clz(bf) >> 3 : 4u;
+            nbt = nbt > ct ? ct : nbt;                      // ct < i
+            nbf = nbf > i - df ? i - df : nbf;
+            const bool gt = valid & tin & (__builtin_amdgcn_alignbyte(T[2], T[1], ts) == v);
+            const bool gf = valid & (df != 0);
+            const bool ut = gt & (!gf | (lt >= lf));
             const uint32_t len = ut ? lt : lf;
-            const uint32_t nb = ut ? bwd(T, ts, ct) : bwd(F, fs, cf);
-            const uint32_t dist = i - (ut ? ct : cf);
-            const bool good = gt || gf;
+            const uint32_t nb = ut ? nbt : nbf;
+            const uint32_t dist = ut ? i - ct : df;
             word[q] = dist | ((len - 4) << 16) | (nb << 24);
             flen[q] = len;
-            mm[q] = __ballot(good);
+            mm[q] = __ballot(gt | gf);
+            if (q & 1) wave_sync();  // bounds the loads hoisted ahead (VGPR pressure)
         }
         const uint64_t tc1 = PROF_NOW();
         PROF_ADD(epr, 1, tc1 - tc0);

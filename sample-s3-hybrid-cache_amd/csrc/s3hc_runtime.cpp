@@ -282,7 +282,7 @@ static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t
     HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     {
         KTimer TS(ctx, ctx->side);
-        TS.begin("xxh32");
+        TS.begin("xxh32_side");  // overlaps enc_parse: its span is not exclusive time
         HIPCHK(launch_xxh32(d_src, P->d_frame_src_off.as<uint64_t>(), P->d_frame_src_len.as<uint32_t>(), nf,
                             P->d_frame_hash.as<uint32_t>(), ctx->side));
         TS.end();
@@ -322,7 +322,12 @@ extern "C" int s3hc_create(s3hc_ctx** out, int device) {
     std::unique_ptr<s3hc_ctx> c(new s3hc_ctx);
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    {
+        // the side stream's few checksum waves are dispatched ahead of the match finder's
+        int least = 0, greatest = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, greatest));
+    }
     HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     *out = c.release();
