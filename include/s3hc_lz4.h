@@ -95,8 +95,9 @@ void s3hc_stream_close(s3hc_stream* s);
 int s3hc_plan_encode(s3hc_ctx* ctx, const uint64_t* src_off, const uint32_t* len,
                      const uint8_t* mode, uint32_t n, s3hc_plan** out);
 /* Frames of item i land contiguously in d_dst at d_item_off[i], d_item_len[i] bytes
- * (device arrays written by the call). *total (host) = framed bytes of the batch;
- * dst_cap must be >= s3hc_plan_dst_bound(plan). stream = hipStream_t (NULL = ctx stream). */
+ * (device arrays written by the call; the batch's frames are packed in item order).
+ * dst_cap must be >= s3hc_plan_dst_bound(plan). stream = hipStream_t (NULL = ctx stream);
+ * a plan's scratch belongs to one call in flight at a time. */
 int s3hc_encode_dev(s3hc_ctx* ctx, s3hc_plan* plan, const uint8_t* d_src, uint8_t* d_dst,
                     uint64_t dst_cap, uint64_t* d_item_off, uint32_t* d_item_len, void* stream);
 uint64_t s3hc_plan_dst_bound(const s3hc_plan* plan);
@@ -127,6 +128,16 @@ int s3hc_dev_free(s3hc_ctx* ctx, void* p);
 int s3hc_memcpy(s3hc_ctx* ctx, void* dst, const void* src, size_t n, int kind);
 int s3hc_memset(s3hc_ctx* ctx, void* dst, int value, size_t n);
 int s3hc_sync(s3hc_ctx* ctx);
+
+/* ---- pipelined host<->device batches: pinned host memory and caller queues. A queue is a
+ * hipStream_t on the context's device, usable as the `stream` of s3hc_encode_dev /
+ * s3hc_decode_dev; s3hc_memcpy_async orders a copy on it (kind as above). */
+int s3hc_host_alloc(s3hc_ctx* ctx, size_t n, void** out);
+int s3hc_host_free(s3hc_ctx* ctx, void* p);
+int s3hc_queue_create(s3hc_ctx* ctx, void** out);
+int s3hc_queue_destroy(s3hc_ctx* ctx, void* q);
+int s3hc_queue_sync(s3hc_ctx* ctx, void* q);
+int s3hc_memcpy_async(s3hc_ctx* ctx, void* dst, const void* src, size_t n, int kind, void* q);
 
 /* ---- CompressionHandler mirror (compression.rs:169-604) ------------------- */
 /* The host-side mirror of the reference's handler: same decision inputs, same six

@@ -159,12 +159,11 @@ __device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t in) {
     return acc * XP1;
 }
 
-// out[r] = xxh32(base + off[r], len[r], seed 0). Lanes 4r..4r+3 run the 4 accumulator chains.
-__global__ __launch_bounds__(256) void k_xxh32_ranges(const uint8_t* __restrict__ base,
-                                                      const uint64_t* __restrict__ off,
-                                                      const uint32_t* __restrict__ len, uint32_t n,
-                                                      uint32_t* __restrict__ out) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+// out[r] = xxh32(base + off[r], len[r], seed 0). Lanes 4r..4r+3 run the 4 accumulator chains
+// (gid = global thread index of the calling grid's xxh32 threads).
+__device__ __forceinline__ void xxh32_ranges_dev(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                 const uint32_t* __restrict__ len, uint32_t n,
+                                                 uint32_t* __restrict__ out, uint32_t gid) {
     const uint32_t r = gid >> 2, a = gid & 3;
     const int lane = lane_id();
     const bool act = r < n;
@@ -211,6 +210,12 @@ __global__ __launch_bounds__(256) void k_xxh32_ranges(const uint8_t* __restrict_
     h ^= h >> 16;
     out[r] = h;
 }
+__global__ __launch_bounds__(256) void k_xxh32_ranges(const uint8_t* __restrict__ base,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ len, uint32_t n,
+                                                      uint32_t* __restrict__ out) {
+    xxh32_ranges_dev(base, off, len, n, out, blockIdx.x * blockDim.x + threadIdx.x);
+}
 
 // ================================================================== decode
 namespace dec {
@@ -222,7 +227,8 @@ constexpr uint32_t kRing = 4096;   // recent output kept in LDS per wave (match 
 constexpr uint32_t kMask = kRing - 1;
 constexpr uint32_t kFlush = 1024;  // ring -> HBM flush granule
 constexpr uint32_t kWin = 1024;    // output bytes executed per window (byte-parallel)
-constexpr uint32_t kWaveLds = kRing + kCring + (kWin + 64) + 2 * kWin;
+constexpr uint32_t kSink = 192;    // per-lane store sink: 64 B for ring bytes, 128 B for refs
+constexpr uint32_t kWaveLds = kRing + kCring + (kWin + 64) + 2 * kWin + kSink;
 constexpr int kWaves = 4;
 enum : uint32_t { F_ERR = 1, F_LAST = 2, F_LONG = 4, F_MORE = 8 };
 }  // namespace dec
@@ -232,6 +238,7 @@ struct DecWave {
     uint8_t* cin;        // kCring bytes: compressed input, byte p of the block at (p + mis) & kCmask
     uint8_t* marks;      // kWin + 64 bytes: sequence start marks of the current window
     uint16_t* refs;      // kWin entries: in-window match source of each output byte
+    uint8_t* sink;       // kSink bytes: target of stores from lanes with nothing to store
     uint8_t* out;        // unit output base in HBM
 #ifdef S3HC_PROF
     uint64_t pr[16];
@@ -430,28 +437,37 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, bool isM, uint32_t S
             lv[k] = w.cin[(mlit + t[k] - mo) & kCmask];
             rv[k] = w.ring[y[k] & kMask];
         }
-        bool anyold = false, anypnd = false;
-        bool old[4];
+        bool anypnd = false;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             val[k] = lit_[k] ? lv[k] : rv[k];
-            const bool ok = t[k] < S;
-            const uint32_t ry = y[k] - upos;  // < S: source inside the window
-            pnd[k] = ok && !lit_[k] && ry < S && ry >= b;  // earlier passes are final in the ring
-            old[k] = ok && !lit_[k] && ry >= S && y[k] + (kRing - S) < upos;
-            anyold |= old[k];
+            // literal bytes get ry = ~0 (never pending); (ry - b) < (S - b) <=> b <= ry < S
+            const uint32_t ry = lit_[k] ? 0xFFFFFFFFu : y[k] - upos;
+            pnd[k] = (t[k] < S) & (ry - b < S - b);  // earlier passes are final in the ring
             anypnd |= pnd[k];
         }
-        if (__ballot(anyold)) {           // older than the ring: already in HBM
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (old[k]) val[k] = w.out[y[k]];
-        }
+        // every lane stores; bytes past the window go to a per-lane sink (no exec masking)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (t[k] < S) {
-                w.ring[(upos + t[k]) & kMask] = (uint8_t)val[k];
-                refs[t[k]] = (uint16_t)(pnd[k] ? y[k] - upos : 0xFFFFu);
+            const bool ok = t[k] < S;
+            uint8_t* rp = ok ? w.ring + ((upos + t[k]) & kMask) : w.sink + lane;
+            uint16_t* fp = ok ? refs + t[k] : (uint16_t*)(w.sink + 64) + lane;
+            *rp = (uint8_t)val[k];
+            *fp = (uint16_t)(pnd[k] ? y[k] - upos : 0xFFFFu);
+        }
+        if (upos > kRing - S) {
+            // sources older than the ring are read back from HBM (already flushed); kept apart
+            // so the common path never waits on the wave's outstanding flush stores
+            bool old[4], anyold = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                old[k] = (t[k] < S) & !lit_[k] & (y[k] < upos - (kRing - S));
+                anyold |= old[k];
+            }
+            if (__ballot(anyold)) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (old[k]) w.ring[(upos + t[k]) & kMask] = w.out[y[k]];
             }
         }
         if (__ballot(anypnd)) {
@@ -684,6 +700,7 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     w.cin = w.ring + dec::kRing;
     w.marks = w.cin + dec::kCring;
     w.refs = (uint16_t*)(w.marks + dec::kWin + 64);
+    w.sink = (uint8_t*)(w.refs + dec::kWin);
     w.out = dst + blk[U.first].dst_off;
     w.upos = 0;
     w.flushed = 0;
@@ -728,7 +745,8 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
 // ================================================================== encode
 namespace enc {
 constexpr uint32_t kPad = 16;                               // front pad: reads at i-8 stay in bounds
-constexpr uint32_t kIn = kPad + kPrewarm + kSeg + 128;      // staged input bytes (+ read-ahead pad)
+constexpr uint32_t kGIn = kPad + kPrewarm + kGroupSegs * kSeg + 128;  // a group's staged input (+ read-ahead)
+constexpr uint32_t kGThreads = 64 * kGroupSegs;
 constexpr uint32_t kTbl = 1u << kHashLog;
 constexpr uint32_t kSteps = 8;                              // 64-position steps per sub-block
 constexpr uint32_t kFwd = 19;                               // forward bytes measured per probe (4 + 15)
@@ -746,20 +764,20 @@ __device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t l) {
 // Stage block bytes [lo, hi) into lds (lds[x - lo]); any alignment. Every lane issues all of
 // its loads (8 x 16 B per pass) before the first LDS store, so staging costs one HBM round trip
 // per 8 KiB instead of one per dword.
-__device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* lds, int lane) {
+__device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* lds, uint32_t lane, uint32_t nthr) {
     const uint32_t n = hi - lo;
     const uint8_t* g = blk + lo;
     const uint32_t nv = n >> 4;  // whole 16-byte vectors
     if (nv && (((uintptr_t)g) & 15) == 0) {
         const uint4* sv = (const uint4*)g;
-        for (uint32_t base = 0; base < nv; base += 64 * 8) {
+        for (uint32_t base = 0; base < nv; base += nthr * 8) {
             // loads are unconditional (clamped index) so the group stays in registers
             uint4 v0, v1, v2, v3, v4, v5, v6, v7;
-#define S3HC_LD(q, vq) { const uint32_t j = base + lane + 64 * q; vq = sv[j < nv ? j : nv - 1]; }
+#define S3HC_LD(q, vq) { const uint32_t j = base + lane + nthr * q; vq = sv[j < nv ? j : nv - 1]; }
             S3HC_LD(0, v0) S3HC_LD(1, v1) S3HC_LD(2, v2) S3HC_LD(3, v3)
             S3HC_LD(4, v4) S3HC_LD(5, v5) S3HC_LD(6, v6) S3HC_LD(7, v7)
 #undef S3HC_LD
-#define S3HC_ST(q, vq) { const uint32_t j = base + lane + 64 * q; if (j < nv) *(uint4*)(lds + 16 * j) = vq; }
+#define S3HC_ST(q, vq) { const uint32_t j = base + lane + nthr * q; if (j < nv) *(uint4*)(lds + 16 * j) = vq; }
             S3HC_ST(0, v0) S3HC_ST(1, v1) S3HC_ST(2, v2) S3HC_ST(3, v3)
             S3HC_ST(4, v4) S3HC_ST(5, v5) S3HC_ST(6, v6) S3HC_ST(7, v7)
 #undef S3HC_ST
@@ -768,8 +786,8 @@ __device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* 
         const uintptr_t a = (uintptr_t)g & ~(uintptr_t)3;
         const uint32_t sh = (uint32_t)((uintptr_t)g & 3);
         const uint32_t* sw = (const uint32_t*)a;
-        for (uint32_t base = 0; base < nv; base += 64 * 2) {
-            const uint32_t ja = base + lane, jb = base + lane + 64;
+        for (uint32_t base = 0; base < nv; base += nthr * 2) {
+            const uint32_t ja = base + lane, jb = base + lane + nthr;
             const uint32_t ka = ja < nv ? ja : nv - 1, kb = jb < nv ? jb : nv - 1;
             const uint32_t a0 = sw[4 * ka], a1 = sw[4 * ka + 1], a2 = sw[4 * ka + 2], a3 = sw[4 * ka + 3];
             const uint32_t a4 = sh ? sw[4 * ka + 4] : 0u;  // holds valid bytes only when sh != 0
@@ -783,17 +801,16 @@ __device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* 
                                                       __builtin_amdgcn_alignbyte(b3, b2, sh), __builtin_amdgcn_alignbyte(b4, b3, sh));
         }
     }
-    for (uint32_t t = 16 * nv + lane; t < n; t += 64) lds[t] = g[t];
-    wave_sync();
+    for (uint32_t t = 16 * nv + lane; t < n; t += nthr) lds[t] = g[t];
 }
 
 // Lane-parallel LZ4 sequence records for the greedy hops of one 64-position chunk (bit j of
 // hm = a match taken at base + j; lane j holds that position's probe word and forward length):
 // clip each backward extension at the previous match end, form (literal length, match length,
 // offset), add up the encoded sizes, store the records.
-__device__ __forceinline__ void enc_chunk_records(int lane, uint64_t hm, uint32_t base, uint32_t word, uint32_t lenf,
-                                                  uint32_t& last_end, uint32_t& nseq, uint32_t& body,
-                                                  uint32_t& ll0, uint2* myrec) {
+__device__ __forceinline__ uint32_t enc_chunk_records(int lane, uint64_t hm, uint32_t base, uint32_t word,
+                                                      uint32_t lenf, uint32_t last_end, uint32_t nseq,
+                                                      uint32_t& ll0, uint2* myrec) {
     const bool hop = (hm >> lane) & 1ull;
     const uint64_t below = hm & ((1ull << lane) - 1ull);
     const uint32_t P = base + lane;
@@ -811,12 +828,9 @@ __device__ __forceinline__ void enc_chunk_records(int lane, uint64_t hm, uint32_
     const uint32_t gj = nseq + rank;
     const uint32_t tok = gj == 0 ? 0u : 1u + ext_bytes(ll);
     const uint32_t sz = hop ? tok + ll + 2u + ext_bytes(len - 4) : 0u;
-    body += rdl(wave_incl_sum(sz), 63);
-    const uint32_t first = (uint32_t)__builtin_ctzll(hm);
-    if (nseq == 0) ll0 = rdl(ll, first);
+    if (nseq == 0) ll0 = rdl(ll, (uint32_t)__builtin_ctzll(hm));
     if (hop) myrec[gj] = make_uint2(ll | (len << 16), word & 0xFFFFu);
-    last_end = rdl(endj, 63u - (uint32_t)__builtin_clzll(hm));
-    nseq += (uint32_t)__builtin_popcountll(hm);
+    return rdl(wave_incl_sum(sz), 63);  // encoded bytes of these sequences
 }
 
 // Match finding for one 4 KiB segment per wave (the segment's 4 KiB prefix window is staged
@@ -832,34 +846,54 @@ __device__ __forceinline__ void enc_chunk_records(int lane, uint64_t hm, uint32_
 //      or after the greedy position (s_ff1), its word by v_readlane, long matches extended
 //      wave-wide; the chunk's hops then become sequence records lane-parallel.
 // Matches end inside the segment, so segments are independent; k_enc_sizes stitches them.
-__global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ src,
-                                                   const EncBlock* __restrict__ blocks,
-                                                   const uint32_t* __restrict__ seg_block, uint32_t nseg,
-                                                   uint2* __restrict__ recs, SegSummary* __restrict__ summ) {
+__global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __restrict__ src,
+                                                              const EncBlock* __restrict__ blocks,
+                                                              const uint2* __restrict__ groups, uint32_t ngroups,
+                                                              uint32_t nxx, const uint64_t* __restrict__ fsrc_off,
+                                                              const uint32_t* __restrict__ fsrc_len, uint32_t nframes,
+                                                              uint32_t* __restrict__ fhash, uint2* __restrict__ recs,
+                                                              SegSummary* __restrict__ summ) {
     using namespace enc;
-    __shared__ __attribute__((aligned(16))) uint8_t inb_raw[kIn];
-    __shared__ __attribute__((aligned(16))) uint16_t tbl[kTbl + 8];  // slot kTbl: sink for idle lanes
+    __shared__ __attribute__((aligned(16))) uint8_t inb_raw[kGIn];
+    __shared__ __attribute__((aligned(16))) uint16_t tbl_all[kGroupSegs][kTbl + 8];  // slot kTbl: sink
+    // The first nxx workgroups compute the frames' content xxh32 (they are dispatched first and
+    // overlap the match finding; the emitter reads the hashes).
+    if (blockIdx.x < nxx) {
+        xxh32_ranges_dev(src, fsrc_off, fsrc_len, nframes, fhash, blockIdx.x * kGThreads + threadIdx.x);
+        return;
+    }
+    const uint32_t gi = blockIdx.x - nxx;
+    if (gi >= ngroups) return;
+    // A group = up to kGroupSegs consecutive segments of one block, one wave each, sharing one
+    // staged copy of the group's input and the 4 KiB window before it.
+    const uint2 G = groups[gi];
+    const EncBlock B = blocks[G.x];
+    const uint32_t U = B.len;
+    const uint32_t ns = B.nseg - G.y < kGroupSegs ? B.nseg - G.y : kGroupSegs;
+    const uint32_t g_lo = G.y * kSeg;
+    const uint32_t g_hi = g_lo + ns * kSeg < U ? g_lo + ns * kSeg : U;
+    const uint32_t stage_lo = g_lo > kPrewarm ? g_lo - kPrewarm : 0;
+    const uint32_t stage_hi = g_hi + 64 < U ? g_hi + 64 : U;
+    const uint8_t* bin = src + B.src_off;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = lane_id();
-    const uint32_t s = blockIdx.x;
-    if (s >= nseg) return;
-    const uint32_t b = seg_block[s];
-    const EncBlock B = blocks[b];
-    if (B.flags & (EB_STORE | EB_EMPTY)) return;
+    uint16_t* tbl = tbl_all[wv];
+    for (uint32_t t = lane; t < (kTbl + 8) / 8; t += 64) ((uint4*)tbl)[t] = make_uint4(~0u, ~0u, ~0u, ~0u);
+    stage_in(bin, stage_lo, stage_hi, inb_raw + kPad, threadIdx.x, kGThreads);
+    __syncthreads();
+    if (wv >= ns) return;  // no barrier below
 #ifdef S3HC_PROF
     uint64_t epr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t tk0 = PROF_NOW();
 #endif
-    uint8_t* inb = inb_raw + kPad;               // inb[x - pw_lo] = block byte x
-    const uint32_t* dw = (const uint32_t*)inb;   // dw[-4 .. -1] is the pad
-    const uint32_t U = B.len;
-    const uint32_t k = s - B.seg0;
+    const uint32_t k = G.y + wv;
+    const uint32_t s = B.seg0 + k;
     const uint32_t seg_lo = k * kSeg;
     const uint32_t seg_hi = seg_lo + kSeg < U ? seg_lo + kSeg : U;
     const uint32_t pw_lo = seg_lo > kPrewarm ? seg_lo - kPrewarm : 0;
-    const uint32_t st_hi = seg_hi + 64 < U ? seg_hi + 64 : U;
-    const uint8_t* bin = src + B.src_off;
-    for (uint32_t t = lane; t < (kTbl + 8) / 8; t += 64) ((uint4*)tbl)[t] = make_uint4(~0u, ~0u, ~0u, ~0u);
-    stage_in(bin, pw_lo, st_hi, inb, lane);
+    uint8_t* inb = inb_raw + kPad + (pw_lo - stage_lo);  // inb[x - pw_lo] = block byte x
+    const uint32_t* dw = (const uint32_t*)inb;          // dw[-2 .. -1]: pad or earlier bytes
+    const uint32_t ia_max = kGIn - kPad - (pw_lo - stage_lo) - 8;  // last safe lds32u index
     // Largest match end / start (LZ4: the last 5 bytes are literals and the last match starts
     // at least 12 bytes before the block end; segment matches end inside the segment).
     const uint32_t blk_end_lim = U >= 5 ? U - 5 : 0;
@@ -957,17 +991,22 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
         }
         const uint64_t tc1 = PROF_NOW();
         PROF_ADD(epr, 1, tc1 - tc0);
-        // ---- C: greedy walk per chunk, records per chunk
+        // ---- C: greedy walk over the chunks (scalar), then every chunk's records at once (the
+        // chunks' record passes are independent, so their latencies overlap)
+        uint64_t hms[kSteps];
+        uint32_t le_in[kSteps], ns_in[kSteps];
 #pragma unroll
         for (uint32_t q = 0; q < kSteps; ++q) {
             const uint32_t base = sb + 64 * q;
+            hms[q] = 0;
+            le_in[q] = last_end;
+            ns_in[q] = nseq;
             if (x >= base + 64 || !mm[q]) continue;
             uint64_t hm = 0;
-            uint32_t lenv = flen[q];
             // per lane: greedy position after taking this lane's match (chunk-relative);
             // 0x100 marks a match that reached kFwd and needs the wave-wide extension
-            const uint32_t nxr = (uint32_t)lane + lenv + (lenv == kFwd ? 0x100u : 0u);
-            uint32_t r = x > base ? x - base : 0u;
+            const uint32_t nxr = (uint32_t)lane + flen[q] + (flen[q] == kFwd ? 0x100u : 0u);
+            uint32_t r = x > base ? x - base : 0u, rend = 0;
             while (r < 64u) {
                 const uint64_t av = mm[q] & (~0ull << r);
                 if (!av) break;
@@ -987,7 +1026,7 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
                             e2 = 0;
                         } else {
                             uint32_t ia = P + rel - pw_lo;
-                            if (ia > kIn - kPad - 8) ia = kIn - kPad - 8;
+                            if (ia > ia_max) ia = ia_max;
                             const uint32_t xa = lds32u(inb, ia), ya = lds32u(inb, c + rel - pw_lo);
                             e2 = xa == ya ? 4u : (uint32_t)__builtin_ctz(xa ^ ya) >> 3;
                             if (e2 > maxf - rel) e2 = maxf - rel;
@@ -998,17 +1037,23 @@ __global__ __launch_bounds__(64) void k_enc_parse(const uint8_t* __restrict__ sr
                         lenf += 4u * g + rdl(e2, g);
                         break;
                     }
-                    lenv = (uint32_t)lane == j ? lenf : lenv;
+                    flen[q] = (uint32_t)lane == j ? lenf : flen[q];
                     r = j + lenf;
                 }
+                rend = r;
             }
             x = base + r;
             if (hm) {
-                const uint64_t tf0 = PROF_NOW();
-                enc_chunk_records(lane, hm, base, word[q], lenv, last_end, nseq, body, ll0, myrec);
-                PROF_ADD(epr, 4, PROF_NOW() - tf0);
+                hms[q] = hm;
+                last_end = base + rend;
+                nseq += (uint32_t)__builtin_popcountll(hm);
             }
         }
+        const uint64_t tf0 = PROF_NOW();
+#pragma unroll
+        for (uint32_t q = 0; q < kSteps; ++q)
+            if (hms[q]) body += enc_chunk_records(lane, hms[q], sb + 64 * q, word[q], flen[q], le_in[q], ns_in[q], ll0, myrec);
+        PROF_ADD(epr, 4, PROF_NOW() - tf0);
         PROF_ADD(epr, 3, PROF_NOW() - tc1);
     }
 #ifdef S3HC_PROF
@@ -1149,7 +1194,8 @@ __global__ __launch_bounds__(256) void k_enc_emit(const uint8_t* __restrict__ sr
         wave_copy_global(pay + o, bin + seg_lo - P.carry, P.carry, lane);
         o += P.carry;
         // body: records -> LDS, then one coalesced store
-        stage_in(bin, seg_lo, seg_hi, ib, lane);
+        stage_in(bin, seg_lo, seg_hi, ib, lane, 64);
+        wave_sync();
         uint32_t ob_len = 0;   // bytes assembled in ob
         uint32_t in_pos = 0;   // segment-relative input cursor
         for (uint32_t g = 0; g < S.nseq; g += 64) {
@@ -1439,11 +1485,13 @@ hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock*
                        units, nunits, blk_out, blk_status);
     return hipGetLastError();
 }
-hipError_t launch_enc_parse(const uint8_t* src, const EncBlock* blocks, const uint32_t* seg_block, uint32_t nseg,
+hipError_t launch_enc_parse(const uint8_t* src, const EncBlock* blocks, const uint2* groups, uint32_t ngroups,
+                            const uint64_t* fsrc_off, const uint32_t* fsrc_len, uint32_t nframes, uint32_t* fhash,
                             uint2* recs, SegSummary* summ, hipStream_t st) {
-    if (!nseg) return hipSuccess;
-    hipLaunchKernelGGL(k_enc_parse, dim3(nseg), dim3(64), 0, st, src, blocks,
-                       seg_block, nseg, recs, summ);
+    const uint32_t nxx = cdiv((uint64_t)nframes * 4, enc::kGThreads);
+    if (!ngroups && !nxx) return hipSuccess;
+    hipLaunchKernelGGL(k_enc_parse, dim3(nxx + ngroups), dim3(enc::kGThreads), 0, st, src, blocks, groups, ngroups,
+                       nxx, fsrc_off, fsrc_len, nframes, fhash, recs, summ);
     return hipGetLastError();
 }
 hipError_t launch_enc_sizes(const EncBlock* blocks, uint32_t nblocks, const SegSummary* summ, SegPlace* place,

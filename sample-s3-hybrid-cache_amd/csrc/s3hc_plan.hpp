@@ -16,9 +16,17 @@ constexpr uint8_t kFlgIndependentChecksum = 0x64;  // version 01 | independent |
 
 // ---- encode -------------------------------------------------------------
 constexpr uint32_t kSeg = 4096;          // bytes of input per match-finding wave
-constexpr uint32_t kPrewarm = 4096;      // bytes before a segment inserted into its hash table
-constexpr uint32_t kHashLog = 11;        // per-wave hash table: 2^11 x u16 positions
+// kernel-only tuning constants (diagnostic builds may override them; the host never reads them)
+#ifndef S3HC_PREWARM
+#define S3HC_PREWARM 4096
+#endif
+#ifndef S3HC_HASHLOG
+#define S3HC_HASHLOG 11
+#endif
+constexpr uint32_t kPrewarm = S3HC_PREWARM;  // bytes before a segment inserted into its hash table
+constexpr uint32_t kHashLog = S3HC_HASHLOG;  // per-wave hash table: 2^11 x u16 positions
 constexpr uint32_t kMaxSeqPerSeg = kSeg / 4 + 1;
+constexpr uint32_t kGroupSegs = 8;       // segments (waves) per match-finding workgroup
 
 enum : uint32_t {
     EB_STORE = 1,        // write this block stored (store-mode frame or caller decision)

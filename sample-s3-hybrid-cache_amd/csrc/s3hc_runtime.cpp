@@ -24,8 +24,8 @@ namespace s3hc {
 hipError_t launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_decode_units(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*,
                                int32_t*, hipStream_t);
-hipError_t launch_enc_parse(const uint8_t*, const EncBlock*, const uint32_t*, uint32_t, uint2*, SegSummary*,
-                            hipStream_t);
+hipError_t launch_enc_parse(const uint8_t*, const EncBlock*, const uint2*, uint32_t, const uint64_t*, const uint32_t*,
+                            uint32_t, uint32_t*, uint2*, SegSummary*, hipStream_t);
 hipError_t launch_enc_sizes(const EncBlock*, uint32_t, const SegSummary*, SegPlace*, uint32_t*, uint32_t*,
                             uint32_t*, hipStream_t);
 hipError_t launch_scan(const uint32_t*, uint32_t, uint64_t*, uint64_t*, hipStream_t);
@@ -121,8 +121,6 @@ struct TimedSpan {
 struct s3hc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;          // content xxh32 beside the match finder
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::mutex mu;
     bool timing = false;
     std::map<std::string, float> kernel_ms;
@@ -161,12 +159,13 @@ struct s3hc_plan {
     // ---- encode
     std::vector<EncBlock> blocks;
     std::vector<uint32_t> seg_block;
+    std::vector<uint2> groups;           // match-finding workgroups: (block, first segment)
     std::vector<uint32_t> frame_blk0, frame_nblk;
     std::vector<uint64_t> frame_src_off;
     std::vector<uint32_t> frame_src_len;
     std::vector<uint32_t> item_blk0, item_nblk;
     uint64_t dst_bound = 0;
-    DevBuf d_blocks, d_seg_block, d_frame_src_off, d_frame_src_len, d_item_blk0, d_item_nblk;
+    DevBuf d_groups, d_blocks, d_seg_block, d_frame_src_off, d_frame_src_len, d_item_blk0, d_item_nblk;
     DevBuf d_recs, d_summ, d_place, d_blk_payload, d_blk_size, d_blk_carry, d_blk_off, d_frame_hash, d_total;
     // ---- decode
     uint32_t nframes = 0;
@@ -190,9 +189,6 @@ s3hc_ctx::~s3hc_ctx() {
     for (auto& t : pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     for (auto e : event_pool) (void)hipEventDestroy(e);
     delete host_plan;
-    if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (ev_join) (void)hipEventDestroy(ev_join);
-    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -256,6 +252,13 @@ static int plan_upload_encode(s3hc_plan* P, hipStream_t st) {
     const size_t nseg = P->seg_block.size(), nb = P->blocks.size(), nf = P->frame_blk0.size();
     HIPCHK(upload(P->d_blocks, P->blocks, st));
     HIPCHK(upload(P->d_seg_block, P->seg_block, st));
+    P->groups.clear();
+    for (uint32_t b = 0; b < (uint32_t)P->blocks.size(); ++b) {
+        const EncBlock& B = P->blocks[b];
+        if (B.flags & (EB_STORE | EB_EMPTY)) continue;  // nothing to match
+        for (uint32_t k = 0; k < B.nseg; k += kGroupSegs) P->groups.push_back(make_uint2(b, k));
+    }
+    HIPCHK(upload(P->d_groups, P->groups, st));
     HIPCHK(upload(P->d_frame_src_off, P->frame_src_off, st));
     HIPCHK(upload(P->d_frame_src_len, P->frame_src_len, st));
     HIPCHK(upload(P->d_item_blk0, P->item_blk0, st));
@@ -277,20 +280,11 @@ static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t
     const uint32_t nseg = (uint32_t)P->seg_block.size(), nb = (uint32_t)P->blocks.size();
     const uint32_t nf = (uint32_t)P->frame_blk0.size(), ni = (uint32_t)P->item_blk0.size();
     KTimer T(ctx, st);
-    // content checksums run on the side stream, overlapping the match finder; emit joins
-    HIPCHK(hipEventRecord(ctx->ev_fork, st));
-    HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-    {
-        KTimer TS(ctx, ctx->side);
-        TS.begin("xxh32_side");  // overlaps enc_parse: its span is not exclusive time
-        HIPCHK(launch_xxh32(d_src, P->d_frame_src_off.as<uint64_t>(), P->d_frame_src_len.as<uint32_t>(), nf,
-                            P->d_frame_hash.as<uint32_t>(), ctx->side));
-        TS.end();
-    }
-    HIPCHK(hipEventRecord(ctx->ev_join, ctx->side));
+    // match finding; the grid's first workgroups compute the frames' content xxh32 meanwhile
     T.begin("enc_parse");
-    HIPCHK(launch_enc_parse(d_src, P->d_blocks.as<EncBlock>(), P->d_seg_block.as<uint32_t>(), nseg,
-                            P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), st));
+    HIPCHK(launch_enc_parse(d_src, P->d_blocks.as<EncBlock>(), P->d_groups.as<uint2>(), (uint32_t)P->groups.size(),
+                            P->d_frame_src_off.as<uint64_t>(), P->d_frame_src_len.as<uint32_t>(), nf,
+                            P->d_frame_hash.as<uint32_t>(), P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), st));
     T.end();
     T.begin("enc_sizes");
     HIPCHK(launch_enc_sizes(P->d_blocks.as<EncBlock>(), nb, P->d_summ.as<SegSummary>(), P->d_place.as<SegPlace>(),
@@ -298,7 +292,6 @@ static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t
                             P->d_blk_carry.as<uint32_t>(), st));
     HIPCHK(launch_scan(P->d_blk_size.as<uint32_t>(), nb, P->d_blk_off.as<uint64_t>(), P->d_total.as<uint64_t>(), st));
     T.end();
-    HIPCHK(hipStreamWaitEvent(st, ctx->ev_join, 0));
     T.begin("enc_emit");
     HIPCHK(launch_enc_emit(d_src, P->d_blocks.as<EncBlock>(), P->d_seg_block.as<uint32_t>(), nseg,
                            P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), P->d_place.as<SegPlace>(),
@@ -322,14 +315,6 @@ extern "C" int s3hc_create(s3hc_ctx** out, int device) {
     std::unique_ptr<s3hc_ctx> c(new s3hc_ctx);
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    {
-        // the side stream's few checksum waves are dispatched ahead of the match finder's
-        int least = 0, greatest = 0;
-        HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, greatest));
-    }
-    HIPCHK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
     *out = c.release();
     return S3HC_OK;
 }
@@ -937,5 +922,42 @@ extern "C" int s3hc_sync(s3hc_ctx* ctx) {
     if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    return S3HC_OK;
+}
+extern "C" int s3hc_host_alloc(s3hc_ctx* ctx, size_t n, void** out) {
+    if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipHostMalloc(out, n ? n : 16, hipHostMallocDefault));
+    return S3HC_OK;
+}
+extern "C" int s3hc_host_free(s3hc_ctx* ctx, void* p) {
+    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+    if (p) HIPCHK(hipHostFree(p));
+    return S3HC_OK;
+}
+extern "C" int s3hc_queue_create(s3hc_ctx* ctx, void** out) {
+    if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = (void*)s;
+    return S3HC_OK;
+}
+extern "C" int s3hc_queue_destroy(s3hc_ctx* ctx, void* q) {
+    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+    if (q) HIPCHK(hipStreamDestroy((hipStream_t)q));
+    return S3HC_OK;
+}
+extern "C" int s3hc_queue_sync(s3hc_ctx* ctx, void* q) {
+    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(q ? (hipStream_t)q : ctx->stream));
+    return S3HC_OK;
+}
+extern "C" int s3hc_memcpy_async(s3hc_ctx* ctx, void* dst, const void* src, size_t n, int kind, void* q) {
+    if (!ctx || kind < 1 || kind > 3) return fail(S3HC_INVALID_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    if (n) HIPCHK(hipMemcpyAsync(dst, src, n, k, q ? (hipStream_t)q : ctx->stream));
     return S3HC_OK;
 }

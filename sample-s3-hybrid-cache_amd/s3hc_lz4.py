@@ -39,6 +39,11 @@ def build(force: bool = False) -> str:
     return LIB_PATH
 
 
+def _q(stream):
+    """Queue, raw hipStream_t pointer value, or None (the context stream)."""
+    return getattr(stream, "q", stream)
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built (run __graft_entry__.build()); there is no CPU fallback")
@@ -91,6 +96,12 @@ def _load():
         "s3hc_memcpy": (i32, [vp, vp, vp, sz, i32]),
         "s3hc_memset": (i32, [vp, vp, i32, sz]),
         "s3hc_sync": (i32, [vp]),
+        "s3hc_host_alloc": (i32, [vp, sz, ctypes.POINTER(vp)]),
+        "s3hc_host_free": (i32, [vp, vp]),
+        "s3hc_queue_create": (i32, [vp, ctypes.POINTER(vp)]),
+        "s3hc_queue_destroy": (i32, [vp, vp]),
+        "s3hc_queue_sync": (i32, [vp, vp]),
+        "s3hc_memcpy_async": (i32, [vp, vp, vp, sz, i32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -211,6 +222,19 @@ class Engine:
         b.write(data)
         return b
 
+    # ---- pipelined host<->device batches
+    def host_alloc(self, nbytes: int) -> "HostBuffer":
+        return HostBuffer(self, nbytes)
+
+    def queue(self) -> "Queue":
+        return Queue(self)
+
+    def copy_async(self, dst, src, n: int, kind: int, queue: "Queue" = None, dst_off: int = 0, src_off: int = 0):
+        """kind 1 H2D, 2 D2H, 3 D2D; dst/src: DeviceBuffer or HostBuffer (data_ptr())."""
+        _check(lib.s3hc_memcpy_async(self.h, ctypes.c_void_p(dst.data_ptr() + dst_off),
+                                     ctypes.c_void_p(src.data_ptr() + src_off), n, kind,
+                                     queue.q if queue is not None else None))
+
     # ---- device-resident batches (DeviceBuffer or any object with data_ptr()/numel())
     def plan_encode(self, src_off, lengths, modes=None) -> "Plan":
         n = len(src_off)
@@ -223,7 +247,7 @@ class Engine:
 
     def encode_dev(self, plan: "Plan", d_src, d_dst, d_item_off, d_item_len, stream=None):
         _check(lib.s3hc_encode_dev(self.h, plan.h, d_src.data_ptr(), d_dst.data_ptr(), d_dst.numel(),
-                                   d_item_off.data_ptr(), d_item_len.data_ptr(), stream))
+                                   d_item_off.data_ptr(), d_item_len.data_ptr(), _q(stream)))
 
     def plan_decode(self, frame_off, frame_len, dst_off, dst_cap) -> "Plan":
         n = len(frame_off)
@@ -235,7 +259,57 @@ class Engine:
 
     def decode_dev(self, plan: "Plan", d_src, d_dst, d_out_len, d_status, stream=None):
         _check(lib.s3hc_decode_dev(self.h, plan.h, d_src.data_ptr(), d_dst.data_ptr(), d_out_len.data_ptr(),
-                                   d_status.data_ptr(), stream))
+                                   d_status.data_ptr(), _q(stream)))
+
+
+class HostBuffer:
+    """Pinned host memory (hipHostMalloc) for overlapped copies; numpy view via .view()."""
+
+    def __init__(self, eng: Engine, nbytes: int):
+        self.eng, self.nbytes = eng, int(nbytes)
+        p = ctypes.c_void_p()
+        _check(lib.s3hc_host_alloc(eng.h, self.nbytes, ctypes.byref(p)))
+        self.ptr = p
+
+    def data_ptr(self) -> int:
+        return self.ptr.value
+
+    def numel(self) -> int:
+        return self.nbytes
+
+    def view(self):
+        import numpy as np
+        return np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr.value))
+
+    def free(self):
+        if self.ptr:
+            lib.s3hc_host_free(self.eng.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            if self.ptr and self.eng.h:
+                self.free()
+        except Exception:
+            pass
+
+
+class Queue:
+    """A HIP stream of the engine's device (the `stream` argument of encode_dev/decode_dev)."""
+
+    def __init__(self, eng: Engine):
+        self.eng = eng
+        q = ctypes.c_void_p()
+        _check(lib.s3hc_queue_create(eng.h, ctypes.byref(q)))
+        self.q = q
+
+    def sync(self):
+        _check(lib.s3hc_queue_sync(self.eng.h, self.q))
+
+    def close(self):
+        if self.q:
+            lib.s3hc_queue_destroy(self.eng.h, self.q)
+            self.q = None
 
 
 class DeviceBuffer:

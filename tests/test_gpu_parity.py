@@ -309,6 +309,61 @@ def test_batch_decode_reports_corruption(engine, oracle):
     assert want[3] == 2 and want[5] != 0
 
 
+def test_pipelined_queues_pinned_host(engine, oracle):
+    """Chunks of a batch rotate over 3 queues with pinned host buffers (the end-to-end path):
+    H2D, encode, D2H of the frame table and frames; then H2D, decode, D2H. Same bytes as the
+    synchronous path, every frame decodes with the oracle."""
+    block, n, chunk, nq = 65536, 48, 8, 3
+    data = synth.log_text(n * block, 91)
+    h_in = engine.host_alloc(len(data))
+    h_in.view()[:] = np.frombuffer(data, dtype=np.uint8)
+    h_out = engine.host_alloc(len(data))
+    qs = [engine.queue() for _ in range(nq)]
+    nch = n // chunk
+    lanes = []
+    for _ in range(nq):
+        plan = engine.plan_encode([i * block for i in range(chunk)], [block] * chunk)
+        lanes.append(dict(plan=plan, src=engine.alloc(chunk * block), dst=engine.alloc(plan.dst_bound),
+                          ioff=engine.alloc(8 * chunk), ilen=engine.alloc(4 * chunk),
+                          meta=engine.host_alloc(12 * chunk), out=engine.alloc(chunk * block),
+                          olen=engine.alloc(4 * chunk), ost=engine.alloc(4 * chunk)))
+    frames = []
+    for c in range(nch):
+        L, q = lanes[c % nq], qs[c % nq]
+        engine.copy_async(L["src"], h_in, chunk * block, 1, q, src_off=c * chunk * block)
+        engine.encode_dev(L["plan"], L["src"], L["dst"], L["ioff"], L["ilen"], q)
+        engine.copy_async(L["meta"], L["ioff"], 8 * chunk, 2, q)
+        engine.copy_async(L["meta"], L["ilen"], 4 * chunk, 2, q, dst_off=8 * chunk)
+        q.sync()
+        mv = L["meta"].view()
+        fo = mv[:8 * chunk].view(np.uint64).tolist()
+        fl = mv[8 * chunk:12 * chunk].view(np.uint32).tolist()
+        blob = L["dst"].read(fo[-1] + fl[-1])
+        for i in range(chunk):
+            f = blob[fo[i]:fo[i] + fl[i]]
+            assert oracle.decompress_data(f) == data[(c * chunk + i) * block:(c * chunk + i + 1) * block]
+        frames.append((blob, fo, fl))
+    h_fr = engine.host_alloc(sum(len(b) for b, _, _ in frames))
+    hv, pos, dplans, cins = h_fr.view(), 0, [], []
+    for blob, fo, fl in frames:
+        hv[pos:pos + len(blob)] = np.frombuffer(blob, dtype=np.uint8)
+        dplans.append((engine.plan_decode(fo, fl, [i * block for i in range(chunk)], [block] * chunk), pos, len(blob)))
+        pos += len(blob)
+    for L in lanes:
+        cins.append(engine.alloc(chunk * (block + 64)))
+    for c in range(nch):
+        L, q, cin = lanes[c % nq], qs[c % nq], cins[c % nq]
+        dp, hoff, clen = dplans[c]
+        engine.copy_async(cin, h_fr, clen, 1, q, src_off=hoff)
+        engine.decode_dev(dp, cin, L["out"], L["olen"], L["ost"], q)
+        engine.copy_async(h_out, L["out"], chunk * block, 2, q, dst_off=c * chunk * block)
+    for q in qs:
+        q.sync()
+    assert bytes(h_out.view()) == data
+    for q in qs:
+        q.close()
+
+
 # ---- CompressionHandler mirror: ports of src/compression.rs unit tests (:607-992)
 def _handler(engine, threshold=10, enabled=True):
     import s3hc_lz4 as S
