@@ -228,7 +228,7 @@ constexpr uint32_t kMask = kRing - 1;
 constexpr uint32_t kFlush = 1024;  // ring -> HBM flush granule
 constexpr uint32_t kWin = 1024;    // output bytes executed per window (byte-parallel)
 constexpr uint32_t kSink = 192;    // per-lane store sink: 64 B for ring bytes, 128 B for refs
-constexpr uint32_t kWaveLds = kRing + kCring + (kWin + 64) + 2 * kWin + kSink;
+constexpr uint32_t kWaveLds = kRing + kCring + (kWin + 64) + 2 * kWin + kSink + 128 * 8;
 constexpr int kWaves = 4;
 enum : uint32_t { F_ERR = 1, F_LAST = 2, F_LONG = 4, F_MORE = 8 };
 }  // namespace dec
@@ -239,6 +239,7 @@ struct DecWave {
     uint8_t* marks;      // kWin + 64 bytes: sequence start marks of the current window
     uint16_t* refs;      // kWin entries: in-window match source of each output byte
     uint8_t* sink;       // kSink bytes: target of stores from lanes with nothing to store
+    uint2* mtab;         // 128 entries: the window's member sequences (start, ll, off, literal)
     uint8_t* out;        // unit output base in HBM
 #ifdef S3HC_PROF
     uint64_t pr[16];
@@ -368,18 +369,22 @@ __device__ __forceinline__ int dec_seq(DecWave& w, const uint8_t* in, uint32_t l
 // source lies inside the window then follow the chain of in-window sources (refs) to a byte
 // written in the first pass. A fixed handful of LDS round trips per window instead of two per
 // sequence, and almost no scalar work.
-__device__ __forceinline__ void dec_window_exec(DecWave& w, bool isM, uint32_t S, uint32_t orel, uint32_t sl,
-                                                uint32_t lit, uint32_t ll, uint32_t off, uint32_t mis) {
+__device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM0, bool isM1, uint32_t orel0,
+                                                uint32_t orel1, uint32_t sl0, uint32_t sl1, uint32_t ll0,
+                                                uint32_t ll1, uint32_t pkB0, uint32_t pkB1) {
     using namespace dec;
     const int lane = w.lane;
     uint8_t* marks = w.marks;
     uint16_t* refs = w.refs;
     *(uint4*)(marks + 16 * lane) = make_uint4(0, 0, 0, 0);  // clears [0, kWin)
     wave_sync();
-    if (isM && sl) marks[orel] = (uint8_t)(lane + 1);
+    // member m (token position q + m, m < 128) starts at output byte orel: marks hold m + 1;
+    // the member table holds (orel | ll << 16, off | literal ring index << 16)
+    *((isM0 && sl0) ? marks + orel0 : w.sink + lane) = (uint8_t)(lane + 1);
+    *((isM1 && sl1) ? marks + orel1 : w.sink + lane) = (uint8_t)(lane + 65);
+    w.mtab[lane] = make_uint2(orel0 | (ll0 << 16), pkB0);
+    w.mtab[64 + lane] = make_uint2(orel1 | (ll1 << 16), pkB1);
     wave_sync();
-    const uint32_t pkA = orel | (ll << 16);
-    const uint32_t pkB = off | (((lit + mis) & kCmask) << 16);
     const uint32_t upos = w.upos;
     // Passes of 256 bytes: byte t = b + 64k + lane, k = 0..3, with every LDS read of the pass
     // issued before its writes (four independent chunks per round trip).
@@ -404,8 +409,9 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, bool isM, uint32_t S
         uint32_t A[4], B[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            A[k] = __shfl(pkA, (int)mk[k] - 1);
-            B[k] = __shfl(pkB, (int)mk[k] - 1);
+            const uint2 f = w.mtab[(mk[k] - 1) & 127u];
+            A[k] = f.x;
+            B[k] = f.y;
         }
         uint32_t y[4], val[4];
         bool lit_[4], pnd[4], wrap[4];
@@ -506,6 +512,43 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, bool isM, uint32_t S
     PROF_ADD(w.pr, 10, PROF_NOW() - tf);
 }
 
+// Speculative LZ4 token parse at block position qq (the window assumes a token there): two
+// LDS round trips (token + up to two length bytes; offset + up to two match-length bytes),
+// no branches. Flags: F_ERR malformed, F_LAST last sequence, F_LONG a length run beyond two
+// bytes, F_MORE bytes past the staged input (both go to the slow path).
+struct DecTok {
+    uint32_t flags, nxt, lit, ll, off, ml;
+};
+__device__ __forceinline__ DecTok dec_spec(const uint8_t* cin, uint32_t qq, uint32_t mis, uint32_t C, uint32_t fill) {
+    using namespace dec;
+    DecTok T;
+    const uint32_t i = qq + mis;
+    const uint32_t w0 = cin32(cin, i);
+    const uint32_t t = w0 & 0xFFu, L = t >> 4, M = t & 15u;
+    const uint32_t e1 = (w0 >> 8) & 0xFFu, e2 = (w0 >> 16) & 0xFFu;
+    const uint32_t x1 = L == 15u ? 1u : 0u, x2 = (L == 15u && e1 == 255u) ? 1u : 0u;
+    T.ll = L + (x1 ? e1 : 0u) + (x2 ? e2 : 0u);
+    T.lit = qq + 1u + x1 + x2;
+    const uint32_t mp = T.lit + T.ll;
+    const uint32_t mi = mp + mis;
+    const uint32_t w1 = cin32(cin, mi);
+    T.off = w1 & 0xFFFFu;
+    const uint32_t f1 = (w1 >> 16) & 0xFFu, f2 = w1 >> 24;
+    const uint32_t y1 = M == 15u ? 1u : 0u, y2 = (M == 15u && f1 == 255u) ? 1u : 0u;
+    T.ml = M + 4u + (y1 ? f1 : 0u) + (y2 ? f2 : 0u);
+    T.nxt = mp + 2u + y1 + y2;
+    // precedence (lowest first): long match run, ext byte past the end, offset past the
+    // staged input, offset cut off, last sequence, bad literal run
+    uint32_t fm = (y2 && f2 == 255u) ? F_LONG : 0u;
+    fm = (T.nxt > C) ? F_ERR : fm;
+    fm = (mi + 4 > fill) ? F_MORE : fm;
+    fm = (C - mp < 2) ? F_ERR : fm;
+    fm = (mp == C) ? (mi > fill ? F_MORE : F_LAST) : fm;
+    fm = (qq >= C || T.lit > C || T.ll > C - T.lit) ? F_ERR : fm;
+    T.flags = fm | ((x2 && e2 == 255u) ? F_LONG : 0u);
+    return T;
+}
+
 // Decode one compressed block of C bytes. hist = bytes of earlier unit output matches may use.
 // Output overflowing `limit` is corruption (lz4_flex: output sink bounded by the block size);
 // overflowing only `cap` is DST_TOO_SMALL.
@@ -550,96 +593,99 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
             wave_sync();
         }
         const uint64_t tp0 = PROF_NOW();
-        // ---- speculative parse: lane assumes a token at qq = q + lane. Two LDS round trips
-        // (token + up to two length bytes; offset + up to two match-length bytes), no branches.
-        const uint32_t qq = q + lane;
-        const uint32_t i = qq + mis;
-        uint32_t flags, nxt, lit, ll, off, ml;
-        {
-            const uint32_t w0 = cin32(w.cin, i);
-            const uint32_t t = w0 & 0xFFu, L = t >> 4, M = t & 15u;
-            const uint32_t e1 = (w0 >> 8) & 0xFFu, e2 = (w0 >> 16) & 0xFFu;
-            const uint32_t x1 = L == 15u ? 1u : 0u, x2 = (L == 15u && e1 == 255u) ? 1u : 0u;
-            ll = L + (x1 ? e1 : 0u) + (x2 ? e2 : 0u);
-            lit = qq + 1u + x1 + x2;
-            const uint32_t mp = lit + ll;
-            const uint32_t mi = mp + mis;
-            const uint32_t w1 = cin32(w.cin, mi);
-            off = w1 & 0xFFFFu;
-            const uint32_t f1 = (w1 >> 16) & 0xFFu, f2 = w1 >> 24;
-            const uint32_t y1 = M == 15u ? 1u : 0u, y2 = (M == 15u && f1 == 255u) ? 1u : 0u;
-            ml = M + 4u + (y1 ? f1 : 0u) + (y2 ? f2 : 0u);
-            nxt = mp + 2u + y1 + y2;
-            // precedence (lowest first): long match run, ext byte past the end, offset past the
-            // stage, offset cut off, last sequence, bad literal run
-            uint32_t fm = (y2 && f2 == 255u) ? F_LONG : 0u;
-            fm = (nxt > C) ? F_ERR : fm;
-            fm = (mi + 4 > fill) ? F_MORE : fm;
-            fm = (C - mp < 2) ? F_ERR : fm;
-            fm = (mp == C) ? (mi > fill ? F_MORE : F_LAST) : fm;
-            fm = (qq >= C || lit > C || ll > C - lit) ? F_ERR : fm;
-            flags = fm | ((x2 && e2 == 255u) ? F_LONG : 0u);
-        }
-        // ---- walk the true token chain through the window (scalar, one readlane per hop)
-        const bool term = (flags & (F_ERR | F_LONG | F_MORE | F_LAST)) != 0;
-        const uint32_t nx = term ? 64u : (nxt - q < 64u ? nxt - q : 64u);
-        uint64_t members = 0;
-        uint32_t l = 0, lastl;
-        do {
+        // ---- speculative parse at the window's 128 token positions: lane holds q + lane (set 0)
+        // and q + 64 + lane (set 1)
+        const DecTok t0 = dec_spec(w.cin, q + lane, mis, C, fill);
+        const DecTok t1 = dec_spec(w.cin, q + 64 + lane, mis, C, fill);
+        // ---- walk the true token chain (scalar, one readlane per hop); nx = next position - q,
+        // 128 for a position that ends the chain (error, long run, past the ring, last)
+        auto nxof = [&](const DecTok& T) -> uint32_t {
+            const bool term = (T.flags & (F_ERR | F_LONG | F_MORE | F_LAST)) != 0;
+            return term ? 128u : (T.nxt - q < 128u ? T.nxt - q : 128u);
+        };
+        const uint32_t nx0 = nxof(t0), nx1 = nxof(t1);
+        uint64_t m0 = 0, m1 = 0;
+        uint32_t l = 0, lastl = 0;
+        while (l < 64u) {
             lastl = l;
-            members |= 1ull << l;
-            l = rdl(nx, l);
-        } while (l < 64u);
+            m0 |= 1ull << l;
+            l = rdl(nx0, l);
+        }
+        while (l < 128u) {
+            lastl = l;
+            m1 |= 1ull << (l - 64);
+            l = rdl(nx1, l - 64);
+        }
+        auto rd2 = [&](uint32_t v0, uint32_t v1, uint32_t m) -> uint32_t { return m < 64 ? rdl(v0, m) : rdl(v1, m - 64); };
         int stop = 0;  // 0 window exhausted, 1 last sequence, 2 error, 3 slow path at cur, 4 long sequence
         uint32_t cur;
         {
-            const uint32_t fl = rdl(flags, lastl);
+            const uint32_t fl = rd2(t0.flags, t1.flags, lastl);
             if (fl & (F_LONG | F_MORE | F_ERR)) {
-                members &= ~(1ull << lastl);
+                if (lastl < 64) m0 &= ~(1ull << lastl);
+                else m1 &= ~(1ull << (lastl - 64));
                 stop = (fl & (F_LONG | F_MORE)) ? 3 : 2;
                 cur = q + lastl;
             } else if (fl & F_LAST) {
                 stop = 1;
                 cur = C;
             } else {
-                cur = rdl(nxt, lastl);
+                cur = rd2(t0.nxt, t1.nxt, lastl);
             }
         }
         const uint64_t tp1 = PROF_NOW();
         PROF_ADD(w.pr, 1, tp1 - tp0);
-        if (members) {
-            bool isM = (members >> lane) & 1ull;
-            const uint32_t sl = isM ? ll + ((flags & F_LAST) ? 0u : ml) : 0u;
-            const uint32_t orel = wave_excl_scan(sl, lane);
-            uint32_t S = rdl(orel + sl, 63);
+        if (m0 | m1) {
+            bool isM0 = (m0 >> lane) & 1ull, isM1 = (m1 >> lane) & 1ull;
+            const uint32_t sl0 = isM0 ? t0.ll + ((t0.flags & F_LAST) ? 0u : t0.ml) : 0u;
+            const uint32_t sl1 = isM1 ? t1.ll + ((t1.flags & F_LAST) ? 0u : t1.ml) : 0u;
+            const uint32_t orel0 = wave_excl_scan(sl0, lane);
+            const uint32_t tot0 = rdl(orel0 + sl0, 63);
+            const uint32_t orel1 = tot0 + wave_excl_scan(sl1, lane);
+            uint32_t S = rdl(orel1 + sl1, 63);
             // output budget: the members that fit in kWin run now, the rest next window
-            const uint64_t cut = __ballot(isM && orel + sl > kWin);
-            if (cut) {
-                const uint32_t c = (uint32_t)__builtin_ctzll(cut);
-                members &= (1ull << c) - 1ull;
-                isM = isM && (uint32_t)lane < c;
-                S = rdl(orel, c);
-                stop = members ? 0 : 4;
+            const uint64_t cut0 = __ballot(isM0 && orel0 + sl0 > kWin);
+            const uint64_t cut1 = __ballot(isM1 && orel1 + sl1 > kWin);
+            if (cut0 | cut1) {
+                const uint32_t c = cut0 ? (uint32_t)__builtin_ctzll(cut0) : 64u + (uint32_t)__builtin_ctzll(cut1);
+                if (c < 64) {
+                    m0 &= (1ull << c) - 1ull;
+                    m1 = 0;
+                } else {
+                    m1 &= (1ull << (c - 64)) - 1ull;
+                }
+                isM0 = (m0 >> lane) & 1ull;
+                isM1 = (m1 >> lane) & 1ull;
+                S = rd2(orel0, orel1, c);
+                stop = (m0 | m1) ? 0 : 4;
                 cur = q + c;
             }
-            if (members) {
+            if (m0 | m1) {
                 // lz4_flex bound checks, lane-parallel; the first failing member decides
-                const uint32_t produced = w.upos - bstart + orel;
-                const bool lastm = (flags & F_LAST) != 0;
-                const uint32_t have = produced + ll;
-                int st = S3HC_OK;
-                st = (!lastm && ml > cap - have) ? S3HC_DST_TOO_SMALL : st;
-                st = (!lastm && ml > limit - have) ? S3HC_CORRUPT : st;
-                st = (!lastm && (off == 0 || off > have + hist)) ? S3HC_CORRUPT : st;
-                st = (ll > cap - produced) ? S3HC_DST_TOO_SMALL : st;
-                st = (ll > limit - produced) ? S3HC_CORRUPT : st;
-                const uint64_t bad = __ballot(isM && st != S3HC_OK);
-                if (bad) return (int)rdl((uint32_t)st, (uint32_t)__builtin_ctzll(bad));
-                dec_window_exec(w, isM, S, orel, sl, lit, ll, off, mis);
+                const uint32_t base = w.upos - bstart;
+                auto check = [&](const DecTok& T, uint32_t orel) -> int {
+                    const uint32_t produced = base + orel;
+                    const bool lastm = (T.flags & F_LAST) != 0;
+                    const uint32_t have = produced + T.ll;
+                    int st = S3HC_OK;
+                    st = (!lastm && T.ml > cap - have) ? S3HC_DST_TOO_SMALL : st;
+                    st = (!lastm && T.ml > limit - have) ? S3HC_CORRUPT : st;
+                    st = (!lastm && (T.off == 0 || T.off > have + hist)) ? S3HC_CORRUPT : st;
+                    st = (T.ll > cap - produced) ? S3HC_DST_TOO_SMALL : st;
+                    st = (T.ll > limit - produced) ? S3HC_CORRUPT : st;
+                    return st;
+                };
+                const int st0 = check(t0, orel0), st1 = check(t1, orel1);
+                const uint64_t bad0 = __ballot(isM0 && st0 != S3HC_OK);
+                const uint64_t bad1 = __ballot(isM1 && st1 != S3HC_OK);
+                if (bad0) return (int)rdl((uint32_t)st0, (uint32_t)__builtin_ctzll(bad0));
+                if (bad1) return (int)rdl((uint32_t)st1, (uint32_t)__builtin_ctzll(bad1));
+                dec_window_exec(w, S, isM0, isM1, orel0, orel1, sl0, sl1, t0.ll, t1.ll,
+                                t0.off | (((t0.lit + mis) & kCmask) << 16), t1.off | (((t1.lit + mis) & kCmask) << 16));
                 PROF_ADD(w.pr, 2, PROF_NOW() - tp1);
                 PROF_ADD(w.pr, 5, 1);
-                PROF_ADD(w.pr, 6, __builtin_popcountll(members));
-                PROF_ADD(w.pr, 7, (S + 63) / 64);
+                PROF_ADD(w.pr, 6, __builtin_popcountll(m0) + __builtin_popcountll(m1));
+                PROF_ADD(w.pr, 7, (S + 255) / 256);
                 PROF_ADD(w.pr, 11, S);
             }
         }
@@ -648,12 +694,12 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
         if (stop == 2) return S3HC_CORRUPT;
         if (stop == 4) {
             const uint32_t c = cur - q;
-            const uint32_t f = rdl(flags, c);
-            const int rc = dec_seq(w, in, rdl(lit, c), rdl(ll, c), (f & F_LAST) != 0, rdl(off, c), rdl(ml, c),
-                                   mis, fill, bstart, limit, cap, hist);
+            const uint32_t f = rd2(t0.flags, t1.flags, c);
+            const int rc = dec_seq(w, in, rd2(t0.lit, t1.lit, c), rd2(t0.ll, t1.ll, c), (f & F_LAST) != 0,
+                                   rd2(t0.off, t1.off, c), rd2(t0.ml, t1.ml, c), mis, fill, bstart, limit, cap, hist);
             if (rc) return rc;
             if (f & F_LAST) return S3HC_OK;
-            cur = rdl(nxt, c);
+            cur = rd2(t0.nxt, t1.nxt, c);
         }
         if (stop == 3) {
             // Slow path: this sequence has long length runs or reaches past the stage.
@@ -701,6 +747,7 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     w.marks = w.cin + dec::kCring;
     w.refs = (uint16_t*)(w.marks + dec::kWin + 64);
     w.sink = (uint8_t*)(w.refs + dec::kWin);
+    w.mtab = (uint2*)(w.sink + dec::kSink);
     w.out = dst + blk[U.first].dst_off;
     w.upos = 0;
     w.flushed = 0;

@@ -11,4 +11,7 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
 tail -1 gpurun_out/bench_2rank.json | cut -c1-300
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o rstats -- python bench.py --no-cpu-baseline --steps 10 --warmup 2 > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err || { tail -5 gpurun_out/prof_bench.err; exit 1; }
+
+timeout -k 10 600 python tools_e2e.py > gpurun_out/e2e.json 2> gpurun_out/e2e.err || { tail -5 gpurun_out/e2e.err; exit 1; }
+echo e2e-ok
 echo round-ok
