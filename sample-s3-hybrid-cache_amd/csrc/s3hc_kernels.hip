@@ -226,9 +226,10 @@ constexpr uint32_t kAhead = 512;   // input kept staged ahead of the parse posit
 constexpr uint32_t kRing = 4096;   // recent output kept in LDS per wave (match sources)
 constexpr uint32_t kMask = kRing - 1;
 constexpr uint32_t kFlush = 1024;  // ring -> HBM flush granule
-constexpr uint32_t kWin = 1024;    // output bytes executed per window (byte-parallel)
-constexpr uint32_t kSink = 192;    // per-lane store sink: 64 B for ring bytes, 128 B for refs
-constexpr uint32_t kWaveLds = kRing + kCring + (kWin + 64) + 2 * kWin + kSink + 128 * 8;
+constexpr uint32_t kWin = 768;     // output bytes executed per window (byte-parallel)
+constexpr uint32_t kMarks = 1024;  // marks/refs entries: >= kWin + 3 rounded up to the 256-byte pass
+constexpr uint32_t kSink = 64;     // per-lane store sink for lanes with nothing to store
+constexpr uint32_t kWaveLds = kRing + kCring + kMarks + 2 * kMarks + kSink + 128 * 8;
 constexpr int kWaves = 4;
 enum : uint32_t { F_ERR = 1, F_LAST = 2, F_LONG = 4, F_MORE = 8 };
 }  // namespace dec
@@ -236,8 +237,8 @@ enum : uint32_t { F_ERR = 1, F_LAST = 2, F_LONG = 4, F_MORE = 8 };
 struct DecWave {
     uint8_t* ring;
     uint8_t* cin;        // kCring bytes: compressed input, byte p of the block at (p + mis) & kCmask
-    uint8_t* marks;      // kWin + 64 bytes: sequence start marks of the current window
-    uint16_t* refs;      // kWin entries: in-window match source of each output byte
+    uint8_t* marks;      // kMarks bytes: sequence start marks of the current window
+    uint16_t* refs;      // kMarks entries: in-pass match source of each output byte
     uint8_t* sink;       // kSink bytes: target of stores from lanes with nothing to store
     uint2* mtab;         // 128 entries: the window's member sequences (start, ll, off, literal)
     uint8_t* out;        // unit output base in HBM
@@ -363,12 +364,13 @@ __device__ __forceinline__ int dec_seq(DecWave& w, const uint8_t* in, uint32_t l
     return S3HC_OK;
 }
 
-// Byte-parallel execution of one window's sequences (lanes in `members`; S output bytes,
-// S <= kWin). Every output byte t finds its sequence (start marks + max-scan), literal bytes
-// and match bytes whose source precedes the window are written at once, and match bytes whose
-// source lies inside the window then follow the chain of in-window sources (refs) to a byte
-// written in the first pass. A fixed handful of LDS round trips per window instead of two per
-// sequence, and almost no scalar work.
+// Byte-parallel execution of one window's sequences (members: lanes of set 0/1; S output
+// bytes, S <= kWin). Passes of 256 output bytes, 4 consecutive bytes per lane (one aligned
+// ring dword): each byte finds its sequence (start marks + DPP max-scan; a lane's 4 bytes
+// touch at most 2 sequences), literal bytes and match bytes whose source precedes this pass
+// are read at once, the dword is merged and stored, and bytes whose source lies in this pass
+// follow the chain of in-pass sources (refs) to a byte already final. A fixed handful of LDS
+// round trips per 256 bytes, almost no scalar work.
 __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM0, bool isM1, uint32_t orel0,
                                                 uint32_t orel1, uint32_t sl0, uint32_t sl1, uint32_t ll0,
                                                 uint32_t ll1, uint32_t pkB0, uint32_t pkB1) {
@@ -376,136 +378,127 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
     const int lane = w.lane;
     uint8_t* marks = w.marks;
     uint16_t* refs = w.refs;
-    *(uint4*)(marks + 16 * lane) = make_uint4(0, 0, 0, 0);  // clears [0, kWin)
+    const uint32_t upos = w.upos;
+    const uint32_t a0 = upos & 3u;        // byte u of a pass = window byte u - a0 (ring dwords aligned)
+    const uint32_t xbase = upos - a0;
+    const uint32_t np = (S + a0 + 255u) >> 8;
+    ((uint4*)marks)[lane] = make_uint4(0, 0, 0, 0);  // clears [0, kMarks)
     wave_sync();
-    // member m (token position q + m, m < 128) starts at output byte orel: marks hold m + 1;
-    // the member table holds (orel | ll << 16, off | literal ring index << 16)
-    *((isM0 && sl0) ? marks + orel0 : w.sink + lane) = (uint8_t)(lane + 1);
-    *((isM1 && sl1) ? marks + orel1 : w.sink + lane) = (uint8_t)(lane + 65);
+    // member m (token position q + m) starts at window byte orel: marks[orel + a0] = m + 1; the
+    // member table holds (orel | ll << 16, off | literal ring index << 16)
+    *((isM0 && sl0) ? marks + orel0 + a0 : w.sink + lane) = (uint8_t)(lane + 1);
+    *((isM1 && sl1) ? marks + orel1 + a0 : w.sink + lane) = (uint8_t)(lane + 65);
     w.mtab[lane] = make_uint2(orel0 | (ll0 << 16), pkB0);
     w.mtab[64 + lane] = make_uint2(orel1 | (ll1 << 16), pkB1);
     wave_sync();
-    const uint32_t upos = w.upos;
-    // Passes of 256 bytes: byte t = b + 64k + lane, k = 0..3, with every LDS read of the pass
-    // issued before its writes (four independent chunks per round trip).
     uint32_t carry = 0;
-    for (uint32_t b = 0; b < S; b += 256) {
-        uint32_t mk[4], t[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            t[k] = b + 64u * k + lane;
-            mk[k] = (uint32_t)marks[t[k]];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) mk[k] = wave_incl_max(mk[k]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            // lanes t >= S only compute (their reads stay inside this wave's LDS) and never
-            // write; they sit above every valid byte, so they do not disturb the scan
-            const uint32_t top = rdl(mk[k], 63);
-            mk[k] = mk[k] > carry ? mk[k] : carry;
-            carry = top > carry ? top : carry;
-        }
-        uint32_t A[4], B[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint2 f = w.mtab[(mk[k] - 1) & 127u];
-            A[k] = f.x;
-            B[k] = f.y;
-        }
-        uint32_t y[4], val[4];
-        bool lit_[4], pnd[4], wrap[4];
+    for (uint32_t p = 0; p < np; ++p) {
+        const uint32_t u0 = 256u * p + 4u * (uint32_t)lane;  // marks/refs index of this lane's byte 0
+        const uint32_t t0 = u0 - a0;                         // window byte of byte 0 (may wrap below 0)
+        const uint32_t X = xbase + u0;                        // output position of byte 0 (4-aligned)
+        const uint32_t brc = p ? 256u * p - a0 : 0u;          // first window byte of this pass
+        // ---- owners
+        const uint32_t md = ((const uint32_t*)marks)[64u * p + (uint32_t)lane];
+        const uint32_t b0 = md & 0xFFu, b1 = (md >> 8) & 0xFFu, b2 = (md >> 16) & 0xFFu, b3 = md >> 24;
+        const uint32_t c1 = umax32(b0, b1), c2 = umax32(c1, b2), c3 = umax32(c2, b3);
+        const uint32_t inc = wave_incl_max(c3);
+        const uint32_t ex = umax32(dpp0<0x138, 0xF>(inc), carry);  // wave_shr:1 -> exclusive
+        carry = umax32(carry, rdl(inc, 63));
+        uint32_t o[4];
+        o[0] = umax32(ex, b0);
+        o[1] = umax32(ex, c1);
+        o[2] = umax32(ex, c2);
+        o[3] = umax32(ex, c3);
+        const uint2 fA = w.mtab[(o[0] - 1u) & 127u], fB = w.mtab[(o[3] - 1u) & 127u];
+        // ---- sources
+        uint32_t y[4], dd[4], mlit[4], ee[4], mf[4];
+        bool lit[4], ok[4], wrap[4];
         bool anywrap = false;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t mo = A[k] & 0xFFFFu, mll = A[k] >> 16, moff = B[k] & 0xFFFFu;
-            const uint32_t dd = t[k] - mo;
-            lit_[k] = dd < mll;
-            const uint32_t e = dd - mll;  // position inside the match
-            wrap[k] = !lit_[k] && e >= moff && t[k] < S;
-            anywrap |= wrap[k];
-            y[k] = upos + t[k] - moff;    // non-overlapping source
+        for (int j = 0; j < 4; ++j) {
+            const bool useB = o[j] == o[3];
+            const uint32_t fx = useB ? fB.x : fA.x, fy = useB ? fB.y : fA.y;
+            const uint32_t mo = fx & 0xFFFFu, mll = fx >> 16, moff = fy & 0xFFFFu;
+            mlit[j] = fy >> 16;
+            ok[j] = t0 + j < S;
+            dd[j] = t0 + j - mo;
+            lit[j] = dd[j] < mll;
+            ee[j] = dd[j] - mll;              // position inside the match
+            mf[j] = moff;
+            wrap[j] = ok[j] & !lit[j] & (ee[j] >= moff);
+            anywrap |= wrap[j];
+            y[j] = X + j - moff;              // non-overlapping source
         }
-        if (__ballot(anywrap)) {          // overlapping matches: period moff
+        if (__ballot(anywrap)) {              // overlapping matches: period moff
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (wrap[k]) {
-                    const uint32_t mo = A[k] & 0xFFFFu, mll = A[k] >> 16, moff = B[k] & 0xFFFFu;
-                    const uint32_t e = t[k] - mo - mll;
-                    y[k] = upos + mo + mll - moff + e % moff;
-                }
-            }
+            for (int j = 0; j < 4; ++j)
+                if (wrap[j]) y[j] = X + j - ee[j] - mf[j] + ee[j] % mf[j];
         }
-        uint8_t lv[4], rv[4];
+        const uint32_t oldw = ((const uint32_t*)w.ring)[(X & kMask) >> 2];
+        uint32_t v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t mo = A[k] & 0xFFFFu, mlit = B[k] >> 16;
-            lv[k] = w.cin[(mlit + t[k] - mo) & kCmask];
-            rv[k] = w.ring[y[k] & kMask];
+        for (int j = 0; j < 4; ++j) {
+            const uint8_t* a = lit[j] ? w.cin + ((mlit[j] + dd[j]) & kCmask) : w.ring + (y[j] & kMask);
+            v[j] = *a;
         }
+        bool pnd[4];
         bool anypnd = false;
+        uint32_t vm = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            val[k] = lit_[k] ? lv[k] : rv[k];
-            // literal bytes get ry = ~0 (never pending); (ry - b) < (S - b) <=> b <= ry < S
-            const uint32_t ry = lit_[k] ? 0xFFFFFFFFu : y[k] - upos;
-            pnd[k] = (t[k] < S) & (ry - b < S - b);  // earlier passes are final in the ring
-            anypnd |= pnd[k];
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t ry = y[j] - upos;  // window byte of the source (< S: inside the window)
+            pnd[j] = ok[j] & !lit[j] & (ry - brc < S - brc);  // earlier passes are final in the ring
+            anypnd |= pnd[j];
+            vm |= ok[j] ? 0xFFu << (8 * j) : 0u;
         }
-        // every lane stores; bytes past the window go to a per-lane sink (no exec masking)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const bool ok = t[k] < S;
-            uint8_t* rp = ok ? w.ring + ((upos + t[k]) & kMask) : w.sink + lane;
-            uint16_t* fp = ok ? refs + t[k] : (uint16_t*)(w.sink + 64) + lane;
-            *rp = (uint8_t)val[k];
-            *fp = (uint16_t)(pnd[k] ? y[k] - upos : 0xFFFFu);
-        }
+        const uint32_t val = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+        ((uint32_t*)w.ring)[(X & kMask) >> 2] = (val & vm) | (oldw & ~vm);
+        const uint32_t r0 = pnd[0] ? y[0] - upos : 0xFFFFu, r1 = pnd[1] ? y[1] - upos : 0xFFFFu;
+        const uint32_t r2 = pnd[2] ? y[2] - upos : 0xFFFFu, r3 = pnd[3] ? y[3] - upos : 0xFFFFu;
+        *(uint2*)(refs + u0) = make_uint2(r0 | (r1 << 16), r2 | (r3 << 16));
         if (upos > kRing - S) {
             // sources older than the ring are read back from HBM (already flushed); kept apart
             // so the common path never waits on the wave's outstanding flush stores
             bool old[4], anyold = false;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                old[k] = (t[k] < S) & !lit_[k] & (y[k] < upos - (kRing - S));
-                anyold |= old[k];
+            for (int j = 0; j < 4; ++j) {
+                old[j] = ok[j] & !lit[j] & (y[j] < upos - (kRing - S));
+                anyold |= old[j];
             }
             if (__ballot(anyold)) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (old[k]) w.ring[(upos + t[k]) & kMask] = w.out[y[k]];
+                for (int j = 0; j < 4; ++j)
+                    if (old[j]) w.ring[(X + j) & kMask] = w.out[y[j]];
             }
         }
         if (__ballot(anypnd)) {
-            // sources inside the window: follow refs through this pass's pending bytes (bytes
-            // of earlier passes and bytes with refs == 0xFFFF are final in the ring)
+            // sources inside this pass: follow refs through pending bytes (bytes of earlier
+            // passes and bytes with refs == 0xFFFF are final in the ring)
             wave_sync();
             uint32_t z[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) z[k] = pnd[k] ? y[k] - upos : 0u;
+            for (int j = 0; j < 4; ++j) z[j] = pnd[j] ? y[j] - upos : brc;
             for (;;) {
                 bool more = false;
                 uint32_t r[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) r[k] = refs[z[k]];
+                for (int j = 0; j < 4; ++j) r[j] = refs[z[j] + a0];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const bool mo = pnd[k] && z[k] >= b && r[k] != 0xFFFFu;
-                    z[k] = mo ? r[k] : z[k];
+                for (int j = 0; j < 4; ++j) {
+                    const bool mo = pnd[j] & (z[j] >= brc) & (r[j] != 0xFFFFu);
+                    z[j] = mo ? r[j] : z[j];
                     more |= mo;
                 }
                 if (!__ballot(more)) break;
             }
-            uint8_t v[4];
+            uint8_t vv[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) v[k] = w.ring[(upos + z[k]) & kMask];
+            for (int j = 0; j < 4; ++j) vv[j] = w.ring[(upos + z[j]) & kMask];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (pnd[k]) w.ring[(upos + t[k]) & kMask] = v[k];
+            for (int j = 0; j < 4; ++j) *(pnd[j] ? w.ring + ((X + j) & kMask) : w.sink + lane) = vv[j];
         }
         wave_sync();
     }
-    wave_sync();
     w.upos = upos + S;
     const uint64_t tf = PROF_NOW();
     dec_maybe_flush(w);
@@ -745,8 +738,8 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     w.ring = smem + wv * dec::kWaveLds;
     w.cin = w.ring + dec::kRing;
     w.marks = w.cin + dec::kCring;
-    w.refs = (uint16_t*)(w.marks + dec::kWin + 64);
-    w.sink = (uint8_t*)(w.refs + dec::kWin);
+    w.refs = (uint16_t*)(w.marks + dec::kMarks);
+    w.sink = (uint8_t*)(w.refs + dec::kMarks);
     w.mtab = (uint2*)(w.sink + dec::kSink);
     w.out = dst + blk[U.first].dst_off;
     w.upos = 0;
