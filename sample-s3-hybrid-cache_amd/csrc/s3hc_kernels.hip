@@ -789,6 +789,7 @@ constexpr uint32_t kGIn = kPad + kPrewarm + kGroupSegs * kSeg + 128;  // a group
 constexpr uint32_t kGThreads = 64 * kGroupSegs;
 constexpr uint32_t kTbl = 1u << kHashLog;
 constexpr uint32_t kSteps = 8;                              // 64-position steps per sub-block
+constexpr uint32_t kStash = 64 * kSteps / 4;                // hops per sub-block (a hop covers >= 4 bytes)
 constexpr uint32_t kFwd = 19;                               // forward bytes measured per probe (4 + 15)
 constexpr uint32_t kEmpty = 0xFFFFu;
 }  // namespace enc
@@ -844,35 +845,6 @@ __device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* 
     for (uint32_t t = 16 * nv + lane; t < n; t += nthr) lds[t] = g[t];
 }
 
-// Lane-parallel LZ4 sequence records for the greedy hops of one 64-position chunk (bit j of
-// hm = a match taken at base + j; lane j holds that position's probe word and forward length):
-// clip each backward extension at the previous match end, form (literal length, match length,
-// offset), add up the encoded sizes, store the records.
-__device__ __forceinline__ uint32_t enc_chunk_records(int lane, uint64_t hm, uint32_t base, uint32_t word,
-                                                      uint32_t lenf, uint32_t last_end, uint32_t nseq,
-                                                      uint32_t& ll0, uint2* myrec) {
-    const bool hop = (hm >> lane) & 1ull;
-    const uint64_t below = hm & ((1ull << lane) - 1ull);
-    const uint32_t P = base + lane;
-    const uint32_t endj = P + lenf;
-    const uint32_t bh = (uint32_t)(below >> 32), bl = (uint32_t)below;
-    const int ph = 63 - __builtin_clz(bh | 1u), plo = 31 - __builtin_clz(bl | 1u);
-    const int pl = bh ? ph : plo;  // previous hop lane (any lane when there is none)
-    const uint32_t pe = __shfl(endj, pl);
-    const uint32_t prev = below ? pe : last_end;
-    uint32_t nb = (word >> 24) & 7u;
-    if (nb > P - prev) nb = P - prev;
-    const uint32_t ll = P - nb - prev;
-    const uint32_t len = nb + lenf;
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0));
-    const uint32_t gj = nseq + rank;
-    const uint32_t tok = gj == 0 ? 0u : 1u + ext_bytes(ll);
-    const uint32_t sz = hop ? tok + ll + 2u + ext_bytes(len - 4) : 0u;
-    if (nseq == 0) ll0 = rdl(ll, (uint32_t)__builtin_ctzll(hm));
-    if (hop) myrec[gj] = make_uint2(ll | (len << 16), word & 0xFFFFu);
-    return rdl(wave_incl_sum(sz), 63);  // encoded bytes of these sequences
-}
-
 // Match finding for one 4 KiB segment per wave (the segment's 4 KiB prefix window is staged
 // too and pre-inserted into the hash table). Per 512-position sub-block:
 //   A  table pass: every position hashes its 4 bytes, reads the per-wave LDS table (u16
@@ -896,6 +868,7 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
     using namespace enc;
     __shared__ __attribute__((aligned(16))) uint8_t inb_raw[kGIn];
     __shared__ __attribute__((aligned(16))) uint16_t tbl_all[kGroupSegs][kTbl + 8];  // slot kTbl: sink
+    __shared__ __attribute__((aligned(16))) uint2 stash_all[kGroupSegs][kStash + 8];  // hops of a sub-block (+ sink)
     // The first nxx workgroups compute the frames' content xxh32 (they are dispatched first and
     // overlap the match finding; the emitter reads the hashes).
     if (blockIdx.x < nxx) {
@@ -918,6 +891,7 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = lane_id();
     uint16_t* tbl = tbl_all[wv];
+    uint2* stash = stash_all[wv];
     for (uint32_t t = lane; t < (kTbl + 8) / 8; t += 64) ((uint4*)tbl)[t] = make_uint4(~0u, ~0u, ~0u, ~0u);
     stage_in(bin, stage_lo, stage_hi, inb_raw + kPad, threadIdx.x, kGThreads);
     __syncthreads();
@@ -1031,16 +1005,12 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
         }
         const uint64_t tc1 = PROF_NOW();
         PROF_ADD(epr, 1, tc1 - tc0);
-        // ---- C: greedy walk over the chunks (scalar), then every chunk's records at once (the
-        // chunks' record passes are independent, so their latencies overlap)
-        uint64_t hms[kSteps];
-        uint32_t le_in[kSteps], ns_in[kSteps];
+        // ---- C: greedy walk over the chunks (scalar); each chunk's hops are stashed in LDS in
+        // order, then the sub-block's sequence records are formed 64 hops at a time
+        const uint32_t ns_sb = nseq, le_sb = last_end;
 #pragma unroll
         for (uint32_t q = 0; q < kSteps; ++q) {
             const uint32_t base = sb + 64 * q;
-            hms[q] = 0;
-            le_in[q] = last_end;
-            ns_in[q] = nseq;
             if (x >= base + 64 || !mm[q]) continue;
             uint64_t hm = 0;
             // per lane: greedy position after taking this lane's match (chunk-relative);
@@ -1084,15 +1054,42 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
             }
             x = base + r;
             if (hm) {
-                hms[q] = hm;
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0));
+                const uint32_t hidx = (hm >> lane) & 1ull ? nseq - ns_sb + rank : kStash + ((uint32_t)lane & 7u);
+                stash[hidx] = make_uint2((base + lane - seg_lo) | (flen[q] << 16), word[q]);
                 last_end = base + rend;
                 nseq += (uint32_t)__builtin_popcountll(hm);
             }
         }
         const uint64_t tf0 = PROF_NOW();
-#pragma unroll
-        for (uint32_t q = 0; q < kSteps; ++q)
-            if (hms[q]) body += enc_chunk_records(lane, hms[q], sb + 64 * q, word[q], flen[q], le_in[q], ns_in[q], ll0, myrec);
+        wave_sync();
+        {
+            const uint32_t H = nseq - ns_sb;
+            uint32_t carry_end = le_sb;
+            for (uint32_t g = 0; g < H; g += 64) {
+                const uint32_t idx = g + lane;
+                const bool act = idx < H;
+                const uint2 e = stash[act ? idx : 0u];
+                const uint32_t P = seg_lo + (e.x & 0xFFFFu), lenf = e.x >> 16, wd = e.y;
+                const uint32_t endj = P + lenf;
+                const uint32_t pe = dpp0<0x138, 0xF>(endj);  // wave_shr:1: previous hop's end
+                const uint32_t prev = lane == 0 ? carry_end : pe;
+                uint32_t nb = (wd >> 24) & 7u;
+                nb = nb > P - prev ? P - prev : nb;
+                const uint32_t ll = P - nb - prev;
+                const uint32_t len = nb + lenf;
+                const uint32_t gj = ns_sb + idx;
+                const uint32_t tok = gj == 0 ? 0u : 1u + ext_bytes(ll);
+                const uint32_t sz = act ? tok + ll + 2u + ext_bytes(len - 4) : 0u;
+                body += rdl(wave_incl_sum(sz), 63);
+                if (ns_sb == 0 && g == 0) ll0 = rdl(ll, 0);  // first sequence of the segment
+                if (act) myrec[gj] = make_uint2(ll | (len << 16), wd & 0xFFFFu);
+                const uint32_t last = H - g < 64 ? H - g - 1 : 63u;
+                carry_end = rdl(endj, last);
+            }
+        }
+        wave_sync();
         PROF_ADD(epr, 4, PROF_NOW() - tf0);
         PROF_ADD(epr, 3, PROF_NOW() - tc1);
     }
