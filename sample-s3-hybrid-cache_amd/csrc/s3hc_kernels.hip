@@ -973,31 +973,38 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
 #pragma unroll
             for (int j = 0; j < 4; ++j) Q[j + 1] = __builtin_amdgcn_alignbyte(O[j + 1], O[j], sh);
             const uint32_t maxf = end_lim - P;  // >= 4 for P <= smax
-            const uint32_t fs = (4u - df) & 3u;
-            uint32_t lt = 20u, lf = 20u;
+            uint32_t lt = 20u;
 #pragma unroll
             for (int j = 3; j >= 0; --j) {
                 const uint32_t dt = Q[j + 1] ^ __builtin_amdgcn_alignbyte(T[j + 3], T[j + 2], ts);
-                const uint32_t dfw = Q[j + 1] ^ __builtin_amdgcn_alignbyte(Q[j + 1], Q[j], fs);
                 lt = dt ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dt) >> 3) : lt;
-                lf = dfw ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dfw) >> 3) : lf;
             }
             lt = lt > kFwd ? kFwd : lt;
             lt = lt > maxf ? maxf : lt;
-            lf = lf > kFwd ? kFwd : lf;
-            lf = lf > maxf ? maxf : lf;
             const uint32_t bt = vm4 ^ __builtin_amdgcn_alignbyte(T[1], T[0], ts);
-            const uint32_t bf = vm4 ^ __builtin_amdgcn_alignbyte(vm4, vm8[q], fs);
             uint32_t nbt = bt ? (uint32_t)__builtin_clz(bt) >> 3 : 4u;
-            uint32_t nbf = bf ? (uint32_t)__builtin_clz(bf) >> 3 : 4u;
             nbt = nbt > ct ? ct : nbt;                      // ct < i
-            nbf = nbf > i - df ? i - df : nbf;
             const bool gt = valid & tin & (__builtin_amdgcn_alignbyte(T[2], T[1], ts) == v);
             const bool gf = valid & (df != 0);
-            const bool ut = gt & (!gf | (lt >= lf));
-            const uint32_t len = ut ? lt : lf;
-            const uint32_t nb = ut ? nbt : nbf;
-            const uint32_t dist = ut ? i - ct : df;
+            uint32_t len = lt, nb = nbt, dist = i - ct;
+            if (__ballot(gf)) {  // short-distance repeats are rare in most steps
+                const uint32_t fs = (4u - df) & 3u;
+                uint32_t lf = 20u;
+#pragma unroll
+                for (int j = 3; j >= 0; --j) {
+                    const uint32_t dfw = Q[j + 1] ^ __builtin_amdgcn_alignbyte(Q[j + 1], Q[j], fs);
+                    lf = dfw ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dfw) >> 3) : lf;
+                }
+                lf = lf > kFwd ? kFwd : lf;
+                lf = lf > maxf ? maxf : lf;
+                const uint32_t bf = vm4 ^ __builtin_amdgcn_alignbyte(vm4, vm8[q], fs);
+                uint32_t nbf = bf ? (uint32_t)__builtin_clz(bf) >> 3 : 4u;
+                nbf = nbf > i - df ? i - df : nbf;
+                const bool ut = gt & (!gf | (lt >= lf));
+                len = ut ? lt : lf;
+                nb = ut ? nbt : nbf;
+                dist = ut ? i - ct : df;
+            }
             word[q] = dist | ((len - 4) << 16) | (nb << 24);
             flen[q] = len;
             mm[q] = __ballot(gt | gf);
