@@ -915,7 +915,18 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
     int64_t smax = (int64_t)end_lim - 4;
     if ((int64_t)U - 12 < smax) smax = (int64_t)U - 12;
     // prewarm the table with the window before the segment
-    for (uint32_t x = pw_lo + lane; x + 4 <= seg_lo; x += 64) tbl[hash4(lds32u(inb, x - pw_lo))] = (uint16_t)(x - pw_lo);
+    // (four positions per lane from one aligned 8-byte read)
+    {
+        const uint32_t lim = seg_lo - pw_lo;  // window position i is inserted when i + 4 <= lim
+        for (uint32_t d0 = lane; 4 * d0 < lim; d0 += 64) {
+            const uint32_t w0 = dw[d0], w1 = dw[d0 + 1];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t i = 4 * d0 + j;
+                tbl[i + 4 <= lim ? hash4(__builtin_amdgcn_alignbyte(w1, w0, j)) : kTbl] = (uint16_t)i;
+            }
+        }
+    }
     wave_sync();
 #ifdef S3HC_PROF
     epr[0] = PROF_NOW() - tk0;
@@ -954,11 +965,8 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
             const bool valid = P < sb_end;
             const uint32_t i = P - pw_lo;
             const uint32_t v = vv[q], vm4 = vm[q];
-            const bool r1 = (__builtin_amdgcn_alignbyte(v, vm4, 3) == v) & (i >= 1);
-            const bool r2 = (__builtin_amdgcn_alignbyte(v, vm4, 2) == v) & (i >= 2);
-            const bool r3 = (__builtin_amdgcn_alignbyte(v, vm4, 1) == v) & (i >= 3);
-            const bool r4 = (vm4 == v) & (i >= 4);
-            const uint32_t df = r1 ? 1u : (r2 ? 2u : (r3 ? 3u : (r4 ? 4u : 0u)));
+            const bool e1 = __builtin_amdgcn_alignbyte(v, vm4, 3) == v, e2 = __builtin_amdgcn_alignbyte(v, vm4, 2) == v;
+            const bool e3 = __builtin_amdgcn_alignbyte(v, vm4, 1) == v, e4 = vm4 == v;
             const uint32_t c16 = cc[q];
             const bool tin = (c16 != kEmpty) & (c16 < i);
             const uint32_t ct = tin ? c16 : i;
@@ -985,9 +993,11 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
             uint32_t nbt = bt ? (uint32_t)__builtin_clz(bt) >> 3 : 4u;
             nbt = nbt > ct ? ct : nbt;                      // ct < i
             const bool gt = valid & tin & (__builtin_amdgcn_alignbyte(T[2], T[1], ts) == v);
-            const bool gf = valid & (df != 0);
             uint32_t len = lt, nb = nbt, dist = i - ct;
-            if (__ballot(gf)) {  // short-distance repeats are rare in most steps
+            bool gf = false;
+            if (__ballot(valid & (e1 | e2 | e3 | e4))) {  // short-distance repeats are rare in most steps
+                const uint32_t df = (e1 & (i >= 1)) ? 1u : ((e2 & (i >= 2)) ? 2u : ((e3 & (i >= 3)) ? 3u : ((e4 & (i >= 4)) ? 4u : 0u)));
+                gf = valid & (df != 0);
                 const uint32_t fs = (4u - df) & 3u;
                 uint32_t lf = 20u;
 #pragma unroll
