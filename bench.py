@@ -109,6 +109,26 @@ def cpu_baseline(data: bytes, block: int, seconds: float):
     }
 
 
+KERNEL_SYMBOL = {"enc_parse": "k_enc_parse", "enc_emit": "k_enc_emit", "decode": "k_decode_units",
+                 "xxh32": "k_xxh32_ranges"}
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/rNN/traffic.json, made by tools_traffic.sh from this same bench command:
+    FETCH_SIZE and WRITE_SIZE in separate --pmc passes, per-dispatch averages in KB).
+    FETCH_SIZE is doubled: on gfx950 it counts half the bytes of 16-B/lane streaming reads."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get(KERNEL_SYMBOL.get(kernel, kernel), {})
+    if "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
+        return None, None
+    return int((2 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024), os.path.relpath(files[-1], ROOT)
+
+
 def main():
     args = parse_args()
     g = shard.Group()
@@ -189,11 +209,14 @@ def main():
             "xxh32": nb * block,                      # U read (decode-side verify; encode side runs on the side stream)
         }.get(dom, nb * block)
         achieved = alg / per_launch_s / 1e9
+        traffic, tsrc = pmc_traffic(dom)
         roof = {
             "bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ms / n, 4),
         }
+        if tsrc:
+            roof["traffic_source"] = tsrc + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same bench command)"
     per_kernel = {k: round(v[0] / args.steps, 4) for k, v in kt.items()}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
