@@ -219,26 +219,32 @@ __global__ __launch_bounds__(256) void k_xxh32_ranges(const uint8_t* __restrict_
 
 // ================================================================== decode
 namespace dec {
-constexpr uint32_t kCring = 1024;  // compressed input ring per wave (aligned-address space)
+constexpr uint32_t kCring = 2048;  // compressed input ring per wave (aligned-address space)
 constexpr uint32_t kCmask = kCring - 1;
 constexpr uint32_t kChunk = 256;   // ring refill granule: one dword per lane
-constexpr uint32_t kAhead = 512;   // input kept staged ahead of the parse position
+constexpr uint32_t kAhead = 1024;  // input kept staged ahead of the parse position
+constexpr uint32_t kInit = 5;      // chunks loaded up front (>= kAhead + 3 bytes)
+constexpr uint32_t kPos = 256;     // token positions examined per window (4 per lane)
+constexpr uint32_t kMaxMem = 128;  // members (sequences) per window
 constexpr uint32_t kRing = 4096;   // recent output kept in LDS per wave (match sources)
 constexpr uint32_t kMask = kRing - 1;
 constexpr uint32_t kFlush = 1024;  // ring -> HBM flush granule
-constexpr uint32_t kWin = 768;     // output bytes executed per window (byte-parallel)
-constexpr uint32_t kMarks = 1024;  // marks/refs entries: >= kWin + 3 rounded up to the 256-byte pass
+constexpr uint32_t kWin = 1024;    // output bytes executed per window (byte-parallel)
+constexpr uint32_t kMarks = 1280;  // marks entries: >= kWin + 3 rounded up to the 256-byte pass
+constexpr uint32_t kRefs = 256;    // refs entries: one 256-byte pass
 constexpr uint32_t kSink = 64;     // per-lane store sink for lanes with nothing to store
-constexpr uint32_t kWaveLds = kRing + kCring + kMarks + 2 * kMarks + kSink + 128 * 8;
+constexpr uint32_t kWaveLds = kRing + kCring + kMarks + 2 * kRefs + kSink + kMaxMem * 8;
 constexpr int kWaves = 4;
 enum : uint32_t { F_ERR = 1, F_LAST = 2, F_LONG = 4, F_MORE = 8 };
+static_assert(kInit * kChunk >= kAhead + 3, "initial stage must cover the look-ahead");
+static_assert(kMaxMem <= 255, "marks hold member index + 1 in a byte");
 }  // namespace dec
 
 struct DecWave {
     uint8_t* ring;
     uint8_t* cin;        // kCring bytes: compressed input, byte p of the block at (p + mis) & kCmask
-    uint8_t* marks;      // kMarks bytes: sequence start marks of the current window
-    uint16_t* refs;      // kMarks entries: in-pass match source of each output byte
+    uint8_t* marks;      // kMarks bytes: sequence start marks of the current window (zero between windows)
+    uint16_t* refs;      // kRefs entries: in-pass match source of each output byte of the current pass
     uint8_t* sink;       // kSink bytes: target of stores from lanes with nothing to store
     uint2* mtab;         // 128 entries: the window's member sequences (start, ll, off, literal)
     uint8_t* out;        // unit output base in HBM
@@ -382,10 +388,9 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
     const uint32_t a0 = upos & 3u;        // byte u of a pass = window byte u - a0 (ring dwords aligned)
     const uint32_t xbase = upos - a0;
     const uint32_t np = (S + a0 + 255u) >> 8;
-    ((uint4*)marks)[lane] = make_uint4(0, 0, 0, 0);  // clears [0, kMarks)
-    wave_sync();
-    // member m (token position q + m) starts at window byte orel: marks[orel + a0] = m + 1; the
-    // member table holds (orel | ll << 16, off | literal ring index << 16)
+    // member m starts at window byte orel: marks[orel + a0] = m + 1 (marks are zero between
+    // windows: each pass clears the dwords it reads); the member table holds
+    // (orel | ll << 16, off | literal ring index << 16)
     *((isM0 && sl0) ? marks + orel0 + a0 : w.sink + lane) = (uint8_t)(lane + 1);
     *((isM1 && sl1) ? marks + orel1 + a0 : w.sink + lane) = (uint8_t)(lane + 65);
     w.mtab[lane] = make_uint2(orel0 | (ll0 << 16), pkB0);
@@ -399,6 +404,7 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
         const uint32_t brc = p ? 256u * p - a0 : 0u;          // first window byte of this pass
         // ---- owners
         const uint32_t md = ((const uint32_t*)marks)[64u * p + (uint32_t)lane];
+        ((uint32_t*)marks)[64u * p + (uint32_t)lane] = 0u;
         const uint32_t b0 = md & 0xFFu, b1 = (md >> 8) & 0xFFu, b2 = (md >> 16) & 0xFFu, b3 = md >> 24;
         const uint32_t c1 = umax32(b0, b1), c2 = umax32(c1, b2), c3 = umax32(c2, b3);
         const uint32_t inc = wave_incl_max(c3);
@@ -429,10 +435,22 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
             anywrap |= wrap[j];
             y[j] = X + j - moff;              // non-overlapping source
         }
-        if (__ballot(anywrap)) {              // overlapping matches: period moff
+        if (__ballot(anywrap)) {
+            // overlapping matches (period moff): the source is the byte ee mod moff of the first
+            // period. ee < kWin and moff < ee, so ee * rcp(moff) is within 2^-11 of ee / moff and
+            // its truncation is exact or one short (at exact multiples), fixed by one compare.
+            const float rA = __builtin_amdgcn_rcpf((float)(fA.y & 0xFFFFu));
+            const float rB = __builtin_amdgcn_rcpf((float)(fB.y & 0xFFFFu));
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (wrap[j]) y[j] = X + j - ee[j] - mf[j] + ee[j] % mf[j];
+            for (int j = 0; j < 4; ++j) {
+                if (wrap[j]) {
+                    const float rf = o[j] == o[3] ? rB : rA;
+                    const uint32_t qt = (uint32_t)((float)ee[j] * rf);
+                    uint32_t rm = ee[j] - __umul24(qt, mf[j]);
+                    rm = rm >= mf[j] ? rm - mf[j] : rm;
+                    y[j] = X + j - ee[j] - mf[j] + rm;
+                }
+            }
         }
         const uint32_t oldw = ((const uint32_t*)w.ring)[(X & kMask) >> 2];
         uint32_t v[4];
@@ -455,7 +473,7 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
         ((uint32_t*)w.ring)[(X & kMask) >> 2] = (val & vm) | (oldw & ~vm);
         const uint32_t r0 = pnd[0] ? y[0] - upos : 0xFFFFu, r1 = pnd[1] ? y[1] - upos : 0xFFFFu;
         const uint32_t r2 = pnd[2] ? y[2] - upos : 0xFFFFu, r3 = pnd[3] ? y[3] - upos : 0xFFFFu;
-        *(uint2*)(refs + u0) = make_uint2(r0 | (r1 << 16), r2 | (r3 << 16));
+        *(uint2*)(refs + 4u * (uint32_t)lane) = make_uint2(r0 | (r1 << 16), r2 | (r3 << 16));  // pass-local
         if (upos > kRing - S) {
             // sources older than the ring are read back from HBM (already flushed); kept apart
             // so the common path never waits on the wave's outstanding flush stores
@@ -481,8 +499,9 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
             for (;;) {
                 bool more = false;
                 uint32_t r[4];
+                // refs index of window byte z in this pass: z + a0 - 256p (in [0, 256) for z >= brc)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) r[j] = refs[z[j] + a0];
+                for (int j = 0; j < 4; ++j) r[j] = refs[(z[j] + a0 - 256u * p) & (kRefs - 1u)];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const bool mo = pnd[j] & (z[j] >= brc) & (r[j] != 0xFFFFu);
@@ -542,6 +561,27 @@ __device__ __forceinline__ DecTok dec_spec(const uint8_t* cin, uint32_t qq, uint
     return T;
 }
 
+// Next-token step of a token assumed at block position qq, for the chain walk of the window at
+// q: nxt - q (1..kPos-1) when the next token lies inside the window and this token is an
+// ordinary sequence; kPos when the chain leaves the window here (next token at or past q + kPos,
+// last sequence, malformed, long length run, or bytes past the staged input — dec_spec then
+// tells which). Consistent with dec_spec: a step < kPos implies dec_spec flags are clear.
+__device__ __forceinline__ uint32_t dec_step(const uint8_t* cin, uint32_t qq, uint32_t q, uint32_t mis, uint32_t C,
+                                             uint32_t fill) {
+    using namespace dec;
+    const uint32_t w0 = cin32(cin, qq + mis);
+    const uint32_t t = w0 & 0xFFu, L = t >> 4, M = t & 15u;
+    const uint32_t e1 = (w0 >> 8) & 0xFFu, e2 = (w0 >> 16) & 0xFFu;
+    const bool x1 = L == 15u, x2 = x1 && e1 == 255u;
+    const uint32_t mp = qq + 1u + L + (x1 ? 1u + e1 : 0u) + (x2 ? 1u + e2 : 0u);
+    const uint32_t w1 = cin32(cin, mp + mis);
+    const uint32_t f1 = (w1 >> 16) & 0xFFu, f2 = w1 >> 24;
+    const bool y1 = M == 15u, y2 = y1 && f1 == 255u;
+    const uint32_t nxt = mp + 2u + (y1 ? 1u : 0u) + (y2 ? 1u : 0u);
+    const bool stop = (x2 && e2 == 255u) | (y2 && f2 == 255u) | (mp + mis + 4u > fill) | (nxt >= C) | (nxt - q >= kPos);
+    return stop ? kPos : nxt - q;
+}
+
 // Decode one compressed block of C bytes. hist = bytes of earlier unit output matches may use.
 // Output overflowing `limit` is corruption (lz4_flex: output sink bounded by the block size);
 // overflowing only `cap` is DST_TOO_SMALL.
@@ -560,12 +600,17 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
     uint32_t fill;
     uint32_t pf;
     {
-        const uint32_t k0 = (uint32_t)lane, k1 = k0 + 64, k2 = k0 + 128;
-        const uint32_t d0 = aw[k0 < kmax ? k0 : kmax], d1 = aw[k1 < kmax ? k1 : kmax];
-        pf = aw[k2 < kmax ? k2 : kmax];
-        cr[k0] = d0;
-        cr[k1] = d1;
-        fill = 2 * kChunk;
+        uint32_t d[kInit];
+#pragma unroll
+        for (uint32_t c = 0; c < kInit; ++c) {
+            const uint32_t k = 64u * c + (uint32_t)lane;
+            d[c] = aw[k < kmax ? k : kmax];
+        }
+        const uint32_t kp = 64u * kInit + (uint32_t)lane;
+        pf = aw[kp < kmax ? kp : kmax];
+#pragma unroll
+        for (uint32_t c = 0; c < kInit; ++c) cr[64u * c + (uint32_t)lane] = d[c];
+        fill = kInit * kChunk;
     }
     uint32_t q = 0;
     for (;;) {
@@ -586,74 +631,86 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
             wave_sync();
         }
         const uint64_t tp0 = PROF_NOW();
-        // ---- speculative parse at the window's 128 token positions: lane holds q + lane (set 0)
-        // and q + 64 + lane (set 1)
-        const DecTok t0 = dec_spec(w.cin, q + lane, mis, C, fill);
-        const DecTok t1 = dec_spec(w.cin, q + 64 + lane, mis, C, fill);
-        // ---- walk the true token chain (scalar, one readlane per hop); nx = next position - q,
-        // 128 for a position that ends the chain (error, long run, past the ring, last)
-        auto nxof = [&](const DecTok& T) -> uint32_t {
-            const bool term = (T.flags & (F_ERR | F_LONG | F_MORE | F_LAST)) != 0;
-            return term ? 128u : (T.nxt - q < 128u ? T.nxt - q : 128u);
-        };
-        const uint32_t nx0 = nxof(t0), nx1 = nxof(t1);
-        uint64_t m0 = 0, m1 = 0;
+        // ---- chain walk over the window's kPos token positions. Each lane evaluates the
+        // next-token step at positions q + lane + 64k (k = 0..3); the scalar walk follows the true
+        // chain from q (one readlane per hop) and marks members in four 64-bit masks; members are
+        // then compacted into member order (mbcnt ranks through a small LDS slot table).
+        const uint32_t nx0 = dec_step(w.cin, q + lane, q, mis, C, fill);
+        const uint32_t nx1 = dec_step(w.cin, q + 64 + lane, q, mis, C, fill);
+        const uint32_t nx2 = dec_step(w.cin, q + 128 + lane, q, mis, C, fill);
+        const uint32_t nx3 = dec_step(w.cin, q + 192 + lane, q, mis, C, fill);
+        uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
         uint32_t l = 0, lastl = 0;
-        while (l < 64u) {
-            lastl = l;
-            m0 |= 1ull << l;
-            l = rdl(nx0, l);
+        while (l < 64u) { lastl = l; m0 |= 1ull << l; l = rdl(nx0, l); }
+        while (l < 128u) { lastl = l; m1 |= 1ull << (l - 64u); l = rdl(nx1, l - 64u); }
+        while (l < 192u) { lastl = l; m2 |= 1ull << (l - 128u); l = rdl(nx2, l - 128u); }
+        while (l < 256u) { lastl = l; m3 |= 1ull << (l - 192u); l = rdl(nx3, l - 192u); }
+        // members are >= 3 bytes apart except the last, so at most 86 of them (< kMaxMem)
+        const uint32_t c1 = (uint32_t)__builtin_popcountll(m0), c2 = c1 + (uint32_t)__builtin_popcountll(m1);
+        const uint32_t c3 = c2 + (uint32_t)__builtin_popcountll(m2);
+        uint32_t n = c3 + (uint32_t)__builtin_popcountll(m3);
+        {
+            uint8_t* slots = (uint8_t*)w.refs;  // refs are free between passes
+            auto put = [&](uint64_t m, uint32_t base, uint32_t k) {
+                const uint32_t rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                *(((m >> lane) & 1ull) ? slots + rank : w.sink + lane) = (uint8_t)(64u * k + (uint32_t)lane);
+            };
+            put(m0, 0, 0);
+            if (m1) put(m1, c1, 1);
+            if (m2) put(m2, c2, 2);
+            if (m3) put(m3, c3, 3);
+            wave_sync();
         }
-        while (l < 128u) {
-            lastl = l;
-            m1 |= 1ull << (l - 64);
-            l = rdl(nx1, l - 64);
-        }
+        const uint32_t rp0 = ((const uint8_t*)w.refs)[lane];
+        const uint32_t rp1 = n > 64u ? ((const uint8_t*)w.refs)[64 + lane] : 0u;
+        // ---- members decoded densely: member m's token in lane m (set 0) / m - 64 (set 1)
+        const DecTok t0 = dec_spec(w.cin, q + rp0, mis, C, fill);
+        DecTok t1 = {0u, 0u, 0u, 0u, 0u, 0u};
+        if (n > 64u) t1 = dec_spec(w.cin, q + rp1, mis, C, fill);
         auto rd2 = [&](uint32_t v0, uint32_t v1, uint32_t m) -> uint32_t { return m < 64 ? rdl(v0, m) : rdl(v1, m - 64); };
         int stop = 0;  // 0 window exhausted, 1 last sequence, 2 error, 3 slow path at cur, 4 long sequence
-        uint32_t cur;
+        uint32_t cur, cm = 0;  // cm: member run by the long-sequence path (stop 4)
         {
-            const uint32_t fl = rd2(t0.flags, t1.flags, lastl);
+            const uint32_t fl = rd2(t0.flags, t1.flags, n - 1u);
             if (fl & (F_LONG | F_MORE | F_ERR)) {
-                if (lastl < 64) m0 &= ~(1ull << lastl);
-                else m1 &= ~(1ull << (lastl - 64));
+                --n;  // the chain's last token goes to the slow path (or is an error)
                 stop = (fl & (F_LONG | F_MORE)) ? 3 : 2;
                 cur = q + lastl;
             } else if (fl & F_LAST) {
                 stop = 1;
                 cur = C;
             } else {
-                cur = rd2(t0.nxt, t1.nxt, lastl);
+                cur = rd2(t0.nxt, t1.nxt, n - 1u);
             }
         }
         const uint64_t tp1 = PROF_NOW();
         PROF_ADD(w.pr, 1, tp1 - tp0);
-        if (m0 | m1) {
-            bool isM0 = (m0 >> lane) & 1ull, isM1 = (m1 >> lane) & 1ull;
+        if (n) {
+            bool isM0 = (uint32_t)lane < n, isM1 = (uint32_t)lane + 64u < n;
             const uint32_t sl0 = isM0 ? t0.ll + ((t0.flags & F_LAST) ? 0u : t0.ml) : 0u;
             const uint32_t sl1 = isM1 ? t1.ll + ((t1.flags & F_LAST) ? 0u : t1.ml) : 0u;
             const uint32_t orel0 = wave_excl_scan(sl0, lane);
             const uint32_t tot0 = rdl(orel0 + sl0, 63);
-            const uint32_t orel1 = tot0 + wave_excl_scan(sl1, lane);
-            uint32_t S = rdl(orel1 + sl1, 63);
+            uint32_t orel1 = tot0;
+            uint32_t S = tot0;
+            if (n > 64u) {
+                orel1 = tot0 + wave_excl_scan(sl1, lane);
+                S = rdl(orel1 + sl1, 63);
+            }
             // output budget: the members that fit in kWin run now, the rest next window
             const uint64_t cut0 = __ballot(isM0 && orel0 + sl0 > kWin);
             const uint64_t cut1 = __ballot(isM1 && orel1 + sl1 > kWin);
             if (cut0 | cut1) {
                 const uint32_t c = cut0 ? (uint32_t)__builtin_ctzll(cut0) : 64u + (uint32_t)__builtin_ctzll(cut1);
-                if (c < 64) {
-                    m0 &= (1ull << c) - 1ull;
-                    m1 = 0;
-                } else {
-                    m1 &= (1ull << (c - 64)) - 1ull;
-                }
-                isM0 = (m0 >> lane) & 1ull;
-                isM1 = (m1 >> lane) & 1ull;
+                n = c;
+                isM0 = (uint32_t)lane < n;
+                isM1 = (uint32_t)lane + 64u < n;
                 S = rd2(orel0, orel1, c);
-                stop = (m0 | m1) ? 0 : 4;
-                cur = q + c;
+                stop = n ? 0 : 4;
+                cm = c;
+                cur = q + rd2(rp0, rp1, c);
             }
-            if (m0 | m1) {
+            if (n) {
                 // lz4_flex bound checks, lane-parallel; the first failing member decides
                 const uint32_t base = w.upos - bstart;
                 auto check = [&](const DecTok& T, uint32_t orel) -> int {
@@ -677,7 +734,7 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
                                 t0.off | (((t0.lit + mis) & kCmask) << 16), t1.off | (((t1.lit + mis) & kCmask) << 16));
                 PROF_ADD(w.pr, 2, PROF_NOW() - tp1);
                 PROF_ADD(w.pr, 5, 1);
-                PROF_ADD(w.pr, 6, __builtin_popcountll(m0) + __builtin_popcountll(m1));
+                PROF_ADD(w.pr, 6, n);
                 PROF_ADD(w.pr, 7, (S + 255) / 256);
                 PROF_ADD(w.pr, 11, S);
             }
@@ -686,7 +743,7 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
         if (stop == 1) return S3HC_OK;
         if (stop == 2) return S3HC_CORRUPT;
         if (stop == 4) {
-            const uint32_t c = cur - q;
+            const uint32_t c = cm;
             const uint32_t f = rd2(t0.flags, t1.flags, c);
             const int rc = dec_seq(w, in, rd2(t0.lit, t1.lit, c), rd2(t0.ll, t1.ll, c), (f & F_LAST) != 0,
                                    rd2(t0.off, t1.off, c), rd2(t0.ml, t1.ml, c), mis, fill, bstart, limit, cap, hist);
@@ -739,8 +796,9 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     w.cin = w.ring + dec::kRing;
     w.marks = w.cin + dec::kCring;
     w.refs = (uint16_t*)(w.marks + dec::kMarks);
-    w.sink = (uint8_t*)(w.refs + dec::kMarks);
+    w.sink = (uint8_t*)(w.refs + dec::kRefs);
     w.mtab = (uint2*)(w.sink + dec::kSink);
+    for (uint32_t i = (uint32_t)lane; i < dec::kMarks / 16; i += 64) ((uint4*)w.marks)[i] = make_uint4(0, 0, 0, 0);
     w.out = dst + blk[U.first].dst_off;
     w.upos = 0;
     w.flushed = 0;
