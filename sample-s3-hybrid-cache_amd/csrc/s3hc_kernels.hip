@@ -33,6 +33,14 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
 }
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)); }
 
+// Serial scalar walks (one readlane per hop) raise the wave's issue priority so their
+// readlanes are not queued behind other waves' vector work (diagnostic builds can disable).
+#ifndef S3HC_WALK_PRIO
+#define S3HC_WALK_PRIO 3
+#endif
+#define WALK_PRIO_ON() __builtin_amdgcn_s_setprio(S3HC_WALK_PRIO)
+#define WALK_PRIO_OFF() __builtin_amdgcn_s_setprio(0)
+
 // Orders this wave's LDS traffic across lanes (lanes of one wave share an in-order LDS queue;
 // this only stops the compiler from moving accesses across the point).
 __device__ __forceinline__ void wave_sync() {
@@ -641,10 +649,12 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
         const uint32_t nx3 = dec_step(w.cin, q + 192 + lane, q, mis, C, fill);
         uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
         uint32_t l = 0, lastl = 0;
+        WALK_PRIO_ON();
         while (l < 64u) { lastl = l; m0 |= 1ull << l; l = rdl(nx0, l); }
         while (l < 128u) { lastl = l; m1 |= 1ull << (l - 64u); l = rdl(nx1, l - 64u); }
         while (l < 192u) { lastl = l; m2 |= 1ull << (l - 128u); l = rdl(nx2, l - 128u); }
         while (l < 256u) { lastl = l; m3 |= 1ull << (l - 192u); l = rdl(nx3, l - 192u); }
+        WALK_PRIO_OFF();
         // members are >= 3 bytes apart except the last, so at most 86 of them (< kMaxMem)
         const uint32_t c1 = (uint32_t)__builtin_popcountll(m0), c2 = c1 + (uint32_t)__builtin_popcountll(m1);
         const uint32_t c3 = c2 + (uint32_t)__builtin_popcountll(m2);
@@ -784,7 +794,10 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
                                                       const DecUnit* __restrict__ units, uint32_t nunits,
                                                       uint32_t* __restrict__ blk_out,
                                                       int32_t* __restrict__ blk_status) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[dec::kWaves * dec::kWaveLds];
+#ifndef S3HC_DEC_LDS_PAD
+#define S3HC_DEC_LDS_PAD 0  // diagnostic builds: extra LDS per workgroup to lower occupancy
+#endif
+    __shared__ __attribute__((aligned(16))) uint8_t smem[dec::kWaves * dec::kWaveLds + S3HC_DEC_LDS_PAD];
     const int lane = lane_id();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t u = blockIdx.x * dec::kWaves + wv;
@@ -1083,6 +1096,7 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
         // ---- C: greedy walk over the chunks (scalar); each chunk's hops are stashed in LDS in
         // order, then the sub-block's sequence records are formed 64 hops at a time
         const uint32_t ns_sb = nseq, le_sb = last_end;
+        WALK_PRIO_ON();
 #pragma unroll
         for (uint32_t q = 0; q < kSteps; ++q) {
             const uint32_t base = sb + 64 * q;
@@ -1099,6 +1113,8 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
                 hm |= 1ull << j;
                 r = rdl(nxr, j);
                 if (r & 0x100u) {  // long match: wave-wide forward extension
+                    const uint64_t tx0 = PROF_NOW();
+                    PROF_ADD(epr, 8, 1);
                     const uint32_t wj = rdl(word[q], j);
                     const uint32_t P = base + j;
                     const uint32_t maxf = end_lim - P;
@@ -1124,6 +1140,7 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
                     }
                     flen[q] = (uint32_t)lane == j ? lenf : flen[q];
                     r = j + lenf;
+                    PROF_ADD(epr, 2, PROF_NOW() - tx0);
                 }
                 rend = r;
             }
@@ -1137,6 +1154,7 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
                 nseq += (uint32_t)__builtin_popcountll(hm);
             }
         }
+        WALK_PRIO_OFF();
         const uint64_t tf0 = PROF_NOW();
         wave_sync();
         {
@@ -1172,7 +1190,7 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
     epr[5] = PROF_NOW() - tk0;
     epr[7] = nseq;
     if (lane == 0)
-        for (int q = 0; q < 8; ++q) atomicAdd(&g_prof[16 + q], (unsigned long long)epr[q]);
+        for (int q = 0; q < 9; ++q) atomicAdd(&g_prof[16 + q], (unsigned long long)epr[q]);
 #endif
     if (lane == 0) {
         SegSummary S;

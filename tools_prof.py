@@ -14,8 +14,8 @@ import synth  # noqa: E402
 
 DEC = ["stage", "parse_walk", "window", "seq", "wave_total", "windows", "members", "passes",
        "pend_windows", "stages", "flush", "bytes"]
-ENC = {16: "stage", 17: "cand", 18: "desc", 19: "walk", 20: "flush", 21: "wave_total", 22: "subblocks",
-       23: "hops"}
+ENC = {16: "stage", 17: "cand", 18: "long_ext", 19: "walk", 20: "flush", 21: "wave_total", 22: "subblocks",
+       23: "hops", 24: "long_matches"}
 
 
 def main():
