@@ -859,9 +859,20 @@ constexpr uint32_t kPad = 16;                               // front pad: reads 
 constexpr uint32_t kGIn = kPad + kPrewarm + kGroupSegs * kSeg + 128;  // a group's staged input (+ read-ahead)
 constexpr uint32_t kGThreads = 64 * kGroupSegs;
 constexpr uint32_t kTbl = 1u << kHashLog;
-constexpr uint32_t kSteps = 8;                              // 64-position steps per sub-block
+#ifndef S3HC_STEPS
+#define S3HC_STEPS 8
+#endif
+#ifndef S3HC_ENC_MINWAVES
+#define S3HC_ENC_MINWAVES 1
+#endif
+constexpr uint32_t kSteps = S3HC_STEPS;                     // 64-position steps per sub-block
 constexpr uint32_t kStash = 64 * kSteps / 4;                // hops per sub-block (a hop covers >= 4 bytes)
-constexpr uint32_t kFwd = 19;                               // forward bytes measured per probe (4 + 15)
+#ifndef S3HC_FWD_DW
+#define S3HC_FWD_DW 5
+#endif
+constexpr int kNQ = S3HC_FWD_DW;                            // dwords compared past the first 4 bytes
+constexpr uint32_t kFwd = 3 + 4 * kNQ;                      // forward bytes measured per probe; a probe
+                                                            // reaching kFwd is extended in the walk
 constexpr uint32_t kEmpty = 0xFFFFu;
 }  // namespace enc
 
@@ -929,7 +940,7 @@ __device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* 
 //      or after the greedy position (s_ff1), its word by v_readlane, long matches extended
 //      wave-wide; the chunk's hops then become sequence records lane-parallel.
 // Matches end inside the segment, so segments are independent; k_enc_sizes stitches them.
-__global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __restrict__ src,
+__global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) void k_enc_parse(const uint8_t* __restrict__ src,
                                                               const EncBlock* __restrict__ blocks,
                                                               const uint2* __restrict__ groups, uint32_t ngroups,
                                                               uint32_t nxx, const uint64_t* __restrict__ fsrc_off,
@@ -940,6 +951,10 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
     __shared__ __attribute__((aligned(16))) uint8_t inb_raw[kGIn];
     __shared__ __attribute__((aligned(16))) uint16_t tbl_all[kGroupSegs][kTbl + 8];  // slot kTbl: sink
     __shared__ __attribute__((aligned(16))) uint2 stash_all[kGroupSegs][kStash + 8];  // hops of a sub-block (+ sink)
+#ifdef S3HC_ENC_LDS_PAD  // diagnostic builds: extra LDS per workgroup to lower occupancy
+    __shared__ uint8_t enc_pad[S3HC_ENC_LDS_PAD];
+    if (ngroups == 0xFFFFFFFFu) ((volatile uint8_t*)enc_pad)[threadIdx.x] = 0;
+#endif
     // The first nxx workgroups compute the frames' content xxh32 (they are dispatched first and
     // overlap the match finding; the emitter reads the hashes).
     if (blockIdx.x < nxx) {
@@ -1042,19 +1057,19 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
             const bool tin = (c16 != kEmpty) & (c16 < i);
             const uint32_t ct = tin ? c16 : i;
             const uint32_t a = i >> 2, sh = i & 3, ta = ct >> 2, ts = ct & 3;
-            uint32_t O[5], T[7];
+            uint32_t O[kNQ + 1], T[kNQ + 3];
 #pragma unroll
-            for (int j = 0; j < 5; ++j) O[j] = dw[a + 1 + j];
+            for (int j = 0; j < kNQ + 1; ++j) O[j] = dw[a + 1 + j];
 #pragma unroll
-            for (int j = 0; j < 7; ++j) T[j] = dw[(int)ta - 1 + j];
-            uint32_t Q[5];  // Q[k] = bytes [P+4k, P+4k+4)
+            for (int j = 0; j < kNQ + 3; ++j) T[j] = dw[(int)ta - 1 + j];
+            uint32_t Q[kNQ + 1];  // Q[k] = bytes [P+4k, P+4k+4)
             Q[0] = v;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) Q[j + 1] = __builtin_amdgcn_alignbyte(O[j + 1], O[j], sh);
+            for (int j = 0; j < kNQ; ++j) Q[j + 1] = __builtin_amdgcn_alignbyte(O[j + 1], O[j], sh);
             const uint32_t maxf = end_lim - P;  // >= 4 for P <= smax
-            uint32_t lt = 20u;
+            uint32_t lt = kFwd + 1u;
 #pragma unroll
-            for (int j = 3; j >= 0; --j) {
+            for (int j = kNQ - 1; j >= 0; --j) {
                 const uint32_t dt = Q[j + 1] ^ __builtin_amdgcn_alignbyte(T[j + 3], T[j + 2], ts);
                 lt = dt ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dt) >> 3) : lt;
             }
@@ -1070,9 +1085,9 @@ __global__ __launch_bounds__(enc::kGThreads) void k_enc_parse(const uint8_t* __r
                 const uint32_t df = (e1 & (i >= 1)) ? 1u : ((e2 & (i >= 2)) ? 2u : ((e3 & (i >= 3)) ? 3u : ((e4 & (i >= 4)) ? 4u : 0u)));
                 gf = valid & (df != 0);
                 const uint32_t fs = (4u - df) & 3u;
-                uint32_t lf = 20u;
+                uint32_t lf = kFwd + 1u;
 #pragma unroll
-                for (int j = 3; j >= 0; --j) {
+                for (int j = kNQ - 1; j >= 0; --j) {
                     const uint32_t dfw = Q[j + 1] ^ __builtin_amdgcn_alignbyte(Q[j + 1], Q[j], fs);
                     lf = dfw ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dfw) >> 3) : lf;
                 }

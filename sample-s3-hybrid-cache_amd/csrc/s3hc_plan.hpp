@@ -26,7 +26,10 @@ constexpr uint32_t kSeg = 4096;          // bytes of input per match-finding wav
 constexpr uint32_t kPrewarm = S3HC_PREWARM;  // bytes before a segment inserted into its hash table
 constexpr uint32_t kHashLog = S3HC_HASHLOG;  // per-wave hash table: 2^11 x u16 positions
 constexpr uint32_t kMaxSeqPerSeg = kSeg / 4 + 1;
-constexpr uint32_t kGroupSegs = 8;       // segments (waves) per match-finding workgroup
+#ifndef S3HC_GROUP_SEGS
+#define S3HC_GROUP_SEGS 8
+#endif
+constexpr uint32_t kGroupSegs = S3HC_GROUP_SEGS;  // segments (waves) per match-finding workgroup
 
 enum : uint32_t {
     EB_STORE = 1,        // write this block stored (store-mode frame or caller decision)
