@@ -170,6 +170,47 @@ void s3hc_handler_record_object(s3hc_handler* h, int compressed);
 /* is_denylisted_extension (:252-308). */
 int s3hc_is_denylisted_extension(const char* path);
 
+/* ---- batched incremental writers + cross-request aggregator ---------------- */
+/* IncrementalRangeWriter (disk_cache.rs:262-305) with flush_batch (:1820-1870) routed
+ * through an aggregator that encodes the full batches of many writers in one GPU launch
+ * (SURVEY.md §8(f) row 2). Every batch is one frame, byte-identical to s3hc_compress_frame
+ * (compression enabled) or s3hc_store_mode_frame (disabled) of the same bytes; a writer's
+ * frames reach its sink in order (the reference's file.write_all, :1858). */
+typedef struct s3hc_aggregator s3hc_aggregator;
+typedef struct s3hc_writer s3hc_writer;
+/* Receives one frame; nonzero return = write failure (the writer's next call fails). */
+typedef int (*s3hc_frame_sink)(void* user, const uint8_t* frame, size_t n);
+/* batch_size: cache.compression_batch_size (config.rs:990-995; the config layer bounds it to
+ * 64 KiB..16 MiB, config.rs:1617-1627, the writer itself takes any size). flush_batches = 1
+ * encodes every batch as soon as it fills (the reference's inline flush_batch). Queued batches are encoded together once flush_bytes bytes or
+ * flush_batches batches are queued (0 = only on commit / s3hc_aggregator_flush).
+ * stats: optional handler whose shared counters get record_batch_bytes per frame and
+ * record_object per committed range (:1865-1867, :2053). */
+int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t flush_bytes, uint32_t flush_batches,
+                           s3hc_handler* stats, s3hc_aggregator** out);
+int s3hc_aggregator_flush(s3hc_aggregator* a);
+/* Encode launches and batches encoded so far. */
+void s3hc_aggregator_counters(const s3hc_aggregator* a, uint64_t* launches, uint64_t* batches);
+void s3hc_aggregator_destroy(s3hc_aggregator* a);
+/* begin_incremental_range_write (:1716-1778): start > end -> S3HC_INVALID_ARG. */
+int s3hc_writer_begin(s3hc_aggregator* a, uint64_t start, uint64_t end, int compression_enabled,
+                      s3hc_frame_sink sink, void* user, s3hc_writer** out);
+/* write_range_chunk (:1798-1810): a batch is flushed once it holds >= batch_size bytes.
+ * A failure of an earlier queued batch (encode or sink) is reported here. */
+int s3hc_writer_write(s3hc_writer* w, const uint8_t* chunk, size_t n);
+size_t s3hc_writer_batch_buf_len(const s3hc_writer* w);                 /* batch_buf_len (:300-304) */
+uint64_t s3hc_writer_bytes_written(const s3hc_writer* w);
+uint64_t s3hc_writer_compressed_bytes_written(const s3hc_writer* w);
+/* finalize_incremental_range (:1968-2090): flushes the residual batch, waits for the
+ * writer's frames, checks bytes_written == end - start + 1 (min_commit_ratio >= 0 salvages a
+ * prefix >= ratio * expected as a clamped range; < 0 = exact only). spec_out = {start, end,
+ * compressed_size, uncompressed_size} (RangeSpec, cache_types.rs:472-508). Frees w. */
+int s3hc_writer_commit(s3hc_writer* w, double min_commit_ratio, uint64_t spec_out[4]);
+/* abort_incremental_range (:2093-2116): queued batches are dropped undelivered. Frees w. */
+void s3hc_writer_abort(s3hc_writer* w);
+/* Message of the last failing writer/aggregator call on this thread. */
+const char* s3hc_writer_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,377 @@
+// s3hc_writer.cpp — batched incremental range writers over a cross-request batch aggregator.
+//
+// Mirrors IncrementalRangeWriter (src/disk_cache.rs:262-305) and its life cycle:
+//   begin_incremental_range_write  (disk_cache.rs:1716-1778)  -> s3hc_writer_begin
+//   write_range_chunk              (disk_cache.rs:1798-1810)  -> s3hc_writer_write
+//   flush_batch                    (disk_cache.rs:1820-1870)  -> queued on the aggregator
+//   finalize_incremental_range     (disk_cache.rs:1968-2090)  -> s3hc_writer_commit
+//   abort_incremental_range        (disk_cache.rs:2093-2116)  -> s3hc_writer_abort
+// The reference encodes every batch inline on the writer's own spawn_blocking thread, one
+// lz4_flex FrameEncoder per ~1 MiB batch. Here a full batch is queued instead, and the
+// aggregator encodes the queued batches of all writers together in one GPU launch (one
+// s3hc_plan_encode item per batch). Each batch still becomes exactly
+// one frame — compressed (lz4_flex Auto layout) when the writer has compression enabled,
+// store-mode otherwise — byte-identical to s3hc_compress_frame / s3hc_store_mode_frame of the
+// same bytes, and each writer's frames reach its sink in batch order (the reference's
+// file.write_all). Batching semantics are unchanged: a batch is flushed when it reaches
+// batch_size (>=), the residual at commit, nothing when empty; bytes_written counts every
+// chunk, compressed_bytes_written counts delivered frames, and the shared handler stats get
+// record_batch_bytes per frame and record_object per committed range.
+//
+// Differences forced by aggregation (documented in DESIGN.md): an encode or sink failure of a
+// queued batch is reported at the writer's next write/commit call instead of by the write that
+// filled the batch; sinks may be called from whichever thread runs the aggregated flush.
+//
+// This file uses only the public C ABI (include/s3hc_lz4.h), like disk_cache.rs uses
+// compression.rs: it is caller-side code, not part of the codec.
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "s3hc_lz4.h"
+
+namespace {
+
+struct Batch {
+    s3hc_writer* w;
+    std::vector<uint8_t> data;
+    uint8_t mode;  // 0 compress, 1 store-mode
+};
+
+// Device + pinned host staging reused across flushes (grown on demand).
+struct Staging {
+    void* h_in = nullptr;
+    size_t h_in_cap = 0;
+    void* h_out = nullptr;
+    size_t h_out_cap = 0;
+    void* h_meta = nullptr;
+    size_t h_meta_cap = 0;
+    void* d_in = nullptr;
+    size_t d_in_cap = 0;
+    void* d_out = nullptr;
+    size_t d_out_cap = 0;
+    void* d_meta = nullptr;
+    size_t d_meta_cap = 0;
+};
+
+int grow_host(s3hc_ctx* ctx, void** p, size_t* cap, size_t n) {
+    if (n <= *cap) return S3HC_OK;
+    if (*p) s3hc_host_free(ctx, *p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t want = std::max<size_t>(n, 1 << 20);
+    int rc = s3hc_host_alloc(ctx, want, p);
+    if (rc == S3HC_OK) *cap = want;
+    return rc;
+}
+int grow_dev(s3hc_ctx* ctx, void** p, size_t* cap, size_t n) {
+    if (n <= *cap) return S3HC_OK;
+    if (*p) s3hc_dev_free(ctx, *p);
+    *p = nullptr;
+    *cap = 0;
+    const size_t want = std::max<size_t>(n, 1 << 20);
+    int rc = s3hc_dev_alloc(ctx, want, p);
+    if (rc == S3HC_OK) *cap = want;
+    return rc;
+}
+
+}  // namespace
+
+struct s3hc_aggregator {
+    s3hc_ctx* ctx;
+    size_t batch_size;
+    size_t flush_bytes;
+    uint32_t flush_batches;
+    s3hc_handler* stats;     // optional shared counters (the writers' Arc<CompressionStatsAtomic>)
+    void* queue = nullptr;   // the aggregator's HIP queue
+    std::mutex mu;           // guards pending / pending_bytes / counters
+    std::mutex flush_mu;     // one aggregated flush at a time (keeps per-writer frame order)
+    std::deque<Batch> pending;
+    size_t pending_bytes = 0;
+    uint64_t launches = 0;
+    uint64_t batches_encoded = 0;
+    Staging stg;
+};
+
+struct s3hc_writer {
+    s3hc_aggregator* agg;
+    s3hc_frame_sink sink;
+    void* user;
+    uint64_t start, end;
+    bool compression_enabled;
+    std::vector<uint8_t> batch_buf;
+    uint64_t bytes_written = 0;             // every chunk (uncompressed)
+    uint64_t compressed_bytes_written = 0;  // delivered frames
+    uint32_t queued = 0;                    // batches queued and not yet delivered
+    int error = S3HC_OK;                    // sticky: first failure of a queued batch
+    std::string error_msg;
+};
+
+static thread_local std::string g_werr;
+extern "C" const char* s3hc_writer_last_error(void) { return g_werr.c_str(); }
+static int werr(int code, const std::string& m) {
+    g_werr = m;
+    return code;
+}
+
+// Encode every queued batch in one launch and deliver the frames in queue order.
+// Caller holds flush_mu.
+static int aggregated_flush(s3hc_aggregator* a) {
+    std::deque<Batch> work;
+    {
+        std::lock_guard<std::mutex> g(a->mu);
+        work.swap(a->pending);
+        a->pending_bytes = 0;
+    }
+    if (work.empty()) return S3HC_OK;
+    const uint32_t n = (uint32_t)work.size();
+    std::vector<uint64_t> off(n);
+    std::vector<uint32_t> len(n);
+    std::vector<uint8_t> mode(n);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        off[i] = total;
+        len[i] = (uint32_t)work[i].data.size();
+        mode[i] = work[i].mode;
+        total += len[i];
+    }
+    auto fail_all = [&](int rc, const char* what) {
+        const std::string msg = std::string(what) + ": " + s3hc_last_error();
+        std::lock_guard<std::mutex> g(a->mu);
+        for (auto& b : work) {
+            if (!b.w->error) { b.w->error = rc; b.w->error_msg = msg; }
+            b.w->queued--;
+        }
+        return werr(rc, msg);
+    };
+    s3hc_ctx* ctx = a->ctx;
+    Staging& S = a->stg;
+    int rc = grow_host(ctx, &S.h_in, &S.h_in_cap, total + 64);
+    if (!rc) rc = grow_dev(ctx, &S.d_in, &S.d_in_cap, total + 64);
+    if (rc) return fail_all(rc, "staging allocation");
+    for (uint32_t i = 0; i < n; ++i) memcpy((uint8_t*)S.h_in + off[i], work[i].data.data(), len[i]);
+    s3hc_plan* plan = nullptr;
+    rc = s3hc_plan_encode(ctx, off.data(), len.data(), mode.data(), n, &plan);
+    if (rc) return fail_all(rc, "plan");
+    const uint64_t bound = s3hc_plan_dst_bound(plan);
+    rc = grow_dev(ctx, &S.d_out, &S.d_out_cap, bound + 64);
+    if (!rc) rc = grow_host(ctx, &S.h_out, &S.h_out_cap, bound + 64);
+    if (!rc) rc = grow_dev(ctx, &S.d_meta, &S.d_meta_cap, 12ull * n + 64);
+    if (!rc) rc = grow_host(ctx, &S.h_meta, &S.h_meta_cap, 12ull * n + 64);
+    uint64_t* d_ioff = (uint64_t*)S.d_meta;
+    uint32_t* d_ilen = (uint32_t*)((uint8_t*)S.d_meta + 8ull * n);
+    if (!rc && total) rc = s3hc_memcpy_async(ctx, S.d_in, S.h_in, total, 1, a->queue);
+    if (!rc) rc = s3hc_encode_dev(ctx, plan, (const uint8_t*)S.d_in, (uint8_t*)S.d_out, S.d_out_cap, d_ioff, d_ilen, a->queue);
+    if (!rc) rc = s3hc_memcpy_async(ctx, S.h_meta, S.d_meta, 12ull * n, 2, a->queue);
+    if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
+    s3hc_plan_free(plan);
+    if (rc) return fail_all(rc, "encode");
+    const uint64_t* io = (const uint64_t*)S.h_meta;
+    const uint32_t* il = (const uint32_t*)((const uint8_t*)S.h_meta + 8ull * n);
+    const uint64_t frames = io[n - 1] + il[n - 1];  // frames are packed in item order
+    rc = s3hc_memcpy_async(ctx, S.h_out, S.d_out, frames, 2, a->queue);
+    if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
+    if (rc) return fail_all(rc, "frame copy");
+    {
+        std::lock_guard<std::mutex> g(a->mu);
+        a->launches++;
+        a->batches_encoded += n;
+    }
+    // deliver in queue order: each writer's frames keep their batch order
+    for (uint32_t i = 0; i < n; ++i) {
+        s3hc_writer* w = work[i].w;
+        const uint8_t* fr = (const uint8_t*)S.h_out + io[i];
+        int src = S3HC_OK;
+        if (!w->error) {
+            if (w->sink && w->sink(w->user, fr, il[i]) != 0) {
+                src = S3HC_INVALID_ARG;
+            } else {
+                w->compressed_bytes_written += il[i];
+                if (a->stats) s3hc_handler_record_batch_bytes(a->stats, len[i], il[i]);
+            }
+        }
+        std::lock_guard<std::mutex> g(a->mu);
+        if (src && !w->error) { w->error = src; w->error_msg = "frame sink failed (write_all)"; }
+        w->queued--;
+    }
+    return S3HC_OK;
+}
+
+static int maybe_flush(s3hc_aggregator* a, bool force) {
+    bool go = force;
+    {
+        std::lock_guard<std::mutex> g(a->mu);
+        if (a->pending.empty()) return S3HC_OK;
+        if (!go) go = (a->flush_bytes && a->pending_bytes >= a->flush_bytes) ||
+                      (a->flush_batches && a->pending.size() >= a->flush_batches);
+    }
+    if (!go) return S3HC_OK;
+    std::lock_guard<std::mutex> f(a->flush_mu);
+    return aggregated_flush(a);
+}
+
+// flush_batch (disk_cache.rs:1820-1870): no-op on an empty buffer; otherwise the batch
+// becomes one queued frame.
+static void queue_batch(s3hc_writer* w) {
+    if (w->batch_buf.empty()) return;
+    s3hc_aggregator* a = w->agg;
+    Batch b;
+    b.w = w;
+    b.mode = w->compression_enabled ? 0 : 1;
+    b.data.swap(w->batch_buf);
+    w->batch_buf.clear();
+    w->batch_buf.reserve(a->batch_size);
+    std::lock_guard<std::mutex> g(a->mu);
+    a->pending_bytes += b.data.size();
+    w->queued++;
+    a->pending.push_back(std::move(b));
+}
+
+extern "C" int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t flush_bytes, uint32_t flush_batches,
+                                      s3hc_handler* stats, s3hc_aggregator** out) {
+    if (!ctx || !out) return werr(S3HC_INVALID_ARG, "bad arguments");
+    *out = nullptr;
+    // DiskCacheManager takes any batch size (its tests use 4-8 KiB); the 64 KiB..16 MiB bounds
+    // belong to Config::validate (config.rs:1617-1627), the caller's configuration layer.
+    if (batch_size == 0 || batch_size > 0xFFFFFFFFull / 2) return werr(S3HC_INVALID_ARG, "batch_size out of range");
+    s3hc_aggregator* a = new s3hc_aggregator;
+    a->ctx = ctx;
+    a->batch_size = batch_size;
+    a->flush_bytes = flush_bytes;
+    a->flush_batches = flush_batches;
+    a->stats = stats;
+    int rc = s3hc_queue_create(ctx, &a->queue);
+    if (rc) {
+        delete a;
+        return werr(rc, std::string("queue: ") + s3hc_last_error());
+    }
+    *out = a;
+    return S3HC_OK;
+}
+
+extern "C" int s3hc_aggregator_flush(s3hc_aggregator* a) {
+    if (!a) return werr(S3HC_INVALID_ARG, "bad arguments");
+    return maybe_flush(a, true);
+}
+
+extern "C" void s3hc_aggregator_counters(const s3hc_aggregator* a, uint64_t* launches, uint64_t* batches) {
+    if (!a) return;
+    std::lock_guard<std::mutex> g(const_cast<s3hc_aggregator*>(a)->mu);
+    if (launches) *launches = a->launches;
+    if (batches) *batches = a->batches_encoded;
+}
+
+extern "C" void s3hc_aggregator_destroy(s3hc_aggregator* a) {
+    if (!a) return;
+    {
+        std::lock_guard<std::mutex> f(a->flush_mu);
+        (void)aggregated_flush(a);
+    }
+    s3hc_ctx* ctx = a->ctx;
+    Staging& S = a->stg;
+    if (S.h_in) s3hc_host_free(ctx, S.h_in);
+    if (S.h_out) s3hc_host_free(ctx, S.h_out);
+    if (S.h_meta) s3hc_host_free(ctx, S.h_meta);
+    if (S.d_in) s3hc_dev_free(ctx, S.d_in);
+    if (S.d_out) s3hc_dev_free(ctx, S.d_out);
+    if (S.d_meta) s3hc_dev_free(ctx, S.d_meta);
+    if (a->queue) s3hc_queue_destroy(ctx, a->queue);
+    delete a;
+}
+
+extern "C" int s3hc_writer_begin(s3hc_aggregator* a, uint64_t start, uint64_t end, int compression_enabled,
+                                 s3hc_frame_sink sink, void* user, s3hc_writer** out) {
+    if (!a || !out) return werr(S3HC_INVALID_ARG, "bad arguments");
+    *out = nullptr;
+    if (start > end) return werr(S3HC_INVALID_ARG, "Invalid range: start > end");  // disk_cache.rs:1723-1728
+    s3hc_writer* w = new s3hc_writer;
+    w->agg = a;
+    w->sink = sink;
+    w->user = user;
+    w->start = start;
+    w->end = end;
+    w->compression_enabled = compression_enabled != 0;
+    w->batch_buf.reserve(a->batch_size);
+    *out = w;
+    return S3HC_OK;
+}
+
+extern "C" int s3hc_writer_write(s3hc_writer* w, const uint8_t* chunk, size_t n) {
+    if (!w || (!chunk && n)) return werr(S3HC_INVALID_ARG, "bad arguments");
+    if (w->error) return werr(w->error, w->error_msg);
+    if (n == 0) return S3HC_OK;                    // disk_cache.rs:1799-1801
+    w->bytes_written += n;
+    w->batch_buf.insert(w->batch_buf.end(), chunk, chunk + n);
+    if (w->batch_buf.size() >= w->agg->batch_size) {  // >= flushes (disk_cache.rs:1806)
+        queue_batch(w);
+        int rc = maybe_flush(w->agg, false);
+        if (rc && !w->error) return rc;
+    }
+    return w->error ? werr(w->error, w->error_msg) : S3HC_OK;
+}
+
+extern "C" size_t s3hc_writer_batch_buf_len(const s3hc_writer* w) { return w ? w->batch_buf.size() : 0; }
+extern "C" uint64_t s3hc_writer_bytes_written(const s3hc_writer* w) { return w ? w->bytes_written : 0; }
+extern "C" uint64_t s3hc_writer_compressed_bytes_written(const s3hc_writer* w) {
+    return w ? w->compressed_bytes_written : 0;
+}
+
+// Wait until every queued batch of w has been delivered (flushes as needed).
+static int drain(s3hc_writer* w) {
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> g(w->agg->mu);
+            if (w->queued == 0) return S3HC_OK;
+        }
+        int rc = maybe_flush(w->agg, true);  // serialized by flush_mu: waits for a flush in flight
+        if (rc) return rc;
+    }
+}
+
+extern "C" int s3hc_writer_commit(s3hc_writer* w, double min_commit_ratio, uint64_t spec_out[4]) {
+    if (!w) return werr(S3HC_INVALID_ARG, "bad arguments");
+    // finalize_incremental_range: residual batch first (disk_cache.rs:1981-1986)
+    queue_batch(w);
+    int rc = drain(w);
+    if (!rc && w->error) rc = werr(w->error, w->error_msg);
+    if (rc) {
+        delete w;  // the reference removes the .tmp file; the caller discards what its sink wrote
+        return rc;
+    }
+    uint64_t end = w->end;
+    const uint64_t expected = w->end - w->start + 1;
+    if (w->bytes_written != expected) {
+        // partial-prefix salvage (disk_cache.rs:1988-2023): read path passes a ratio; < 0 = exact only
+        const bool salvage = min_commit_ratio >= 0.0 && w->bytes_written > 0 && w->bytes_written < expected &&
+                             (double)w->bytes_written >= min_commit_ratio * (double)expected;
+        if (!salvage) {
+            char m[160];
+            snprintf(m, sizeof m, "Incremental write size mismatch: expected %llu bytes, got %llu",
+                     (unsigned long long)expected, (unsigned long long)w->bytes_written);
+            delete w;
+            return werr(S3HC_INVALID_ARG, m);
+        }
+        end = w->start + w->bytes_written - 1;
+    }
+    if (w->agg->stats) s3hc_handler_record_object(w->agg->stats, w->compression_enabled ? 1 : 0);  // :2053
+    if (spec_out) {  // RangeSpec::new(start, end, path, Lz4, compressed, uncompressed) (disk_cache.rs:2080-2087)
+        spec_out[0] = w->start;
+        spec_out[1] = end;
+        spec_out[2] = w->compressed_bytes_written;
+        spec_out[3] = w->bytes_written;
+    }
+    delete w;
+    return S3HC_OK;
+}
+
+extern "C" void s3hc_writer_abort(s3hc_writer* w) {
+    if (!w) return;
+    // queued batches still reference w: let them drain (their frames go to the sink, which the
+    // caller is discarding together with the .tmp file) before freeing
+    w->error = w->error ? w->error : S3HC_INVALID_ARG;
+    (void)drain(w);
+    delete w;
+}

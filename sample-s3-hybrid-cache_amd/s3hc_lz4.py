@@ -102,6 +102,18 @@ def _load():
         "s3hc_queue_destroy": (i32, [vp, vp]),
         "s3hc_queue_sync": (i32, [vp, vp]),
         "s3hc_memcpy_async": (i32, [vp, vp, vp, sz, i32, vp]),
+        "s3hc_aggregator_create": (i32, [vp, sz, sz, u32, vp, ctypes.POINTER(vp)]),
+        "s3hc_aggregator_flush": (i32, [vp]),
+        "s3hc_aggregator_counters": (None, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "s3hc_aggregator_destroy": (None, [vp]),
+        "s3hc_writer_begin": (i32, [vp, u64, u64, i32, vp, vp, ctypes.POINTER(vp)]),
+        "s3hc_writer_write": (i32, [vp, u8p, sz]),
+        "s3hc_writer_batch_buf_len": (sz, [vp]),
+        "s3hc_writer_bytes_written": (u64, [vp]),
+        "s3hc_writer_compressed_bytes_written": (u64, [vp]),
+        "s3hc_writer_commit": (i32, [vp, ctypes.c_double, ctypes.POINTER(u64)]),
+        "s3hc_writer_abort": (None, [vp]),
+        "s3hc_writer_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -520,3 +532,108 @@ class CompressionHandler:
 
     def record_object(self, compressed: bool):
         lib.s3hc_handler_record_object(self.h, 1 if compressed else 0)
+
+
+# ---------------------------------------------------------------------------------------------
+# Batched incremental writers (IncrementalRangeWriter, disk_cache.rs:262-305, 1716-2116) over the
+# cross-request aggregator (one GPU launch for the full batches of many writers).
+FRAME_SINK = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t)
+
+
+def _wcheck(rc: int):
+    if rc != S3HC_OK:
+        raise CodecError(rc, (lib.s3hc_writer_last_error() or b"").decode(errors="replace"))
+
+
+@dataclass
+class RangeSpec:  # cache_types.rs:472-508 (codec fields)
+    start: int
+    end: int
+    compressed_size: int
+    uncompressed_size: int
+
+
+class BatchAggregator:
+    """Coalesces the flush_batch calls of many writers into one encode launch."""
+
+    def __init__(self, eng: Engine, batch_size: int = 1 << 20, flush_bytes: int = 0, flush_batches: int = 0,
+                 stats: "CompressionHandler | None" = None):
+        h = ctypes.c_void_p()
+        _wcheck(lib.s3hc_aggregator_create(eng.h, batch_size, flush_bytes, flush_batches,
+                                           stats.h if stats is not None else None, ctypes.byref(h)))
+        self.h, self.eng, self.stats = h, eng, stats
+
+    def flush(self):
+        _wcheck(lib.s3hc_aggregator_flush(self.h))
+
+    def counters(self) -> tuple[int, int]:
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        lib.s3hc_aggregator_counters(self.h, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
+    def begin(self, start: int, end: int, compression_enabled: bool, sink=None) -> "IncrementalRangeWriter":
+        return IncrementalRangeWriter(self, start, end, compression_enabled, sink)
+
+    def close(self):
+        if self.h:
+            lib.s3hc_aggregator_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class IncrementalRangeWriter:
+    """begin_incremental_range_write / write_range_chunk / commit / abort. Frames go to `sink`
+    (callable(bytes) -> None, the reference's .tmp file) or, by default, to self.file."""
+
+    def __init__(self, agg: BatchAggregator, start: int, end: int, compression_enabled: bool, sink=None):
+        self.agg = agg
+        self.file = bytearray()
+        self._user_sink = sink
+
+        def _sink(_user, frame, n):
+            try:
+                b = ctypes.string_at(frame, n)
+                if self._user_sink is not None:
+                    self._user_sink(b)
+                else:
+                    self.file += b
+                return 0
+            except Exception:
+                return 1
+
+        self._cb = FRAME_SINK(_sink)  # keep alive while the writer exists
+        h = ctypes.c_void_p()
+        _wcheck(lib.s3hc_writer_begin(agg.h, start, end, 1 if compression_enabled else 0,
+                                      ctypes.cast(self._cb, ctypes.c_void_p), None, ctypes.byref(h)))
+        self.h = h
+
+    def write(self, chunk):
+        p, keep = _ptr(chunk)
+        _wcheck(lib.s3hc_writer_write(self.h, p, len(keep)))
+
+    def batch_buf_len(self) -> int:
+        return lib.s3hc_writer_batch_buf_len(self.h)
+
+    @property
+    def bytes_written(self) -> int:
+        return lib.s3hc_writer_bytes_written(self.h)
+
+    @property
+    def compressed_bytes_written(self) -> int:
+        return lib.s3hc_writer_compressed_bytes_written(self.h)
+
+    def commit(self, min_commit_ratio: float | None = None) -> RangeSpec:
+        spec = (ctypes.c_uint64 * 4)()
+        h, self.h = self.h, None
+        _wcheck(lib.s3hc_writer_commit(h, -1.0 if min_commit_ratio is None else min_commit_ratio, spec))
+        return RangeSpec(*list(spec))
+
+    def abort(self):
+        h, self.h = self.h, None
+        if h:
+            lib.s3hc_writer_abort(h)
