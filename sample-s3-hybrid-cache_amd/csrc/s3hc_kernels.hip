@@ -387,7 +387,8 @@ __device__ __forceinline__ int dec_seq(DecWave& w, const uint8_t* in, uint32_t l
 // round trips per 256 bytes, almost no scalar work.
 __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM0, bool isM1, uint32_t orel0,
                                                 uint32_t orel1, uint32_t sl0, uint32_t sl1, uint32_t ll0,
-                                                uint32_t ll1, uint32_t pkB0, uint32_t pkB1) {
+                                                uint32_t ll1, uint32_t off0, uint32_t off1, uint32_t lr0,
+                                                uint32_t lr1) {
     using namespace dec;
     const int lane = w.lane;
     uint8_t* marks = w.marks;
@@ -397,12 +398,22 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
     const uint32_t xbase = upos - a0;
     const uint32_t np = (S + a0 + 255u) >> 8;
     // member m starts at window byte orel: marks[orel + a0] = m + 1 (marks are zero between
-    // windows: each pass clears the dwords it reads); the member table holds
-    // (orel | ll << 16, off | literal ring index << 16)
+    // windows: each pass clears the dwords it reads). The member table holds
+    // (M | E << 16, L | off << 16): M = window byte where the member's match starts (orel + ll),
+    // E = M + off (saturated; bytes at or past E copy an overlapping match), L = literal ring
+    // index minus orel (window byte t of a literal run is cin[(L + t) & kCmask]).
     *((isM0 && sl0) ? marks + orel0 + a0 : w.sink + lane) = (uint8_t)(lane + 1);
     *((isM1 && sl1) ? marks + orel1 + a0 : w.sink + lane) = (uint8_t)(lane + 65);
-    w.mtab[lane] = make_uint2(orel0 | (ll0 << 16), pkB0);
-    w.mtab[64 + lane] = make_uint2(orel1 | (ll1 << 16), pkB1);
+    auto entry = [](uint32_t orel, uint32_t ll, uint32_t off, uint32_t lr) -> uint2 {
+        const uint32_t M = orel + ll;
+        const uint32_t E = M + off < 0xFFFFu ? M + off : 0xFFFFu;
+        return make_uint2(M | (E << 16), ((lr - orel) & 0xFFFFu) | (off << 16));
+    };
+    w.mtab[lane] = entry(orel0, ll0, off0, lr0);
+    w.mtab[64 + lane] = entry(orel1, ll1, off1, lr1);
+    // a source older than the ring (read back from HBM) needs a match offset above kRing - S
+    const bool far = (upos > kRing - S) &&
+                     __ballot((isM0 && sl0 > ll0 && off0 > kRing - S) || (isM1 && sl1 > ll1 && off1 > kRing - S));
     wave_sync();
     uint32_t carry = 0;
     for (uint32_t p = 0; p < np; ++p) {
@@ -425,38 +436,38 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
         o[3] = umax32(ex, c3);
         const uint2 fA = w.mtab[(o[0] - 1u) & 127u], fB = w.mtab[(o[3] - 1u) & 127u];
         // ---- sources
-        uint32_t y[4], dd[4], mlit[4], ee[4], mf[4];
+        uint32_t y[4], ci[4], mst[4], mf[4];
         bool lit[4], ok[4], wrap[4];
         bool anywrap = false;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const bool useB = o[j] == o[3];
             const uint32_t fx = useB ? fB.x : fA.x, fy = useB ? fB.y : fA.y;
-            const uint32_t mo = fx & 0xFFFFu, mll = fx >> 16, moff = fy & 0xFFFFu;
-            mlit[j] = fy >> 16;
-            ok[j] = t0 + j < S;
-            dd[j] = t0 + j - mo;
-            lit[j] = dd[j] < mll;
-            ee[j] = dd[j] - mll;              // position inside the match
-            mf[j] = moff;
-            wrap[j] = ok[j] & !lit[j] & (ee[j] >= moff);
+            const uint32_t t = t0 + j;        // window byte
+            mst[j] = fx & 0xFFFFu;            // match start of the owner
+            mf[j] = fy >> 16;                 // match offset
+            ok[j] = t < S;
+            lit[j] = t < mst[j];
+            wrap[j] = ok[j] & (t >= (fx >> 16));  // inside an overlapping match
             anywrap |= wrap[j];
-            y[j] = X + j - moff;              // non-overlapping source
+            ci[j] = (fy + t) & kCmask;        // literal ring index (carries out of the low half drop)
+            y[j] = X + j - mf[j];             // non-overlapping source
         }
         if (__ballot(anywrap)) {
             // overlapping matches (period moff): the source is the byte ee mod moff of the first
             // period. ee < kWin and moff < ee, so ee * rcp(moff) is within 2^-11 of ee / moff and
             // its truncation is exact or one short (at exact multiples), fixed by one compare.
-            const float rA = __builtin_amdgcn_rcpf((float)(fA.y & 0xFFFFu));
-            const float rB = __builtin_amdgcn_rcpf((float)(fB.y & 0xFFFFu));
+            const float rA = __builtin_amdgcn_rcpf((float)(fA.y >> 16));
+            const float rB = __builtin_amdgcn_rcpf((float)(fB.y >> 16));
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 if (wrap[j]) {
+                    const uint32_t ee = t0 + j - mst[j];  // position inside the match
                     const float rf = o[j] == o[3] ? rB : rA;
-                    const uint32_t qt = (uint32_t)((float)ee[j] * rf);
-                    uint32_t rm = ee[j] - __umul24(qt, mf[j]);
+                    const uint32_t qt = (uint32_t)((float)ee * rf);
+                    uint32_t rm = ee - __umul24(qt, mf[j]);
                     rm = rm >= mf[j] ? rm - mf[j] : rm;
-                    y[j] = X + j - ee[j] - mf[j] + rm;
+                    y[j] = X + j - ee - mf[j] + rm;
                 }
             }
         }
@@ -464,7 +475,7 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
         uint32_t v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint8_t* a = lit[j] ? w.cin + ((mlit[j] + dd[j]) & kCmask) : w.ring + (y[j] & kMask);
+            const uint8_t* a = lit[j] ? w.cin + ci[j] : w.ring + (y[j] & kMask);
             v[j] = *a;
         }
         bool pnd[4];
@@ -479,10 +490,7 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
         }
         const uint32_t val = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
         ((uint32_t*)w.ring)[(X & kMask) >> 2] = (val & vm) | (oldw & ~vm);
-        const uint32_t r0 = pnd[0] ? y[0] - upos : 0xFFFFu, r1 = pnd[1] ? y[1] - upos : 0xFFFFu;
-        const uint32_t r2 = pnd[2] ? y[2] - upos : 0xFFFFu, r3 = pnd[3] ? y[3] - upos : 0xFFFFu;
-        *(uint2*)(refs + 4u * (uint32_t)lane) = make_uint2(r0 | (r1 << 16), r2 | (r3 << 16));  // pass-local
-        if (upos > kRing - S) {
+        if (far) {
             // sources older than the ring are read back from HBM (already flushed); kept apart
             // so the common path never waits on the wave's outstanding flush stores
             bool old[4], anyold = false;
@@ -499,7 +507,11 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
         }
         if (__ballot(anypnd)) {
             // sources inside this pass: follow refs through pending bytes (bytes of earlier
-            // passes and bytes with refs == 0xFFFF are final in the ring)
+            // passes and bytes with refs == 0xFFFF are final in the ring); refs are pass-local
+            // and written only when some byte of the pass needs them
+            const uint32_t r0 = pnd[0] ? y[0] - upos : 0xFFFFu, r1 = pnd[1] ? y[1] - upos : 0xFFFFu;
+            const uint32_t r2 = pnd[2] ? y[2] - upos : 0xFFFFu, r3 = pnd[3] ? y[3] - upos : 0xFFFFu;
+            *(uint2*)(refs + 4u * (uint32_t)lane) = make_uint2(r0 | (r1 << 16), r2 | (r3 << 16));
             wave_sync();
             uint32_t z[4];
 #pragma unroll
@@ -740,8 +752,8 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
                 const uint64_t bad1 = __ballot(isM1 && st1 != S3HC_OK);
                 if (bad0) return (int)rdl((uint32_t)st0, (uint32_t)__builtin_ctzll(bad0));
                 if (bad1) return (int)rdl((uint32_t)st1, (uint32_t)__builtin_ctzll(bad1));
-                dec_window_exec(w, S, isM0, isM1, orel0, orel1, sl0, sl1, t0.ll, t1.ll,
-                                t0.off | (((t0.lit + mis) & kCmask) << 16), t1.off | (((t1.lit + mis) & kCmask) << 16));
+                dec_window_exec(w, S, isM0, isM1, orel0, orel1, sl0, sl1, t0.ll, t1.ll, t0.off, t1.off,
+                                (t0.lit + mis) & kCmask, (t1.lit + mis) & kCmask);
                 PROF_ADD(w.pr, 2, PROF_NOW() - tp1);
                 PROF_ADD(w.pr, 5, 1);
                 PROF_ADD(w.pr, 6, n);
@@ -1053,9 +1065,23 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) void k_enc_parse
             const uint32_t v = vv[q], vm4 = vm[q];
             const bool e1 = __builtin_amdgcn_alignbyte(v, vm4, 3) == v, e2 = __builtin_amdgcn_alignbyte(v, vm4, 2) == v;
             const bool e3 = __builtin_amdgcn_alignbyte(v, vm4, 1) == v, e4 = vm4 == v;
+#ifndef S3HC_SHORT_CAND
+#define S3HC_SHORT_CAND 1
+#endif
             const uint32_t c16 = cc[q];
+#if S3HC_SHORT_CAND == 2
+            // One candidate per position: where the bytes [P-4-d, P+4) repeat with a period d of
+            // 1..4 (runs, padding, repeated separators) the candidate is P - d, otherwise the
+            // table's. Decided from bytes already in registers, so the candidate read is not
+            // delayed and only one candidate is measured.
+            const uint32_t dfs = (e1 & (i >= 5u)) ? 1u : ((e2 & (i >= 6u)) ? 2u : ((e3 & (i >= 7u)) ? 3u : ((e4 & (i >= 8u)) ? 4u : 0u)));
+            const bool per = (dfs != 0u) & (__builtin_amdgcn_alignbyte(vm4, vm8[q], (4u - dfs) & 3u) == vm4);
+            const bool tin = per | ((c16 != kEmpty) & (c16 < i));
+            const uint32_t ct = per ? i - dfs : (tin ? c16 : i);
+#else
             const bool tin = (c16 != kEmpty) & (c16 < i);
             const uint32_t ct = tin ? c16 : i;
+#endif
             const uint32_t a = i >> 2, sh = i & 3, ta = ct >> 2, ts = ct & 3;
             uint32_t O[kNQ + 1], T[kNQ + 3];
 #pragma unroll
@@ -1081,9 +1107,15 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) void k_enc_parse
             const bool gt = valid & tin & (__builtin_amdgcn_alignbyte(T[2], T[1], ts) == v);
             uint32_t len = lt, nb = nbt, dist = i - ct;
             bool gf = false;
-            if (__ballot(valid & (e1 | e2 | e3 | e4))) {  // short-distance repeats are rare in most steps
+#ifndef S3HC_SHORT_MIN
+#define S3HC_SHORT_MIN 16
+#endif
+            // the distance-1..4 candidate is measured only where the table candidate is absent
+            // or shorter than S3HC_SHORT_MIN bytes (a long table match is kept as is)
+            const bool want_short = valid & (e1 | e2 | e3 | e4) & !(gt & (lt >= S3HC_SHORT_MIN));
+            if (S3HC_SHORT_CAND == 1 && __ballot(want_short)) {
                 const uint32_t df = (e1 & (i >= 1)) ? 1u : ((e2 & (i >= 2)) ? 2u : ((e3 & (i >= 3)) ? 3u : ((e4 & (i >= 4)) ? 4u : 0u)));
-                gf = valid & (df != 0);
+                gf = want_short & (df != 0);
                 const uint32_t fs = (4u - df) & 3u;
                 uint32_t lf = kFwd + 1u;
 #pragma unroll
