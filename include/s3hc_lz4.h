@@ -91,7 +91,9 @@ void s3hc_stream_close(s3hc_stream* s);
 /* A batch of n independent items already in HBM. Item i = d_src[src_off[i] ..
  * src_off[i]+len[i]). mode[i]: 0 = compress (lz4_flex Auto layout, as flush_batch),
  * 1 = store-mode frame (as encode_store_mode_frame; the extension denylist path,
- * compression.rs:252-308). Metadata arrays are host arrays; the plan is reusable. */
+ * compression.rs:252-308), 2 = compress as consecutive 64 KiB frames (S3HC_BLK_64K_PER_FRAME:
+ * same bytes once decoded by the reference's frame loop, parallel decode on the GPU).
+ * Metadata arrays are host arrays; the plan is reusable. */
 int s3hc_plan_encode(s3hc_ctx* ctx, const uint64_t* src_off, const uint32_t* len,
                      const uint8_t* mode, uint32_t n, s3hc_plan** out);
 /* Frames of item i land contiguously in d_dst at d_item_off[i], d_item_len[i] bytes
@@ -189,6 +191,10 @@ typedef int (*s3hc_frame_sink)(void* user, const uint8_t* frame, size_t n);
 int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t flush_bytes, uint32_t flush_batches,
                            s3hc_handler* stats, s3hc_aggregator** out);
 int s3hc_aggregator_flush(s3hc_aggregator* a);
+/* Layout of compressed batches: S3HC_BLK_AUTO_LZ4FLEX (default, one frame per batch as
+ * flush_batch writes it) or S3HC_BLK_64K_PER_FRAME (64 KiB frames: a reference reader decodes
+ * them the same, the GPU decoder runs one wave per 64 KiB instead of per batch). */
+int s3hc_aggregator_set_frame_policy(s3hc_aggregator* a, int policy);
 /* Encode launches and batches encoded so far. */
 void s3hc_aggregator_counters(const s3hc_aggregator* a, uint64_t* launches, uint64_t* batches);
 void s3hc_aggregator_destroy(s3hc_aggregator* a);

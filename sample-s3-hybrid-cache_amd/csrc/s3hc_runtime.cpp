@@ -375,7 +375,11 @@ extern "C" int s3hc_plan_encode(s3hc_ctx* ctx, const uint64_t* src_off, const ui
     std::lock_guard<std::mutex> g(ctx->mu);
     HIPCHK(hipSetDevice(ctx->device));
     std::unique_ptr<s3hc_plan> P(new s3hc_plan);
-    for (uint32_t i = 0; i < n; ++i) plan_item(P.get(), src_off[i], len[i], mode ? mode[i] : 0, S3HC_BLK_AUTO_LZ4FLEX);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t m = mode ? mode[i] : 0;
+        if (m > 2) return fail(S3HC_INVALID_ARG, "mode must be 0, 1 or 2");
+        plan_item(P.get(), src_off[i], len[i], m == 1 ? 1 : 0, m == 2 ? S3HC_BLK_64K_PER_FRAME : S3HC_BLK_AUTO_LZ4FLEX);
+    }
     int rc = plan_upload_encode(P.get(), ctx->stream);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(ctx->stream));

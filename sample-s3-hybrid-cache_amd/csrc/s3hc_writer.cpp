@@ -86,6 +86,7 @@ struct s3hc_aggregator {
     size_t flush_bytes;
     uint32_t flush_batches;
     s3hc_handler* stats;     // optional shared counters (the writers' Arc<CompressionStatsAtomic>)
+    uint8_t compress_mode = 0;  // plan mode of compressed batches: 0 lz4_flex Auto, 2 64 KiB frames
     void* queue = nullptr;   // the aggregator's HIP queue
     std::mutex mu;           // guards pending / pending_bytes / counters
     std::mutex flush_mu;     // one aggregated flush at a time (keeps per-writer frame order)
@@ -220,7 +221,7 @@ static void queue_batch(s3hc_writer* w) {
     s3hc_aggregator* a = w->agg;
     Batch b;
     b.w = w;
-    b.mode = w->compression_enabled ? 0 : 1;
+    b.mode = w->compression_enabled ? a->compress_mode : 1;
     b.data.swap(w->batch_buf);
     w->batch_buf.clear();
     w->batch_buf.reserve(a->batch_size);
@@ -249,6 +250,14 @@ extern "C" int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t f
         return werr(rc, std::string("queue: ") + s3hc_last_error());
     }
     *out = a;
+    return S3HC_OK;
+}
+
+extern "C" int s3hc_aggregator_set_frame_policy(s3hc_aggregator* a, int policy) {
+    if (!a || (policy != S3HC_BLK_AUTO_LZ4FLEX && policy != S3HC_BLK_64K_PER_FRAME))
+        return werr(S3HC_INVALID_ARG, "bad arguments");
+    std::lock_guard<std::mutex> g(a->mu);
+    a->compress_mode = policy == S3HC_BLK_64K_PER_FRAME ? 2 : 0;
     return S3HC_OK;
 }
 

@@ -104,6 +104,7 @@ def _load():
         "s3hc_memcpy_async": (i32, [vp, vp, vp, sz, i32, vp]),
         "s3hc_aggregator_create": (i32, [vp, sz, sz, u32, vp, ctypes.POINTER(vp)]),
         "s3hc_aggregator_flush": (i32, [vp]),
+        "s3hc_aggregator_set_frame_policy": (i32, [vp, i32]),
         "s3hc_aggregator_counters": (None, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "s3hc_aggregator_destroy": (None, [vp]),
         "s3hc_writer_begin": (i32, [vp, u64, u64, i32, vp, vp, ctypes.POINTER(vp)]),
@@ -557,11 +558,13 @@ class BatchAggregator:
     """Coalesces the flush_batch calls of many writers into one encode launch."""
 
     def __init__(self, eng: Engine, batch_size: int = 1 << 20, flush_bytes: int = 0, flush_batches: int = 0,
-                 stats: "CompressionHandler | None" = None):
+                 stats: "CompressionHandler | None" = None, frame_policy: int = BLK_AUTO_LZ4FLEX):
         h = ctypes.c_void_p()
         _wcheck(lib.s3hc_aggregator_create(eng.h, batch_size, flush_bytes, flush_batches,
                                            stats.h if stats is not None else None, ctypes.byref(h)))
         self.h, self.eng, self.stats = h, eng, stats
+        if frame_policy != BLK_AUTO_LZ4FLEX:
+            _wcheck(lib.s3hc_aggregator_set_frame_policy(h, frame_policy))
 
     def flush(self):
         _wcheck(lib.s3hc_aggregator_flush(self.h))

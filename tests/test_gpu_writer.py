@@ -234,3 +234,29 @@ def test_abort_drops_queued_batches(engine):
     w.abort()
     agg.flush()
     assert not got
+
+
+def test_64k_frame_policy(engine, oracle):
+    # GPU-friendly layout: each batch becomes consecutive 64 KiB frames, identical to
+    # s3hc_compress_frame(policy=64K) of the batch; the reference's frame loop decodes it the same
+    import s3hc_lz4 as S
+
+    agg = _agg(engine, MiB, flush_batches=4, frame_policy=S.BLK_64K_PER_FRAME)
+    data = synth.log_text(2 * MiB + 12_345, 31)
+    w = agg.begin(0, len(data) - 1, True)
+    for i in range(0, len(data), 100_000):
+        w.write(data[i:i + 100_000])
+    sink = w.file
+    w.commit()
+    file = bytes(sink)
+    assert oracle.decompress_data(file) == data
+    fr = _frames(file)
+    sizes = [1_100_000, len(data) - 1_100_000]  # one full batch (11 chunks) + the residual at commit
+    assert all(f[5] == 0x40 for f in fr) and len(fr) == sum(-(-n // 65536) for n in sizes)
+    o, k = 0, 0
+    for n in sizes:
+        want = engine.compress_frame(data[o:o + n], S.BLK_64K_PER_FRAME)
+        got = b"".join(fr[k:k + len(_frames(want))])
+        assert got == want
+        k += len(_frames(want))
+        o += n

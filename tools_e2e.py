@@ -134,7 +134,7 @@ def config2(eng, nb=4096, chunk=512, nq=3, reps=3):
     }, data, frame_tab, h_fr, chunk
 
 
-def config4(eng, data2, nq=3, total_gib=8, batch_bytes_list=(256 << 10, 64 << 20)):
+def config4(eng, data2, nq=3, total_gib=8, batch_bytes_list=(256 << 10, 64 << 20, 256 << 20)):
     """8 GiB object decode in host batches. GPU format: 64 KiB frames of the config-2 text
     (tiled); reference format: 1 MiB frames (one 1 MiB block, BD 0x70)."""
     out = {}
