@@ -87,6 +87,19 @@ int s3hc_stream_read(s3hc_stream* s, uint8_t* dst, size_t cap, size_t* n);
 uint64_t s3hc_stream_total(const s3hc_stream* s);
 void s3hc_stream_close(s3hc_stream* s);
 
+/* ---- pipelined range reader (stream_range_data for throughput, config 4) --- */
+/* Complete frames are grouped into device batches of about batch_bytes compressed bytes that
+ * run on `depth` HIP queues (pinned H2D, device frame walk + decode + checksum verify, D2H), so
+ * batches overlap; decoded bytes come back in stream order. Same semantics as s3hc_stream; the
+ * first failing frame ends the stream after the bytes of every earlier frame. */
+typedef struct s3hc_reader s3hc_reader;
+int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3hc_reader** out);
+int s3hc_reader_feed(s3hc_reader* r, const uint8_t* src, size_t n);
+int s3hc_reader_finish(s3hc_reader* r);
+int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t* n);
+uint64_t s3hc_reader_total(const s3hc_reader* r);
+void s3hc_reader_close(s3hc_reader* r);
+
 /* ---- device-resident batches (benchmark path, configs 2/3/5) -------------- */
 /* A batch of n independent items already in HBM. Item i = d_src[src_off[i] ..
  * src_off[i]+len[i]). mode[i]: 0 = compress (lz4_flex Auto layout, as flush_batch),

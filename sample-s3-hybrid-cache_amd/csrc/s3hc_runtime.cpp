@@ -15,6 +15,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "s3hc_lz4.h"
@@ -964,4 +965,352 @@ extern "C" int s3hc_memcpy_async(s3hc_ctx* ctx, void* dst, const void* src, size
     const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
     if (n) HIPCHK(hipMemcpyAsync(dst, src, n, k, q ? (hipStream_t)q : ctx->stream));
     return S3HC_OK;
+}
+
+// Host copy of a large staging buffer split over a few threads (one thread copies ~6-10 GB/s;
+// the reader's feed/stage/deliver copies are otherwise the bottleneck of the pipeline).
+static void par_memcpy(void* dst, const void* src, size_t n) {
+    constexpr size_t kPiece = 512u << 10;
+    const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    const size_t parts = std::min<size_t>(hw, n / kPiece);
+    if (parts < 2) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t per = ((n + parts - 1) / parts + 63) & ~(size_t)63;  // parts * per >= n
+    std::vector<std::thread> ts;
+    for (size_t k = 1; k < parts; ++k) {
+        const size_t o = k * per;
+        if (o >= n) break;
+        ts.emplace_back([=] { memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, n - o)); });
+    }
+    memcpy(dst, src, std::min(per, n));
+    for (auto& t : ts) t.join();
+}
+
+// ------------------------------------------- pipelined range reader (config 4)
+// stream_range_data (disk_cache.rs:3850-3935) for throughput. Complete frames are grouped into
+// device batches of about batch_bytes compressed bytes; each batch runs on one of `depth` HIP
+// queues (pinned H2D, device frame walk + block decode + content-checksum verify, results D2H),
+// so copies and kernels of different batches overlap. Decoded bytes come back in stream order.
+// Semantics as s3hc_stream / stream_range_data: an empty frame does not end the stream; the
+// first failing frame in stream order ends it after every earlier frame's bytes were delivered;
+// bytes that never form a complete frame are CORRUPT at finish. The caller keeps the reference's
+// final size check (disk_cache.rs:3929-3934) against s3hc_reader_total.
+namespace {
+struct PinnedBuf {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
+        const size_t want = std::max<size_t>(n, 1 << 16);
+        hipError_t e = hipHostMalloc((void**)&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+};
+struct RSlot {
+    hipStream_t st = nullptr;
+    hipEvent_t ev = nullptr;
+    PinnedBuf h_in, h_meta, h_res, h_out;
+    DevBuf d_in, d_out, d_meta, d_res, d_nblk, d_blk_base, d_fwant, d_got, d_total, d_dblocks, d_units, d_blk_out,
+        d_blk_status;
+    uint32_t n = 0;
+    std::vector<uint64_t> dst_off;
+    bool ready = false;     // h_out holds the batch's decoded bytes (in stream order)
+    uint64_t out_len = 0;   // bytes in h_out
+    uint64_t out_pos = 0;   // bytes already read
+};
+}  // namespace
+
+struct s3hc_reader {
+    s3hc_ctx* ctx;
+    size_t batch_bytes;
+    std::vector<RSlot> slots;
+    std::vector<int> inflight;  // slot indices in stream order (head may be ready / being read)
+    std::vector<uint8_t> in;    // buffered input; undecoded bytes start at in_head (a frame boundary)
+    size_t in_head = 0;
+    bool finished = false;
+    int error = S3HC_OK;        // reported once every byte before it was read
+    std::string error_msg;
+    uint64_t total = 0;
+};
+
+// Queue frames [0, nf) of W (all complete) as one batch on slot s.
+static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
+    const HFrame& F0 = W.frames[0];
+    const size_t end = nf < W.frames.size() ? W.frames[nf].pos : W.end;
+    const size_t nin = end - F0.pos;
+    const uint32_t n = (uint32_t)nf;
+    S.n = n;
+    S.dst_off.resize(n);
+    std::vector<uint64_t> fo(n);
+    std::vector<uint32_t> fl(n), dc(n);
+    uint64_t slot = 0, blk_cap = 0;
+    for (uint32_t f = 0; f < n; ++f) {
+        const HFrame& F = W.frames[f];
+        const size_t fe = f + 1 < W.frames.size() ? W.frames[f + 1].pos : W.end;
+        fo[f] = F.pos - F0.pos;
+        fl[f] = (uint32_t)(fe - F.pos);
+        const uint64_t cap = (uint64_t)std::max<uint32_t>(F.nblk, 1u) * F.bmax;  // device slot layout k * bmax
+        if (cap > 0xFFFFFFFFull) return fail(S3HC_UNSUPPORTED, "frame too large for one batch");
+        dc[f] = (uint32_t)cap;
+        S.dst_off[f] = slot;
+        slot += cap;
+        blk_cap += cap / 65536u + 2u;
+    }
+    hipStream_t st = S.st;
+    HIPCHK(S.h_in.ensure(nin));
+    par_memcpy(S.h_in.p, r->in.data() + r->in_head + F0.pos, nin);
+    HIPCHK(S.h_meta.ensure(24ull * n));
+    uint8_t* m = S.h_meta.p;
+    memcpy(m, fo.data(), 8ull * n);
+    memcpy(m + 8ull * n, S.dst_off.data(), 8ull * n);
+    memcpy(m + 16ull * n, fl.data(), 4ull * n);
+    memcpy(m + 20ull * n, dc.data(), 4ull * n);
+    HIPCHK(S.d_in.ensure(nin + 64));
+    HIPCHK(S.d_out.ensure(slot + 64));
+    HIPCHK(S.d_meta.ensure(24ull * n + 64));
+    HIPCHK(S.d_res.ensure(8ull * n + 64));
+    HIPCHK(S.d_nblk.ensure(4ull * n + 16));
+    HIPCHK(S.d_blk_base.ensure(8ull * n + 16));
+    HIPCHK(S.d_fwant.ensure(4ull * n + 16));
+    HIPCHK(S.d_got.ensure(4ull * n + 16));
+    HIPCHK(S.d_total.ensure(16));
+    HIPCHK(S.d_dblocks.ensure(blk_cap * sizeof(DecBlock) + 16));
+    HIPCHK(S.d_units.ensure(blk_cap * sizeof(DecUnit) + 16));
+    HIPCHK(S.d_blk_out.ensure(blk_cap * 4 + 16));
+    HIPCHK(S.d_blk_status.ensure(blk_cap * 4 + 16));
+    HIPCHK(S.h_res.ensure(8ull * n));
+    HIPCHK(hipMemcpyAsync(S.d_in.p, S.h_in.p, nin, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.d_meta.p, S.h_meta.p, 24ull * n, hipMemcpyHostToDevice, st));
+    const uint8_t* src = S.d_in.as<uint8_t>();
+    uint8_t* dm = S.d_meta.as<uint8_t>();
+    const uint64_t* d_fo = (const uint64_t*)dm;
+    const uint64_t* d_do = (const uint64_t*)(dm + 8ull * n);
+    const uint32_t* d_fl = (const uint32_t*)(dm + 16ull * n);
+    const uint32_t* d_dc = (const uint32_t*)(dm + 20ull * n);
+    uint32_t* d_olen = S.d_res.as<uint32_t>();
+    int32_t* d_st = (int32_t*)(S.d_res.as<uint8_t>() + 4ull * n);
+    KTimer T(r->ctx, st);
+    T.begin("dec_plan");
+    HIPCHK(launch_dframe_count(src, d_fo, d_fl, d_dc, n, S.d_nblk.as<uint32_t>(), d_st, st));
+    HIPCHK(launch_scan(S.d_nblk.as<uint32_t>(), n, S.d_blk_base.as<uint64_t>(), S.d_total.as<uint64_t>(), st));
+    HIPCHK(hipMemsetAsync(S.d_units.p, 0, blk_cap * sizeof(DecUnit), st));
+    HIPCHK(launch_dframe_fill(src, d_fo, d_fl, n, d_do, d_dc, S.d_blk_base.as<uint64_t>(), d_st,
+                              S.d_dblocks.as<DecBlock>(), S.d_units.as<DecUnit>(), S.d_fwant.as<uint32_t>(), st));
+    T.end();
+    T.begin("decode");
+    HIPCHK(launch_decode_units(src, S.d_out.as<uint8_t>(), S.d_dblocks.as<DecBlock>(), S.d_units.as<DecUnit>(),
+                               (uint32_t)blk_cap, S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), st));
+    T.end();
+    T.begin("dec_finish");
+    HIPCHK(launch_dframe_finish(S.d_blk_base.as<uint64_t>(), n, S.d_nblk.as<uint32_t>(), S.d_dblocks.as<DecBlock>(),
+                                S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), d_st, d_olen, st));
+    T.end();
+    T.begin("xxh32");
+    HIPCHK(launch_xxh32(S.d_out.as<uint8_t>(), d_do, d_olen, n, S.d_got.as<uint32_t>(), st));
+    T.end();
+    T.begin("dec_finish");
+    HIPCHK(launch_dframe_verify(src, d_fo, n, S.d_fwant.as<uint32_t>(), S.d_got.as<uint32_t>(), d_olen, d_st, st));
+    T.end();
+    HIPCHK(hipMemcpyAsync(S.h_res.p, S.d_res.p, 8ull * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(S.ev, st));
+    r->in_head += end;
+    return S3HC_OK;
+}
+
+// Form and queue batches while a slot is free and complete frames are buffered.
+static int reader_pump(s3hc_reader* r) {
+    while (r->inflight.size() < r->slots.size() && r->in_head < r->in.size()) {
+        // walk only what one batch can use (a frame cut by the limit counts as incomplete);
+        // the whole buffer only when no frame completes within it (frames larger than that)
+        const size_t avail = r->in.size() - r->in_head;
+        const size_t lim = std::min(avail, r->batch_bytes + ((size_t)8 << 20));
+        HWalk W;
+        walk_frames(r->in.data() + r->in_head, lim, W, true, false);
+        size_t nf = W.frames.size();
+        if (nf && W.last_incomplete) nf--;  // (stream mode leaves incomplete frames unwalked)
+        if (nf == 0 && lim < avail) {
+            W = HWalk();
+            walk_frames(r->in.data() + r->in_head, avail, W, true, false);
+            nf = W.frames.size();
+            if (nf && W.last_incomplete) nf--;
+        }
+        if (nf == 0) {
+            if (W.tail_status != S3HC_OK && W.frames.empty() && !r->error) {  // bad header: nothing decodable
+                r->error = W.tail_status;
+                r->error_msg = "malformed frame header";
+                r->in.clear();
+                r->in_head = 0;
+            }
+            return S3HC_OK;
+        }
+        // batch = frames up to batch_bytes of input (at least one)
+        size_t k = 1;
+        while (k < nf && W.frames[k].pos - W.frames[0].pos < r->batch_bytes) ++k;
+        if (k < nf || W.end - W.frames[0].pos >= r->batch_bytes || r->finished) {
+            // full batch (or all that will ever come)
+        } else if (!r->inflight.empty()) {
+            return S3HC_OK;  // wait for more input to fill the batch while others run
+        }
+        std::vector<bool> used(r->slots.size(), false);
+        for (int i : r->inflight) used[i] = true;
+        int s = 0;
+        while (used[s]) ++s;
+        int rc = reader_submit(r, r->slots[s], W, k);
+        if (rc) return rc;
+        r->inflight.push_back(s);
+    }
+    return S3HC_OK;
+}
+
+// Wait for the oldest batch and copy its good frames' bytes (stream order) into its pinned
+// output buffer; a failing frame ends the stream after them.
+static int reader_complete(s3hc_reader* r) {
+    RSlot& S = r->slots[r->inflight.front()];
+    HIPCHK(hipEventSynchronize(S.ev));
+    const uint32_t* olen = (const uint32_t*)S.h_res.p;
+    const int32_t* st = (const int32_t*)(S.h_res.p + 4ull * S.n);
+    uint32_t good = 0;
+    uint64_t bytes = 0;
+    while (good < S.n && st[good] == S3HC_OK) bytes += olen[good++];
+    HIPCHK(S.h_out.ensure(bytes + 16));
+    // frames decode into slots of their block capacity; when every frame but the last filled
+    // its slot (the normal case) the good output is already contiguous: one copy
+    bool packed = true;
+    for (uint32_t f = 0; f + 1 < good; ++f) packed &= S.dst_off[f] + olen[f] == S.dst_off[f + 1];
+    if (packed) {
+        if (bytes) HIPCHK(hipMemcpyAsync(S.h_out.p, S.d_out.p, bytes, hipMemcpyDeviceToHost, S.st));
+    } else {
+        uint64_t o = 0;
+        for (uint32_t f = 0; f < good; ++f) {
+            if (olen[f]) HIPCHK(hipMemcpyAsync(S.h_out.p + o, S.d_out.as<uint8_t>() + S.dst_off[f], olen[f],
+                                               hipMemcpyDeviceToHost, S.st));
+            o += olen[f];
+        }
+    }
+    HIPCHK(hipStreamSynchronize(S.st));
+    S.ready = true;
+    S.out_len = bytes;
+    S.out_pos = 0;
+    r->total += bytes;
+    if (good < S.n) {  // earlier in stream order than any error found while walking later input
+        r->error = st[good];
+        r->error_msg = "frame decode failed";
+        for (size_t k = 1; k < r->inflight.size(); ++k) (void)hipEventSynchronize(r->slots[r->inflight[k]].ev);
+        r->inflight.resize(1);  // drop everything after the failing frame
+        r->in.clear();
+        r->in_head = 0;
+    }
+    return S3HC_OK;
+}
+
+extern "C" int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3hc_reader** out) {
+    if (!ctx || !out || depth < 1 || depth > 16 || batch_bytes == 0) return fail(S3HC_INVALID_ARG, "bad arguments");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    std::unique_ptr<s3hc_reader> r(new s3hc_reader);
+    r->ctx = ctx;
+    r->batch_bytes = batch_bytes;
+    r->slots.resize(depth);
+    for (auto& S : r->slots) {
+        HIPCHK(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+    }
+    *out = r.release();
+    return S3HC_OK;
+}
+extern "C" int s3hc_reader_feed(s3hc_reader* r, const uint8_t* src, size_t n) {
+    if (!r || (!src && n)) return fail(S3HC_INVALID_ARG, "bad arguments");
+    if (r->finished) return fail(S3HC_INVALID_ARG, "reader already finished");
+    if (r->error) return S3HC_OK;  // the stream has ended with an error; input is ignored
+    if (r->in_head && r->in_head >= r->in.size() / 2) {  // drop consumed input (amortized)
+        r->in.erase(r->in.begin(), r->in.begin() + r->in_head);
+        r->in_head = 0;
+    }
+    const size_t old = r->in.size();
+    r->in.resize(old + n);
+    par_memcpy(r->in.data() + old, src, n);
+    std::lock_guard<std::mutex> g(r->ctx->mu);
+    HIPCHK(hipSetDevice(r->ctx->device));
+    return reader_pump(r);
+}
+extern "C" int s3hc_reader_finish(s3hc_reader* r) {
+    if (!r) return fail(S3HC_INVALID_ARG, "bad arguments");
+    r->finished = true;
+    return S3HC_OK;
+}
+extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t* n) {
+    if (!r || !n || (!dst && cap)) return fail(S3HC_INVALID_ARG, "bad arguments");
+    *n = 0;
+    if (!cap) return S3HC_OK;
+    // a ready head batch is delivered without the context lock (the copy is the caller's
+    // Bytes::copy_from_slice; concurrent readers must not serialize on it)
+    if (!r->inflight.empty() && r->slots[r->inflight.front()].ready) {
+        RSlot& S = r->slots[r->inflight.front()];
+        if (S.out_pos < S.out_len) {
+            const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
+            if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
+            S.out_pos += k;
+            *n = k;
+            if (S.out_pos < S.out_len) return S3HC_OK;
+        }
+    }
+    std::lock_guard<std::mutex> g(r->ctx->mu);
+    HIPCHK(hipSetDevice(r->ctx->device));
+    for (;;) {
+        if (!r->inflight.empty() && r->slots[r->inflight.front()].ready) {
+            RSlot& S = r->slots[r->inflight.front()];
+            if (*n == 0 && S.out_pos < S.out_len) {
+                const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
+                if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
+                S.out_pos += k;
+                *n = k;
+            }
+            if (S.out_pos == S.out_len) {  // slot free again: queue the next batch
+                S.ready = false;
+                r->inflight.erase(r->inflight.begin());
+                if (!r->error) {
+                    int rc = reader_pump(r);
+                    if (rc) return rc;
+                }
+            }
+            if (*n) return S3HC_OK;
+            continue;
+        }
+        if (!r->error) {
+            int rc = reader_pump(r);
+            if (rc) return rc;
+        }
+        if (r->inflight.empty()) {
+            if (r->error) return fail(r->error, r->error_msg);
+            if (r->finished && r->in_head < r->in.size()) {
+                r->error = S3HC_CORRUPT;
+                r->error_msg = "truncated frame at end of stream";
+                return fail(r->error, r->error_msg);
+            }
+            return S3HC_OK;  // needs more input, or end of stream
+        }
+        // the oldest batch is still running: wait for it only when the pipeline is full, the
+        // input is finished or it is already done; otherwise ask the caller for more input
+        RSlot& H = r->slots[r->inflight.front()];
+        const bool done = hipEventQuery(H.ev) == hipSuccess;
+        if (!done && r->inflight.size() < r->slots.size() && !r->finished && !r->error) return S3HC_OK;
+        int rc = reader_complete(r);
+        if (rc) return rc;
+    }
+}
+extern "C" uint64_t s3hc_reader_total(const s3hc_reader* r) { return r ? r->total : 0; }
+extern "C" void s3hc_reader_close(s3hc_reader* r) {
+    if (!r) return;
+    (void)hipSetDevice(r->ctx->device);
+    for (auto& S : r->slots) {
+        if (S.st) (void)hipStreamSynchronize(S.st);
+        if (S.ev) (void)hipEventDestroy(S.ev);
+        if (S.st) (void)hipStreamDestroy(S.st);
+    }
+    delete r;
 }

@@ -102,6 +102,12 @@ def _load():
         "s3hc_queue_destroy": (i32, [vp, vp]),
         "s3hc_queue_sync": (i32, [vp, vp]),
         "s3hc_memcpy_async": (i32, [vp, vp, vp, sz, i32, vp]),
+        "s3hc_reader_open": (i32, [vp, sz, i32, ctypes.POINTER(vp)]),
+        "s3hc_reader_feed": (i32, [vp, u8p, sz]),
+        "s3hc_reader_finish": (i32, [vp]),
+        "s3hc_reader_read": (i32, [vp, u8p, sz, szp]),
+        "s3hc_reader_total": (u64, [vp]),
+        "s3hc_reader_close": (None, [vp]),
         "s3hc_aggregator_create": (i32, [vp, sz, sz, u32, vp, ctypes.POINTER(vp)]),
         "s3hc_aggregator_flush": (i32, [vp]),
         "s3hc_aggregator_set_frame_policy": (i32, [vp, i32]),
@@ -432,6 +438,52 @@ class FrameStream:
             if self.h:
                 lib.s3hc_stream_close(self.h)
                 self.h = None
+        except Exception:
+            pass
+
+
+class RangeReader:
+    """Pipelined stream_range_data: feed compressed bytes, read decoded bytes in stream order;
+    batches of ~batch_bytes run on `depth` HIP queues."""
+
+    def __init__(self, eng: Engine, batch_bytes: int = 256 << 10, depth: int = 3):
+        h = ctypes.c_void_p()
+        _check(lib.s3hc_reader_open(eng.h, batch_bytes, depth, ctypes.byref(h)))
+        self.h = h
+
+    def feed(self, data):
+        p, keep = _ptr(data)
+        _check(lib.s3hc_reader_feed(self.h, p, len(keep)))
+
+    def feed_ptr(self, ptr: int, n: int):
+        _check(lib.s3hc_reader_feed(self.h, ctypes.c_void_p(ptr), n))
+
+    def finish(self):
+        _check(lib.s3hc_reader_finish(self.h))
+
+    def read(self, cap: int = 1 << 20) -> bytes:
+        out = ctypes.create_string_buffer(cap)
+        n = ctypes.c_size_t()
+        _check(lib.s3hc_reader_read(self.h, out, cap, ctypes.byref(n)))
+        return out.raw[: n.value]
+
+    def read_into(self, ptr: int, cap: int) -> int:
+        n = ctypes.c_size_t()
+        _check(lib.s3hc_reader_read(self.h, ctypes.c_void_p(ptr), cap, ctypes.byref(n)))
+        return n.value
+
+    @property
+    def total(self) -> int:
+        return lib.s3hc_reader_total(self.h)
+
+    def close(self):
+        if self.h:
+            lib.s3hc_reader_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
         except Exception:
             pass
 

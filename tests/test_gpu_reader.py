@@ -1,0 +1,103 @@
+"""Pipelined range reader (s3hc_reader_*): stream_range_data semantics over batched device
+decodes on several queues. Output must equal the oracle's
+decompress of the same frames, in order, for any feed piece size and batch size; errors end the
+stream after every earlier frame's bytes (tests/streaming_decompression_property_test.rs)."""
+import pytest
+
+import synth
+
+pytestmark = pytest.mark.gpu
+MiB = 1 << 20
+
+
+def _drain(r, out, cap=MiB):
+    while True:
+        c = r.read(cap)
+        if not c:
+            return
+        out += c
+
+
+def _run(engine, frames, piece, batch, depth=3, cap=MiB):
+    import s3hc_lz4 as S
+
+    r = S.RangeReader(engine, batch, depth)
+    out = bytearray()
+    for i in range(0, len(frames), piece):
+        r.feed(frames[i:i + piece])
+        _drain(r, out, cap)
+    r.finish()
+    _drain(r, out, cap)
+    return bytes(out), r
+
+
+@pytest.mark.parametrize("piece,batch,depth", [(1000, 256 << 10, 3), (65536, 256 << 10, 3), (3 * MiB, 64 << 10, 2),
+                                               (777_777, 4 * MiB, 4), (10 * MiB, 1, 1)])
+def test_reader_matches_oracle(engine, oracle, piece, batch, depth):
+    data = synth.log_text(5 * MiB + 321, 41)
+    # mixed layouts: 64 KiB frames, a reference-style 1 MiB frame, a store-mode frame, an empty frame
+    frames = (engine.compress_frame(data[:2 * MiB], 1) + engine.compress_frame(data[2 * MiB:3 * MiB]) +
+              engine.compress_frame(b"") + oracle.store_mode_frame(data[3 * MiB:3 * MiB + 70_000]) +
+              engine.compress_frame(data[3 * MiB + 70_000:], 1))
+    out, r = _run(engine, frames, piece, batch, depth)
+    assert out == data
+    assert r.total == len(data)
+
+
+def test_reader_corrupt_frame_stops_after_earlier_frames(engine, oracle):
+    import s3hc_lz4 as S
+
+    data = synth.log_text(16 * 65536, 42)
+    fr = [engine.compress_frame(data[i:i + 65536]) for i in range(0, len(data), 65536)]
+    bad = bytearray(fr[9])
+    bad[-1] ^= 0x5A  # content checksum of frame 9
+    frames = b"".join(fr[:9]) + bytes(bad) + b"".join(fr[10:])
+    r = S.RangeReader(engine, 3 * 65536, 3)
+    r.feed(frames)
+    r.finish()
+    out = bytearray()
+    with pytest.raises(S.CodecError) as e:
+        _drain(r, out)
+    assert e.value.status == S.S3HC_CHECKSUM
+    assert bytes(out) == data[:9 * 65536]
+
+
+def test_reader_truncated_tail(engine):
+    import s3hc_lz4 as S
+
+    data = synth.log_text(300_000, 43)
+    frames = engine.compress_frame(data[:200_000], 1) + engine.compress_frame(data[200_000:], 1)
+    r = S.RangeReader(engine, 128 << 10, 3)
+    r.feed(frames[:-7])
+    r.finish()
+    out = bytearray()
+    with pytest.raises(S.CodecError) as e:
+        _drain(r, out)
+    assert e.value.status == S.S3HC_CORRUPT
+    assert bytes(out) == data[:len(out)] and len(out) >= 196_608  # the complete 64 KiB frames came first
+
+
+def test_reader_garbage_after_frames(engine):
+    import s3hc_lz4 as S
+
+    data = synth.log_text(100_000, 44)
+    frames = engine.compress_frame(data, 1) + b"\xde\xad\xbe\xef" * 8
+    r = S.RangeReader(engine, 1 << 20, 2)
+    r.feed(frames)
+    r.finish()
+    out = bytearray()
+    with pytest.raises(S.CodecError):
+        _drain(r, out)
+    assert bytes(out) == data
+
+
+@pytest.mark.parametrize("policy", [1, 0])
+@pytest.mark.parametrize("batch", [256 << 10, 4 << 20, 64 << 20])
+def test_reader_large_object_4mib_feeds(engine, policy, batch):
+    # config-4 shape at 1/64 scale: 128 MiB object, 4 MiB file reads, 1 MiB chunk reads
+    data = synth.log_text(128 * MiB, 45)
+    item = 65536 if policy == 1 else MiB
+    frames = b"".join(engine.compress_frame(data[i:i + item], 0) for i in range(0, len(data), item)) if policy == 0 \
+        else engine.compress_frame(data, 1)
+    out, r = _run(engine, frames, 4 * MiB, batch, 3)
+    assert len(out) == len(data) and out == data

@@ -211,11 +211,36 @@ def config4(eng, data2, nq=3, total_gib=8, batch_bytes_list=(256 << 10, 64 << 20
             for L in lanes:
                 L[0].sync()
             dt = time.perf_counter() - t0
-            res[f"e2e_decode_GiBps_batch_{bb >> 10}KiB"] = round(nbat * fpb * item / dt / GiB, 3)
+            res[f"e2e_decode_GiBps_batch_{bb >> 10}KiB"] = round(nbat * fpb * item / dt / GiB, 3)  # Python-driven
             ok = bytes(h_out.view()[:item]) == data2[:item]
             res[f"check_batch_{bb >> 10}KiB"] = ok
             for L in lanes:
                 L[0].close()
+        # the C++ pipelined range reader (s3hc_reader): the object's frames fed in 4 MiB file
+        # reads, decoded bytes read back in 1 MiB chunks (stream_range_data's chunk size)
+        for bb in (256 << 10, 4 << 20, 64 << 20):
+            rd = S.RangeReader(eng, bb, nq)
+            hp, op = h_fr.data_ptr(), h_out.data_ptr()
+            ctot, got = C1 * tiles, 0
+            t0 = time.perf_counter()
+            for o in range(0, ctot, 4 << 20):
+                rd.feed_ptr(hp + o, min(4 << 20, ctot - o))
+                while True:
+                    k = rd.read_into(op + got, min(1 << 20, total_u - got))
+                    if not k:
+                        break
+                    got += k
+            rd.finish()
+            while True:
+                k = rd.read_into(op + got, min(1 << 20, total_u - got))
+                if not k:
+                    break
+                got += k
+            dt = time.perf_counter() - t0
+            assert got == total_u and rd.total == total_u
+            res[f"reader_decode_GiBps_batch_{bb >> 10}KiB"] = round(total_u / dt / GiB, 3)
+            res[f"reader_check_batch_{bb >> 10}KiB"] = bytes(h_out.view()[-item:]) == data2[-item:]
+            rd.close()
         out[fmt] = res
         h_out.free()
         h_fr.free()
@@ -226,12 +251,16 @@ def config4(eng, data2, nq=3, total_gib=8, batch_bytes_list=(256 << 10, 64 << 20
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-config4", action="store_true")
+    ap.add_argument("--skip-config2", action="store_true")
     ap.add_argument("--gib", type=float, default=8.0)
     a = ap.parse_args()
     eng = S.Engine(0)
     res = {"pcie": pcie(eng)}
-    c2, data2, *_ = config2(eng)
-    res["config2"] = c2
+    if a.skip_config2:
+        data2 = synth.log_text(4096 * BLK, synth.SEED_BASE + 1)
+    else:
+        c2, data2, *_ = config2(eng)
+        res["config2"] = c2
     if not a.skip_config4:
         res["config4"] = config4(eng, data2, total_gib=a.gib)
     print(json.dumps(res, indent=1))
