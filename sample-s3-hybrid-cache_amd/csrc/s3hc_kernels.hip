@@ -169,6 +169,7 @@ __device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t in) {
 
 // out[r] = xxh32(base + off[r], len[r], seed 0). Lanes 4r..4r+3 run the 4 accumulator chains
 // (gid = global thread index of the calling grid's xxh32 threads).
+template <uint32_t kIF>  // loads in flight per lane (VGPRs: the match finder's copy uses fewer)
 __device__ __forceinline__ void xxh32_ranges_dev(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                  const uint32_t* __restrict__ len, uint32_t n,
                                                  uint32_t* __restrict__ out, uint32_t gid) {
@@ -183,13 +184,13 @@ __device__ __forceinline__ void xxh32_ranges_dev(const uint8_t* __restrict__ bas
     uint32_t s = 0;
     if ((((uintptr_t)p) & 3) == 0) {
         const uint32_t* w = (const uint32_t*)q;
-        // 32 loads in flight per lane: the chain (add, rotate, multiply) is the only serial part
-        for (; s + 32 <= ns; s += 32) {
-            uint32_t v[32];
+        // kIF loads in flight per lane: the chain (add, rotate, multiply) is the only serial part
+        for (; s + kIF <= ns; s += kIF) {
+            uint32_t v[kIF];
 #pragma unroll
-            for (int k = 0; k < 32; ++k) v[k] = w[4 * (s + k)];
+            for (uint32_t k = 0; k < kIF; ++k) v[k] = w[4 * (s + k)];
 #pragma unroll
-            for (int k = 0; k < 32; ++k) acc = xround(acc, v[k]);
+            for (uint32_t k = 0; k < kIF; ++k) acc = xround(acc, v[k]);
         }
         for (; s < ns; ++s) acc = xround(acc, w[4 * s]);
     } else {
@@ -218,11 +219,11 @@ __device__ __forceinline__ void xxh32_ranges_dev(const uint8_t* __restrict__ bas
     h ^= h >> 16;
     out[r] = h;
 }
-__global__ __launch_bounds__(256) void k_xxh32_ranges(const uint8_t* __restrict__ base,
+__global__ __launch_bounds__(64) void k_xxh32_ranges(const uint8_t* __restrict__ base,
                                                       const uint64_t* __restrict__ off,
                                                       const uint32_t* __restrict__ len, uint32_t n,
                                                       uint32_t* __restrict__ out) {
-    xxh32_ranges_dev(base, off, len, n, out, blockIdx.x * blockDim.x + threadIdx.x);
+    xxh32_ranges_dev<64>(base, off, len, n, out, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // ================================================================== decode
@@ -970,7 +971,7 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) void k_enc_parse
     // The first nxx workgroups compute the frames' content xxh32 (they are dispatched first and
     // overlap the match finding; the emitter reads the hashes).
     if (blockIdx.x < nxx) {
-        xxh32_ranges_dev(src, fsrc_off, fsrc_len, nframes, fhash, blockIdx.x * kGThreads + threadIdx.x);
+        xxh32_ranges_dev<32>(src, fsrc_off, fsrc_len, nframes, fhash, blockIdx.x * kGThreads + threadIdx.x);
         return;
     }
     const uint32_t gi = blockIdx.x - nxx;
@@ -1652,7 +1653,8 @@ static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 hipError_t launch_xxh32(const uint8_t* base, const uint64_t* off, const uint32_t* len, uint32_t n, uint32_t* out,
                         hipStream_t st) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_xxh32_ranges, dim3(cdiv((uint64_t)n * 4, 256)), dim3(256), 0, st, base, off, len, n, out);
+    // 16 ranges per 64-lane workgroup: 4096 frames spread over all 256 CUs instead of 64
+    hipLaunchKernelGGL(k_xxh32_ranges, dim3(cdiv((uint64_t)n * 4, 64)), dim3(64), 0, st, base, off, len, n, out);
     return hipGetLastError();
 }
 hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
