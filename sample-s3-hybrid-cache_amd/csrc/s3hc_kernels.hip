@@ -1309,7 +1309,11 @@ __global__ __launch_bounds__(256) void k_enc_emit(const uint8_t* __restrict__ sr
                                                   const uint32_t* __restrict__ blk_carry,
                                                   const uint64_t* __restrict__ blk_off,
                                                   const uint32_t* __restrict__ frame_hash, uint8_t* dst) {
-    constexpr uint32_t kOut = 2 * kSeg + 1024;  // encoded segment body bound
+    // Encoded body bound of one segment: a record consuming ll + ml input bytes (ml >= 4) emits
+    // [j > 0](1 + ext(ll)) + ll + 2 + ext(ml - 4) bytes, i.e. at most ext(ll) - 1 more than it
+    // consumes (2 + ext(ml - 4) - ml <= -2), and ext(ll) - 1 <= ll / 255; records consume at
+    // most kSeg bytes, so the body is <= kSeg + kSeg / 255 (+ slack).
+    constexpr uint32_t kOut = kSeg + 256;
     constexpr uint32_t kIb = kSeg + 64;
     constexpr uint32_t kWaveLds = kOut + kIb;
     __shared__ __attribute__((aligned(16))) uint8_t smem[2 * kWaveLds];
