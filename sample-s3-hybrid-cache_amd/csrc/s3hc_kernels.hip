@@ -806,7 +806,8 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
                                                       const DecBlock* __restrict__ blk,
                                                       const DecUnit* __restrict__ units, uint32_t nunits,
                                                       uint32_t* __restrict__ blk_out,
-                                                      int32_t* __restrict__ blk_status) {
+                                                      int32_t* __restrict__ blk_status,
+                                                      const uint8_t* __restrict__ unit_lb) {
 #ifndef S3HC_DEC_LDS_PAD
 #define S3HC_DEC_LDS_PAD 0  // diagnostic builds: extra LDS per workgroup to lower occupancy
 #endif
@@ -815,6 +816,7 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t u = blockIdx.x * dec::kWaves + wv;
     if (u >= nunits) return;
+    if (unit_lb && unit_lb[u]) return;  // decoded by the large-block path (s3hc_lb.hip)
     const DecUnit U = units[u];
     if (U.n == 0) return;
     DecWave w;
@@ -953,7 +955,12 @@ __device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* 
 //      or after the greedy position (s_ff1), its word by v_readlane, long matches extended
 //      wave-wide; the chunk's hops then become sequence records lane-parallel.
 // Matches end inside the segment, so segments are independent; k_enc_sizes stitches them.
-__global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) void k_enc_parse(const uint8_t* __restrict__ src,
+#ifdef S3HC_ENC_WPE  // diagnostic builds: cap VGPRs for S3HC_ENC_WPE waves per SIMD
+#define S3HC_ENC_WPE_ATTR __attribute__((amdgpu_num_vgpr(512 / S3HC_ENC_WPE / 8 * 8)))
+#else
+#define S3HC_ENC_WPE_ATTR
+#endif
+__global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATTR void k_enc_parse(const uint8_t* __restrict__ src,
                                                               const EncBlock* __restrict__ blocks,
                                                               const uint2* __restrict__ groups, uint32_t ngroups,
                                                               uint32_t nxx, const uint64_t* __restrict__ fsrc_off,
@@ -1662,10 +1669,11 @@ hipError_t launch_xxh32(const uint8_t* base, const uint64_t* off, const uint32_t
     return hipGetLastError();
 }
 hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
-                               uint32_t nunits, uint32_t* blk_out, int32_t* blk_status, hipStream_t st) {
+                               uint32_t nunits, uint32_t* blk_out, int32_t* blk_status, const uint8_t* unit_lb,
+                               hipStream_t st) {
     if (!nunits) return hipSuccess;
     hipLaunchKernelGGL(k_decode_units, dim3(cdiv(nunits, dec::kWaves)), dim3(64 * dec::kWaves), 0, st, src, dst, blk,
-                       units, nunits, blk_out, blk_status);
+                       units, nunits, blk_out, blk_status, unit_lb);
     return hipGetLastError();
 }
 hipError_t launch_enc_parse(const uint8_t* src, const EncBlock* blocks, const uint2* groups, uint32_t ngroups,

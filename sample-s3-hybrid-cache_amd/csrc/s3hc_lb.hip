@@ -1,0 +1,838 @@
+// s3hc_lb.hip — large-block LZ4 decode on CDNA4 (gfx950): one block, many workgroups.
+//
+// The one-wave-per-block decoder (k_decode_units) is the right shape for 64 KiB blocks, of
+// which a batch holds thousands. The reference's own cache files are different: flush_batch
+// (disk_cache.rs:1820-1870) compresses ~1 MiB batches with lz4_flex BlockSize::Auto, i.e. one
+// block of up to 4 MiB per frame (BD 0x70), and a GET of such a file hands the GPU a handful
+// of large blocks. Decoding those with one wave each leaves the chip idle, so blocks whose
+// frame allows more than 64 KiB go through this path instead (same results, same statuses):
+//
+//   k_lb_classify  (1 workgroup)  takes the eligible units (one independent compressed block,
+//                  frame max block size > 64 KiB) up to the scratch caps; lays out chunks of
+//                  kLbChunk compressed positions per block.
+//   k_lb_gran      per chunk: first non-255 byte at or after each 64-byte granule (length
+//                  extension runs are 255-runs; this makes every run length O(64) to find).
+//   k_lb_exit      per chunk: the next-token position of a token assumed at EVERY position
+//                  (lz4_flex parse rules, exact for long runs), then pointer doubling in LDS:
+//                  each position learns where its token chain leaves the chunk.
+//   k_lb_entry     per block, serial over chunks: the true chain's entry into each chunk.
+//   k_lb_mark      per chunk: doubling again, marking the nodes reachable from the entry =
+//                  the block's real tokens; per-chunk sequence count and output bytes.
+//   (scans)        global sequence index and output offset of each chunk.
+//   k_lb_seq       per chunk: the sequence table (out, literal, ll, ml, offset) and the
+//                  lz4_flex bound checks in stream order (first failing sequence decides).
+//   k_lb_fin       per block: size, status, first sequence.
+//   k_lb_run       one 1024-thread workgroup per block writes the output in 8 KiB steps: in
+//                  each step every byte gets its value (literal, or a match source before the
+//                  step: 64 KiB LDS ring of recent output) or a pointer to its source inside
+//                  the step (overlapping copies folded into the first period), and the
+//                  pointers are jumped in LDS until every byte is final.
+//
+// All of it is integer byte work (no MFMA); every kernel is bound by memory latency or LDS.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "s3hc_lz4.h"
+#include "s3hc_plan.hpp"
+
+namespace s3hc {
+namespace lb {
+constexpr uint32_t kT = 1024;                  // threads of a tokenizing workgroup
+constexpr uint32_t kPer = kLbChunk / kT;       // positions per thread
+constexpr uint32_t kLook = 2048;               // staged bytes past the chunk
+constexpr uint32_t kStage = kLbChunk + kLook;  // staged bytes per chunk
+constexpr uint32_t kGran = 64;                 // 255-run index granule
+constexpr uint32_t kGpc = kLbChunk / kGran;    // granules per chunk
+constexpr uint32_t kWords = kLbChunk / 32;     // bitmap words per chunk
+constexpr uint32_t END = 0xFFFFFFFEu;          // next-token value: last sequence
+constexpr uint32_t BAD = 0xFFFFFFFFu;          // next-token value: malformed token
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t INF = 0xFFFFFFFFu;
+constexpr uint32_t kLevels = 13;               // 2^13 > kLbChunk / 3 tokens in a chunk
+constexpr uint32_t kXT = 1024;                 // threads of an executing workgroup
+constexpr uint32_t kXPer = kLbStep / kXT;      // output bytes per executing thread per step (8)
+constexpr uint32_t kRing = 65536;              // recent output kept in LDS (match sources)
+constexpr uint32_t kMaxSeqS = kLbStep / 4 + 3; // sequences touching one step (all but the last have sl >= 4)
+constexpr uint32_t FIN = 0xFFFFFFFFu;          // source pointer of a final byte
+}  // namespace lb
+
+#if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 10
+#define S3HC_LBPROF 1
+// diagnostic builds: k_lb_run phase times (s_memtime sums of every workgroup's thread 0):
+// 0 owners, 1 classify + literal loads, 2 ring/pointer stores, 3 next step's sequences,
+// 4 chain jumping, 5 flush, 6 -, 7 steps, 8 jump rounds, 9 loop top
+__device__ unsigned long long g_lbprof[12];
+#endif
+
+namespace {
+
+__device__ __forceinline__ int lane64() { return (int)(threadIdx.x & 63u); }
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_add(T x, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const T y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// Workgroup exclusive sum (every thread calls; sh holds one entry per wave).
+template <typename T, int NW>
+__device__ __forceinline__ T wg_excl_add(T v, T* sh, T& total) {
+    const int lane = lane64(), w = (int)(threadIdx.x >> 6);
+    const T inc = wave_incl_add(v, lane);
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    T pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const T s = sh[k];
+        pre += k < w ? s : (T)0;
+        tot += s;
+    }
+    __syncthreads();
+    total = tot;
+    return pre + inc - v;
+}
+
+// Stage block bytes [cs, cs + ns) into LDS (aligned dword loads; returns s with s[i] = byte cs+i).
+__device__ __forceinline__ const uint8_t* lb_stage(const uint8_t* g, uint32_t cs, uint32_t ns, uint8_t* raw) {
+    const uintptr_t a0 = (uintptr_t)(g + cs);
+    const uint32_t mis = (uint32_t)(a0 & 3u);
+    const uint32_t* aw = (const uint32_t*)(a0 - mis);
+    const uint32_t nd = (mis + ns + 3u) >> 2;
+    for (uint32_t d = threadIdx.x; d < nd; d += blockDim.x) ((uint32_t*)raw)[d] = aw[d];
+    return raw + mis;
+}
+
+struct LbView {
+    const uint8_t* g;    // block payload in HBM
+    const uint8_t* s;    // staged bytes: s[p - cs] for p in [cs, cs + ns)
+    const uint32_t* nzg; // granule index, chunk-major
+    uint32_t cs, ns, C, chunk0, nch;
+};
+
+__device__ __forceinline__ uint32_t lb_byte(const LbView& v, uint32_t p) {
+    const uint32_t r = p - v.cs;
+    return r < v.ns ? (uint32_t)v.s[r] : (uint32_t)v.g[p];
+}
+
+// First position >= pos (pos <= C) whose byte is not 255, or C.
+__device__ uint32_t lb_nz(const LbView& v, uint32_t pos) {
+    using namespace lb;
+    uint32_t gend = (pos / kGran + 1u) * kGran;
+    if (gend > v.C) gend = v.C;
+    for (uint32_t k = pos; k < gend; ++k)
+        if (lb_byte(v, k) != 255u) return k;
+    if (gend >= v.C) return v.C;
+    const uint32_t g = gend / kGran;
+    uint32_t c = g / kGpc;
+    uint32_t val = v.nzg[(size_t)(v.chunk0 + c) * kGpc + (g % kGpc)];
+    while (val == INF) {
+        if (++c >= v.nch) return v.C;
+        val = v.nzg[(size_t)(v.chunk0 + c) * kGpc];
+    }
+    return val;
+}
+
+// The sequence whose token is at p, parsed with the rules of the one-wave decoder's exact path
+// (dec_block slow path, lz4_flex decompress order). nxt: next token position, END (the literal
+// run ends the block: last sequence) or BAD; late = 1: the literal run was valid before BAD,
+// 2: the whole sequence was valid but no token follows its match.
+struct LbTok {
+    uint32_t nxt, lit, ll, off, ml, late;
+};
+__device__ LbTok lb_token(const LbView& v, uint32_t p) {
+    using namespace lb;
+    LbTok T;
+    T.lit = 0; T.ll = 0; T.off = 0; T.ml = 0; T.late = 0;
+    const uint32_t C = v.C;
+    const uint32_t t = lb_byte(v, p);
+    uint32_t pos = p + 1u;
+    uint64_t ll = t >> 4;
+    if (ll == 15u) {
+        const uint32_t q = lb_nz(v, pos);
+        if (q >= C) { T.nxt = BAD; return T; }
+        ll = 15ull + 255ull * (q - pos) + lb_byte(v, q);
+        pos = q + 1u;
+    }
+    if (ll > (uint64_t)(C - pos)) { T.nxt = BAD; return T; }
+    T.lit = pos;
+    T.ll = (uint32_t)ll;
+    pos += (uint32_t)ll;
+    if (pos == C) { T.nxt = END; return T; }
+    T.late = 1;
+    if (C - pos < 2u) { T.nxt = BAD; return T; }
+    T.off = lb_byte(v, pos) | (lb_byte(v, pos + 1u) << 8);
+    pos += 2u;
+    uint32_t ml = (t & 15u) + 4u;
+    if ((t & 15u) == 15u) {
+        const uint32_t q = lb_nz(v, pos);
+        if (q >= C) { T.nxt = BAD; return T; }
+        ml = 19u + 255u * (q - pos) + lb_byte(v, q);  // q - pos < C <= 4 MiB: no overflow
+        pos = q + 1u;
+    }
+    T.ml = ml;
+    if (pos >= C) {  // a token must follow a match: the sequence itself is complete (late = 2)
+        T.nxt = BAD;
+        T.late = 2;
+        return T;
+    }
+    T.late = 0;
+    T.nxt = pos;
+    return T;
+}
+
+__device__ __forceinline__ LbView lb_view(const uint8_t* src, const LbBlock& B, const uint32_t* nzg, uint32_t cs,
+                                          const uint8_t* s) {
+    LbView v;
+    v.g = src + B.src_off;
+    v.s = s;
+    v.nzg = nzg;
+    v.cs = cs;
+    v.C = B.C;
+    v.ns = B.C - cs < lb::kStage ? B.C - cs : lb::kStage;
+    v.chunk0 = B.chunk0;
+    v.nch = B.nchunks;
+    return v;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- classify
+__global__ __launch_bounds__(1024) void k_lb_classify(const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+                                                      uint32_t nunits, LbArgs A) {
+    __shared__ uint32_t sh[3][16];
+    __shared__ uint32_t carry[3];
+    __shared__ uint32_t ntaken;
+    const uint32_t t = threadIdx.x;
+    if (t < 3) carry[t] = 0;
+    if (t == 0) ntaken = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nunits; base += 1024) {
+        const uint32_t u = base + t;
+        bool cand = false;
+        DecBlock B{};
+        uint32_t bi = 0;
+        if (u < nunits) {
+            const DecUnit U = units[u];
+            if (U.n == 1) {
+                bi = U.first;
+                B = blk[bi];
+                cand = !(B.flags & (DB_STORED | DB_LINKED)) && B.limit >= kLbMinLimit && B.csize > 0 &&
+                       B.limit <= kLbMaxSteps * kLbStep;
+            }
+        }
+        const uint32_t nch = cand ? (B.csize + kLbChunk - 1) / kLbChunk : 0u;
+        uint32_t tot0, tot1;
+        const uint32_t p0 = wg_excl_add<uint32_t, 16>(cand ? 1u : 0u, sh[0], tot0) + carry[0];
+        const uint32_t p1 = wg_excl_add<uint32_t, 16>(nch, sh[1], tot1) + carry[1];
+        // prefixes grow monotonically, so the taken units are a prefix of the candidates
+        const bool take = cand && p0 + 1u <= A.lb_cap && p1 + nch <= A.chunk_cap;
+        if (u < nunits) A.unit_lb[u] = take ? 1 : 0;
+        if (take) {
+            LbBlock L;
+            L.src_off = B.src_off;
+            L.dst_off = B.dst_off;
+            L.C = B.csize;
+            L.limit = B.limit;
+            L.cap = B.cap;
+            L.blk = bi;
+            L.unit = u;
+            L.chunk0 = p1;
+            L.nchunks = nch;
+            L.pad = 0;
+            A.lbt[p0] = L;
+            A.lb_err[p0] = 0xFFFFFFFFu;
+            atomicMax(&ntaken, p0 + 1u);
+            for (uint32_t k = 0; k < nch; ++k) A.chunk_blk[p1 + k] = p0;
+        }
+        __syncthreads();
+        if (t == 0) {
+            carry[0] += tot0;
+            carry[1] += tot1;
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const uint32_t n = ntaken;  // the taken candidates are a prefix
+        A.ctl->nlb = n;
+        A.ctl->nchunks = n ? A.lbt[n - 1].chunk0 + A.lbt[n - 1].nchunks : 0u;
+    }
+}
+
+// ---------------------------------------------------------------- granules
+__global__ __launch_bounds__(256) void k_lb_gran(const uint8_t* __restrict__ src, LbArgs A) {
+    using namespace lb;
+    __shared__ uint32_t sm[kGpc];
+    const uint32_t c = blockIdx.x;
+    if (c >= A.ctl->nchunks) return;
+    const LbBlock B = A.lbt[A.chunk_blk[c]];
+    const uint8_t* g = src + B.src_off;
+    const uint32_t gi = threadIdx.x;
+    const uint32_t lo = (c - B.chunk0) * kLbChunk + gi * kGran;
+    const uint32_t hi = lo + kGran < B.C ? lo + kGran : B.C;
+    uint32_t f = INF;
+    for (uint32_t k = lo; k < hi; ++k)
+        if (g[k] != 255u) { f = k; break; }
+    sm[gi] = f;
+    __syncthreads();
+    for (uint32_t d = 1; d < kGpc; d <<= 1) {
+        const uint32_t o = gi + d < kGpc ? sm[gi + d] : INF;
+        __syncthreads();
+        sm[gi] = sm[gi] < o ? sm[gi] : o;
+        __syncthreads();
+    }
+    A.nzg[(size_t)c * kGpc + gi] = sm[gi];
+}
+
+// ---------------------------------------------------------------- chunk exits
+__global__ __launch_bounds__(1024) void k_lb_exit(const uint8_t* __restrict__ src, LbArgs A) {
+    using namespace lb;
+    __shared__ __attribute__((aligned(16))) uint8_t raw[kStage + 16];
+    __shared__ uint32_t nx[kLbChunk];
+    __shared__ uint16_t J[kLbChunk];
+    const uint32_t c = blockIdx.x;
+    if (c >= A.ctl->nchunks) return;
+    const LbBlock B = A.lbt[A.chunk_blk[c]];
+    const uint32_t cs = (c - B.chunk0) * kLbChunk;
+    const uint32_t n = B.C - cs < kLbChunk ? B.C - cs : kLbChunk;
+    const uint32_t ce = cs + n;
+    const LbView v = lb_view(src, B, A.nzg, cs, lb_stage(src + B.src_off, cs, B.C - cs < kStage ? B.C - cs : kStage, raw));
+    __syncthreads();
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t r = threadIdx.x + k * kT;
+        if (r < n) {
+            const LbTok T = lb_token(v, cs + r);
+            nx[r] = T.nxt;
+            J[r] = (uint16_t)(T.nxt < ce ? T.nxt - cs : r);  // END / BAD / beyond: the chain leaves here
+        }
+    }
+    __syncthreads();
+    // in-place pointer jumping to the last in-chunk node of each chain (values only move
+    // forward along the chain, so reading a fresher value is harmless)
+    for (uint32_t lev = 0; lev < 16; ++lev) {
+        bool ch = false;
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t r = threadIdx.x + k * kT;
+            if (r < n) {
+                const uint32_t j = J[r], jj = J[j];
+                if (jj != j) { J[r] = (uint16_t)jj; ch = true; }
+            }
+        }
+        if (!__syncthreads_or(ch)) break;
+    }
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t r = threadIdx.x + k * kT;
+        if (r < n) A.E[(size_t)c * kLbChunk + r] = nx[J[r]];
+    }
+}
+
+// ---------------------------------------------------------------- chunk entries
+__global__ void k_lb_entry(LbArgs A) {
+    using namespace lb;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.ctl->nlb) return;
+    const LbBlock B = A.lbt[i];
+    uint32_t e = 0, c = 0;
+    while (c < B.nchunks && e < B.C) {
+        const uint32_t cc = e / kLbChunk;
+        for (; c < cc; ++c) A.entry[B.chunk0 + c] = NONE;
+        const uint32_t rel = e - cc * kLbChunk;
+        A.entry[B.chunk0 + cc] = rel;
+        c = cc + 1u;
+        e = A.E[(size_t)(B.chunk0 + cc) * kLbChunk + rel];
+    }
+    for (; c < B.nchunks; ++c) A.entry[B.chunk0 + c] = NONE;
+}
+
+// ---------------------------------------------------------------- token marks
+__global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ src, LbArgs A) {
+    using namespace lb;
+    __shared__ __attribute__((aligned(16))) uint8_t raw[kStage + 16];
+    __shared__ uint16_t Ja[kLbChunk], Jb[kLbChunk];
+    __shared__ uint8_t mk[kLbChunk];
+    __shared__ uint32_t shc[16];
+    __shared__ uint64_t shs[16];
+    __shared__ uint32_t bad_s;
+    const uint32_t c = blockIdx.x;
+    const bool live = c < A.ctl->nchunks;
+    const uint32_t e = live ? A.entry[c] : NONE;
+    if (e == NONE) {  // no token of the block starts in this chunk (or a chunk beyond the count)
+        if (threadIdx.x == 0) { A.ntok[c] = 0; A.slsum[c] = 0; A.badrel[c] = NONE; }
+        if (live)
+            for (uint32_t w = threadIdx.x; w < kWords; w += kT) A.bits[(size_t)c * kWords + w] = 0;
+        return;
+    }
+    const LbBlock B = A.lbt[A.chunk_blk[c]];
+    const uint32_t cs = (c - B.chunk0) * kLbChunk;
+    const uint32_t n = B.C - cs < kLbChunk ? B.C - cs : kLbChunk;
+    const uint32_t ce = cs + n;
+    const LbView v = lb_view(src, B, A.nzg, cs, lb_stage(src + B.src_off, cs, B.C - cs < kStage ? B.C - cs : kStage, raw));
+    if (threadIdx.x == 0) bad_s = NONE;
+    __syncthreads();
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t r = threadIdx.x + k * kT;
+        if (r < n) {
+            const LbTok T = lb_token(v, cs + r);
+            Ja[r] = (uint16_t)(T.nxt < ce ? T.nxt - cs : r);
+            mk[r] = r == e ? 1 : 0;
+        }
+    }
+    // marks reachable from the entry: level k adds J_k(T_k) with J_k = nxt^(2^k) (exact powers:
+    // the jump table is double-buffered; marks may be set early, they are still chain nodes)
+    uint16_t* Jc = Ja;
+    uint16_t* Jn = Jb;
+    for (uint32_t lev = 0; lev < kLevels; ++lev) {
+        __syncthreads();
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t r = threadIdx.x + k * kT;
+            if (r < n) {
+                const uint32_t j = Jc[r];
+                if (mk[r]) mk[j] = 1;
+                Jn[r] = Jc[j];
+            }
+        }
+        uint16_t* tmp = Jc; Jc = Jn; Jn = tmp;
+    }
+    __syncthreads();
+    uint32_t cnt = 0;
+    uint64_t sl = 0;
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t r = threadIdx.x + k * kT;
+        bool tok = false;
+        if (r < n && mk[r]) {
+            const LbTok T = lb_token(v, cs + r);
+            if (T.nxt == BAD) {
+                bad_s = r;  // the chain's last node (unique)
+            } else {
+                tok = true;
+                ++cnt;
+                const uint64_t s = (uint64_t)T.ll + T.ml;
+                sl += s < (uint64_t)B.limit + 1u ? s : (uint64_t)B.limit + 1u;
+            }
+        }
+        const uint64_t bm = __ballot(tok);
+        // wave w covers positions k*kT + 64w .. +63
+        if (lane64() == 0) {
+            const uint32_t w0 = (k * kT + (threadIdx.x & ~63u)) >> 5;
+            A.bits[(size_t)c * kWords + w0] = (uint32_t)bm;
+            A.bits[(size_t)c * kWords + w0 + 1] = (uint32_t)(bm >> 32);
+        }
+    }
+    uint32_t ctot;
+    uint64_t stot;
+    (void)wg_excl_add<uint32_t, 16>(cnt, shc, ctot);
+    (void)wg_excl_add<uint64_t, 16>(sl, shs, stot);
+    if (threadIdx.x == 0) {
+        A.ntok[c] = ctot;
+        A.slsum[c] = stot < 0xFFFFFFFFull ? (uint32_t)stot : 0xFFFFFFFFu;
+        A.badrel[c] = bad_s;
+    }
+}
+
+// ---------------------------------------------------------------- sequence table
+__device__ __forceinline__ uint32_t lb_check(uint64_t produced, uint32_t ll, uint32_t ml, uint32_t off, bool last,
+                                             uint32_t limit, uint32_t cap) {
+    // dec_block's check(): precedence lowest first, later conditions override
+    const int64_t have = (int64_t)produced + ll;
+    uint32_t st = S3HC_OK;
+    st = (!last && (int64_t)ml > (int64_t)cap - have) ? S3HC_DST_TOO_SMALL : st;
+    st = (!last && (int64_t)ml > (int64_t)limit - have) ? S3HC_CORRUPT : st;
+    st = (!last && (off == 0 || (int64_t)off > have)) ? S3HC_CORRUPT : st;
+    st = ((int64_t)ll > (int64_t)cap - (int64_t)produced) ? S3HC_DST_TOO_SMALL : st;
+    st = ((int64_t)ll > (int64_t)limit - (int64_t)produced) ? S3HC_CORRUPT : st;
+    return st;
+}
+
+__global__ __launch_bounds__(1024) void k_lb_seq(const uint8_t* __restrict__ src, LbArgs A) {
+    using namespace lb;
+    __shared__ __attribute__((aligned(16))) uint8_t raw[kStage + 16];
+    __shared__ uint32_t shc[16];
+    __shared__ uint64_t shs[16];
+    const uint32_t c = blockIdx.x;
+    if (c >= A.ctl->nchunks || A.entry[c] == NONE) return;
+    const uint32_t bi = A.chunk_blk[c];
+    const LbBlock B = A.lbt[bi];
+    const uint32_t cs = (c - B.chunk0) * kLbChunk;
+    const uint32_t n = B.C - cs < kLbChunk ? B.C - cs : kLbChunk;
+    const LbView v = lb_view(src, B, A.nzg, cs, lb_stage(src + B.src_off, cs, B.C - cs < kStage ? B.C - cs : kStage, raw));
+    __syncthreads();
+    // thread t owns positions [kPer*t, kPer*t + kPer) (contiguous: ranks follow position order)
+    const uint32_t r0 = kPer * threadIdx.x;
+    const uint32_t wv = A.bits[(size_t)c * kWords + (r0 >> 5)];
+    const uint32_t m = (wv >> (r0 & 31u)) & ((1u << kPer) - 1u);
+    uint32_t cnt = 0;
+    uint64_t sl = 0;
+    for (uint32_t k = 0; k < kPer; ++k) {
+        if ((m >> k) & 1u) {
+            const LbTok T = lb_token(v, cs + r0 + k);
+            ++cnt;
+            const uint64_t s = (uint64_t)T.ll + T.ml;
+            sl += s < (uint64_t)B.limit + 1u ? s : (uint64_t)B.limit + 1u;
+        }
+    }
+    uint32_t ctot;
+    uint64_t stot;
+    uint32_t rank = wg_excl_add<uint32_t, 16>(cnt, shc, ctot);
+    uint64_t opre = wg_excl_add<uint64_t, 16>(sl, shs, stot);
+    const uint64_t tb0 = A.tokbase[B.chunk0];
+    const uint64_t ob0 = A.outbase[B.chunk0];
+    const uint64_t gbase = A.tokbase[c];
+    const uint32_t brank0 = (uint32_t)(gbase - tb0);
+    uint64_t produced = A.outbase[c] - ob0 + opre;
+    uint32_t bad = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < kPer; ++k) {
+        if ((m >> k) & 1u) {
+            const LbTok S = lb_token(v, cs + r0 + k);
+            const bool last = S.nxt == END;
+            const uint32_t st = lb_check(produced, S.ll, S.ml, S.off, last, B.limit, B.cap);
+            const uint32_t br = brank0 + rank;
+            if (st != S3HC_OK && bad == 0xFFFFFFFFu) bad = (br << 3) | st;
+            A.seq4[gbase + rank] = make_uint4(produced < 0xFFFFFFFFull ? (uint32_t)produced : 0xFFFFFFFFu, S.lit,
+                                              S.ll, S.ml);
+            A.seqoff[gbase + rank] = (uint16_t)S.off;
+            // execution steps whose first byte this sequence produces
+            const uint64_t sl1 = (uint64_t)S.ll + S.ml;
+            if (st == S3HC_OK && sl1) {
+                const uint64_t r_lo = (produced + kLbStep - 1) / kLbStep, r_hi = (produced + sl1 - 1) / kLbStep;
+                for (uint64_t q = r_lo; q <= r_hi && q < kLbMaxSteps; ++q) A.rfirst[(size_t)bi * kLbMaxSteps + q] = br;
+            }
+            produced += sl1 < (uint64_t)B.limit + 1u ? sl1 : (uint64_t)B.limit + 1u;
+            ++rank;
+        }
+    }
+    if (bad != 0xFFFFFFFFu) atomicMin(&A.lb_err[bi], bad);
+    if (threadIdx.x == 0) {
+        const uint32_t br = A.badrel[c];
+        if (br != NONE) {
+            // the malformed token ending the chain: after every sequence of the block
+            const LbTok S = lb_token(v, cs + br);
+            const uint64_t pr = A.outbase[c] - ob0 + stot;
+            uint32_t st = S3HC_CORRUPT, rk = brank0 + ctot;
+            if (S.late == 1) {  // literal checks, then the cut-off offset / length run
+                st = ((int64_t)S.ll > (int64_t)B.cap - (int64_t)pr) ? S3HC_DST_TOO_SMALL : st;
+                st = ((int64_t)S.ll > (int64_t)B.limit - (int64_t)pr) ? S3HC_CORRUPT : st;
+            } else if (S.late == 2) {  // a full sequence, then the missing token
+                const uint32_t sc = lb_check(pr, S.ll, S.ml, S.off, false, B.limit, B.cap);
+                st = sc != S3HC_OK ? sc : S3HC_CORRUPT;
+                rk += sc != S3HC_OK ? 0u : 1u;
+            }
+            atomicMin(&A.lb_err[bi], (rk << 3) | st);
+        }
+    }
+    (void)n;
+}
+
+// ---------------------------------------------------------------- finish parse
+__global__ void k_lb_fin(LbArgs A, uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.ctl->nlb) return;
+    const LbBlock B = A.lbt[i];
+    const uint32_t cl = B.chunk0 + B.nchunks - 1;
+    const uint64_t size = A.outbase[cl] + A.slsum[cl] - A.outbase[B.chunk0];
+    const uint32_t err = A.lb_err[i];
+    const uint32_t stat = err == 0xFFFFFFFFu ? (uint32_t)S3HC_OK : (err & 7u);
+    A.lb_size[i] = stat == S3HC_OK ? (uint32_t)size : 0u;
+    A.lb_stat[i] = stat;
+    A.lb_tok0[i] = (uint32_t)A.tokbase[B.chunk0];
+    A.lb_ntok[i] = (uint32_t)(A.tokbase[cl] + A.ntok[cl] - A.tokbase[B.chunk0]);
+    blk_out[B.blk] = stat == S3HC_OK ? (uint32_t)size : 0u;
+    blk_status[B.blk] = (int32_t)stat;
+}
+
+// ---------------------------------------------------------------- execute
+// One 1024-thread workgroup per block writes the block in kLbStep-byte steps, in order. LDS
+// keeps a 64 KiB ring of the block's recent output (match sources) and the step's sequences.
+// Each byte of a step gets its value right away when it is a literal or its match source lies
+// before the step (ring, or HBM for the few sources the step itself is overwriting in the
+// ring); otherwise it gets a pointer to its source inside the step, and the pointers are jumped
+// (a final source gives the value) until every byte is final: every chain ends in a literal or
+// a byte before the step, so no byte is left over. Then the step is flushed to HBM.
+__global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, LbArgs A) {
+    using namespace lb;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    __shared__ __attribute__((aligned(16))) uint32_t ptr[kLbStep];
+    __shared__ __attribute__((aligned(16))) uint16_t marks[kLbStep];
+    __shared__ __attribute__((aligned(16))) uint4 sq[kMaxSeqS];
+    __shared__ uint16_t so[kMaxSeqS];
+    __shared__ uint32_t rf[kLbMaxSteps + 1];
+    __shared__ uint32_t shm[16];
+    const uint32_t i = blockIdx.x;
+    if (i >= A.ctl->nlb || A.lb_stat[i] != S3HC_OK) return;
+    const LbBlock B = A.lbt[i];
+    const uint32_t size = A.lb_size[i];
+    const uint32_t tok0 = A.lb_tok0[i], ntok = A.lb_ntok[i];
+    const uint8_t* g = src + B.src_off;
+    uint8_t* ob = dst + B.dst_off;
+    const uint32_t t = threadIdx.x;
+    const int lane = lane64();
+    constexpr uint32_t kMask = kRing - 1;
+    const uint32_t nsteps = (size + kLbStep - 1) / kLbStep;
+#ifdef S3HC_LBPROF
+    uint64_t lbp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t lbt = __builtin_amdgcn_s_memtime();
+    // phase k accumulates the time since the previous mark (0: step loop overhead)
+#define LB_T(k) { const uint64_t n_ = __builtin_amdgcn_s_memtime(); lbp[(k) == 0 ? 9 : (k) - 1] += n_ - lbt; lbt = n_; }
+#define LB_ADD(k, v) lbp[k] += (v)
+#else
+#define LB_T(k)
+#define LB_ADD(k, v)
+#endif
+    // step q covers sequences [rf[q], rf[q+1]) (+1 when the next step starts inside one)
+    for (uint32_t q = t; q <= nsteps; q += kXT)
+        rf[q] = q < nsteps ? A.rfirst[(size_t)i * kLbMaxSteps + q] : ntok;
+    __syncthreads();
+    // sequences of a step: loaded into registers one step ahead, stored (with the start marks)
+    // into LDS once the current step no longer needs them (kMaxSeqS <= 3 x kXT)
+    static_assert(kMaxSeqS <= 3 * kXT, "three sequences per thread and step");
+    uint4 pe0 = make_uint4(0, 0, 0, 0), pe1 = pe0, pe2 = pe0;
+    uint32_t po0 = 0, po1 = 0, po2 = 0;
+#define LB_STEP_SEQS(q, s0, ns)                                              \
+    const uint32_t s0 = rf[q];                                               \
+    const uint32_t ns = ((q) + 1 < nsteps ? rf[(q) + 1] + 1u : ntok) - s0 < kMaxSeqS \
+                            ? ((q) + 1 < nsteps ? rf[(q) + 1] + 1u : ntok) - s0      \
+                            : kMaxSeqS;
+#define LB_PREFETCH(q)                                                                   \
+    {                                                                                    \
+        LB_STEP_SEQS(q, s0p, nsp)                                                        \
+        const uint32_t j0 = t, j1 = t + kXT, j2 = t + 2 * kXT;                           \
+        const uint32_t g0 = tok0 + s0p + (j0 < nsp ? j0 : 0u), g1 = tok0 + s0p + (j1 < nsp ? j1 : 0u); \
+        const uint32_t g2 = tok0 + s0p + (j2 < nsp ? j2 : 0u);                           \
+        pe0 = A.seq4[g0]; pe1 = A.seq4[g1]; pe2 = A.seq4[g2];                            \
+        po0 = A.seqoff[g0]; po1 = A.seqoff[g1]; po2 = A.seqoff[g2];                      \
+    }
+#define LB_PUT(j, pe, po, R)                                                             \
+    if ((j) < nsi) {                                                                     \
+        sq[j] = pe;                                                                      \
+        so[j] = (uint16_t)(po);                                                          \
+        const uint32_t rel_ = (pe).x > (R) ? (pe).x - (R) : 0u;                          \
+        if (rel_ < kLbStep && ((j) == 0 || (pe).x > (R))) marks[rel_] = (uint16_t)((j) + 1); \
+    }
+#define LB_INSTALL(q)                                                                    \
+    {                                                                                    \
+        LB_STEP_SEQS(q, s0i, nsi)                                                        \
+        const uint32_t Rq = (q) * kLbStep;                                               \
+        (void)s0i;                                                                       \
+        LB_PUT(t, pe0, po0, Rq) LB_PUT(t + kXT, pe1, po1, Rq) LB_PUT(t + 2 * kXT, pe2, po2, Rq) \
+    }
+    ((uint4*)marks)[t] = make_uint4(0, 0, 0, 0);  // kLbStep u16 = kXT x 16 B
+    LB_PREFETCH(0)
+    __syncthreads();
+    LB_INSTALL(0)
+    if (1 < nsteps) LB_PREFETCH(1)
+    __syncthreads();
+    for (uint32_t q = 0; q < nsteps; ++q) {
+        const uint32_t R = q * kLbStep;
+        LB_T(0);
+        LB_ADD(7, 1);
+        // owner of each byte: running max of the start marks (thread t: bytes 8t .. 8t+7)
+        const uint4 m4 = ((const uint4*)marks)[t];
+        const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
+        uint32_t mx = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t lo = mw[k] & 0xFFFFu, hi = mw[k] >> 16;
+            mx = lo > mx ? lo : mx;
+            mx = hi > mx ? hi : mx;
+        }
+        uint32_t inc = mx;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d);
+            if (lane >= d) inc = y > inc ? y : inc;
+        }
+        if (lane == 63) shm[t >> 6] = inc;
+        __syncthreads();
+        uint32_t cur = __shfl_up(inc, 1);
+        if (lane == 0) cur = 0;
+        for (uint32_t w = 0; w < (t >> 6); ++w) cur = shm[w] > cur ? shm[w] : cur;
+        {
+            // owners written over the marks (then read with the interleaved byte mapping)
+            uint32_t ow[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t lo = mw[k] & 0xFFFFu, hi = mw[k] >> 16;
+                cur = lo > cur ? lo : cur;
+                const uint32_t o0 = cur;
+                cur = hi > cur ? hi : cur;
+                ow[k] = o0 | (cur << 16);
+            }
+            ((uint4*)marks)[t] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        }
+        __syncthreads();
+        // classify the bytes (thread t: bytes t + kXT*j, so lanes touch consecutive bytes):
+        // literal (input address), source before the step (ring value: the ring still holds
+        // [R - 64 KiB, R) until this step's bytes are stored below, and LZ4 offsets are
+        // < 64 KiB), source inside the step (pointer). An overlapping copy's source is taken in
+        // its first period, or in its latest period before the step when there is one.
+        LB_T(1);
+        uint32_t la[kXPer], pv[kXPer], vb[kXPer];
+        uint32_t litm = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) {
+            const uint32_t l = t + kXT * j;
+            const uint32_t x = R + l;
+            pv[j] = FIN;
+            la[j] = 0;
+            vb[j] = 0;
+            if (x < size) {
+                const uint32_t k = marks[l] - 1u;
+                const uint4 e = sq[k];
+                const uint32_t rel = x - e.x;
+                if (rel < e.z) {
+                    la[j] = e.y + rel;
+                    litm |= 1u << j;
+                } else {
+                    const uint32_t off = so[k];
+                    uint32_t y = x - off;
+                    const uint32_t ee = rel - e.z;  // position inside the match
+                    if (y >= R && ee >= off) {
+                        const uint32_t m0 = e.x + e.z;
+                        const uint32_t yf = m0 - off + ee % off;
+                        y = yf < R ? x - ((x - R) / off + 1u) * off : yf;
+                    }
+                    if (y >= R) pv[j] = y - R;
+                    else vb[j] = ring[y & kMask];
+                }
+            }
+        }
+        // literal loads (coalesced across lanes), all issued before the first use
+        uint32_t lv[kXPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) lv[j] = g[(litm >> j) & 1u ? la[j] : 0u];
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) vb[j] = (litm >> j) & 1u ? lv[j] & 0xFFu : vb[j];
+        LB_T(2);
+        __syncthreads();  // every read of the ring slots this step overwrites, and of marks/sq, is done
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) {
+            const uint32_t l = t + kXT * j;
+            ring[(R + l) & kMask] = (uint8_t)vb[j];
+            ptr[l] = pv[j];
+        }
+        ((uint4*)marks)[t] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        LB_T(3);
+        if (q + 1 < nsteps) LB_INSTALL(q + 1)
+        if (q + 2 < nsteps) LB_PREFETCH(q + 2)
+        LB_T(4);
+        // chains inside the step: each round every pending byte reads its source's pointer; a
+        // final source gives the value, a pending one is jumped over (pointer doubling). A
+        // thread's pointers stay in registers (it is their only writer); values are stored
+        // before the pointers that mark them final (a wave's LDS operations complete in order).
+        uint32_t pend = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) pend |= (pv[j] != FIN ? 1u : 0u) << j;
+        for (uint32_t it = 0; it < 20; ++it) {
+#ifdef S3HC_LBPROF
+            const uint64_t tb0 = __builtin_amdgcn_s_memtime();
+#endif
+            if (__syncthreads_or(pend != 0) == 0) break;
+            LB_ADD(8, 1);
+#ifdef S3HC_LBPROF
+            const uint64_t tb1 = __builtin_amdgcn_s_memtime();
+            lbp[10] += tb1 - tb0;
+#endif
+            if (pend) {
+                uint32_t pp[kXPer];
+#pragma unroll
+                for (uint32_t j = 0; j < kXPer; ++j) pp[j] = (pend >> j) & 1u ? ptr[pv[j]] : 0u;
+                uint32_t rv[kXPer];
+                uint32_t fin = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < kXPer; ++j) {
+                    const bool f = ((pend >> j) & 1u) && pp[j] == FIN;
+                    fin |= (f ? 1u : 0u) << j;
+                    rv[j] = f ? ring[(R + pv[j]) & kMask] : 0u;
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < kXPer; ++j)
+                    if ((fin >> j) & 1u) ring[(R + t + kXT * j) & kMask] = (uint8_t)rv[j];
+                if (fin) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#pragma unroll
+                for (uint32_t j = 0; j < kXPer; ++j) {
+                    if ((pend >> j) & 1u) {
+                        pv[j] = (fin >> j) & 1u ? FIN : pp[j];
+                        ptr[t + kXT * j] = pv[j];
+                    }
+                }
+                pend &= ~fin;
+            }
+#ifdef S3HC_LBPROF
+            lbp[11] += __builtin_amdgcn_s_memtime() - tb1;
+#endif
+            __syncthreads();
+        }
+        LB_T(5);
+        // flush the step (thread t: dwords t and t + kXT of the step)
+        const bool al = (((uintptr_t)(ob + R)) & 3u) == 0;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t x0 = R + 4u * (t + kXT * h);
+            const uint32_t v4 = *(const uint32_t*)(ring + (x0 & kMask));
+            if (al && x0 + 4u <= size) {
+                *(uint32_t*)(ob + x0) = v4;
+            } else {
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (x0 + j < size) ob[x0 + j] = (uint8_t)(v4 >> (8 * j));
+            }
+        }
+        LB_T(6);
+    }
+#ifdef S3HC_LBPROF
+    if (t == 0)
+        for (int k = 0; k < 12; ++k) atomicAdd(&g_lbprof[k], (unsigned long long)lbp[k]);
+#endif
+}
+
+#undef LB_T
+#undef LB_ADD
+#undef LB_STEP_SEQS
+#undef LB_PREFETCH
+#undef LB_PUT
+#undef LB_INSTALL
+
+// ================================================================ launchers
+static inline uint32_t cdiv_lb(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+hipError_t launch_scan(const uint32_t* in, uint32_t n, uint64_t* out, uint64_t* total, hipStream_t st);
+
+// Parse stage: classify the units, tokenize, build the sequence table, statuses and sizes of
+// the taken blocks. Must precede k_decode_units (it reads unit_lb).
+hipError_t launch_lb_parse(const LbArgs& A, const uint8_t* src, const DecBlock* blk, const DecUnit* units,
+                           uint32_t nunits, uint32_t* blk_out, int32_t* blk_status, hipStream_t st) {
+    hipLaunchKernelGGL(k_lb_classify, dim3(1), dim3(1024), 0, st, blk, units, nunits, A);
+    hipLaunchKernelGGL(k_lb_gran, dim3(A.chunk_cap), dim3(lb::kGpc), 0, st, src, A);
+    hipLaunchKernelGGL(k_lb_exit, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
+    hipLaunchKernelGGL(k_lb_entry, dim3(cdiv_lb(A.lb_cap, 64)), dim3(64), 0, st, A);
+    hipLaunchKernelGGL(k_lb_mark, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
+    hipError_t e = launch_scan(A.ntok, A.chunk_cap, A.tokbase, A.total, st);
+    if (e != hipSuccess) return e;
+    e = launch_scan(A.slsum, A.chunk_cap, A.outbase, A.total + 1, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_lb_seq, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
+    hipLaunchKernelGGL(k_lb_fin, dim3(cdiv_lb(A.lb_cap, 256)), dim3(256), 0, st, A, blk_out, blk_status);
+    return hipGetLastError();
+}
+
+// Execute stage: one workgroup per taken block.
+hipError_t launch_lb_exec(const LbArgs& A, const uint8_t* src, uint8_t* dst, hipStream_t st) {
+    hipLaunchKernelGGL(k_lb_run, dim3(A.lb_cap), dim3(lb::kXT), 0, st, src, dst, A);
+    return hipGetLastError();
+}
+}  // namespace s3hc
+
+#ifdef S3HC_LBPROF
+extern "C" int s3hc_diag_lbprof(unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(s3hc::g_lbprof), sizeof(unsigned long long) * 12) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[12] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(s3hc::g_lbprof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -84,4 +84,59 @@ struct DecUnit {         // a run of blocks decoded in order by one wave
     uint32_t n;
 };
 
+// ---- large-block decode ---------------------------------
+// Blocks whose frame allows more than 64 KiB (BD 0x50 / 0x70: what lz4_flex writes for the
+// reference's ~1 MiB cache batches) are decoded by a whole workgroup each instead of one wave:
+// the token chain is found by pointer doubling over 16 Ki-position chunks of the compressed
+// block (all chunks of all blocks in parallel), the sequence table comes from scans, and one
+// 1024-thread workgroup per block then writes the output in 8 KiB steps, resolving each step's
+// match chains in LDS by pointer jumping against a 64 KiB ring of recent output.
+constexpr uint32_t kLbChunk = 16384;      // compressed positions per tokenizing workgroup
+constexpr uint32_t kLbStep = 8192;        // output bytes per step of the executing workgroup
+constexpr uint32_t kLbMaxSteps = 512;     // steps of one block (4 MiB / kLbStep)
+constexpr uint32_t kLbMinLimit = 65537;   // frame max block size above 64 KiB selects the path
+
+struct LbBlock {         // 48 bytes; one per block taken by the large-block path
+    uint64_t src_off;    // compressed payload
+    uint64_t dst_off;    // output
+    uint32_t C, limit, cap;
+    uint32_t blk;        // DecBlock index (blk_out / blk_status)
+    uint32_t unit;       // DecUnit index (unit_lb flag)
+    uint32_t chunk0, nchunks;
+    uint32_t pad;
+};
+
+struct LbCtl {           // device-side counters of one large-block launch
+    uint32_t nlb, nchunks, pad0, pad1;
+};
+
+// Device scratch of the large-block path (sized by the host: lb_cap blocks, chunk_cap chunks;
+// blocks beyond a cap are decoded by the one-wave decoder instead).
+struct LbArgs {
+    uint32_t lb_cap, chunk_cap;
+    LbBlock* lbt;
+    LbCtl* ctl;
+    uint8_t* unit_lb;      // per unit: 1 = decoded by this path
+    uint32_t* chunk_blk;   // chunk -> LB block
+    uint32_t* nzg;         // per chunk, per 64-byte granule: first non-255 byte at or after it (chunk-local)
+    uint32_t* E;           // per compressed position: chain exit of its chunk
+    uint32_t* entry;       // per chunk: first chain position (chunk-relative) or ~0
+    uint32_t* bits;        // per chunk: token bitmap
+    uint32_t* ntok;        // per chunk: sequences
+    uint32_t* slsum;       // per chunk: output bytes (saturating)
+    uint32_t* badrel;      // per chunk: malformed token ending the chain, or ~0
+    uint64_t* tokbase;     // exclusive scans of ntok / slsum
+    uint64_t* outbase;
+    uint64_t* total;       // scan totals (2 x u64)
+    uint4* seq4;           // per sequence: out, lit, ll, ml
+    uint16_t* seqoff;      // per sequence: match offset
+    uint32_t* lb_err;      // per LB block: min(rank << 3 | status) of failing sequences
+    uint32_t* lb_size;     // per LB block: decoded bytes (0 unless OK)
+    uint32_t* lb_stat;     // per LB block: status
+    uint32_t* lb_tok0;     // per LB block: global index of its first sequence
+    uint32_t* lb_ntok;
+    uint32_t* rfirst;      // per LB block x kLbMaxSteps: sequence covering each step's first byte
+};
+
+
 }  // namespace s3hc

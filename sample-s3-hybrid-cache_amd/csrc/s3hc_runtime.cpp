@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -24,7 +25,10 @@
 namespace s3hc {
 hipError_t launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_decode_units(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*,
-                               int32_t*, hipStream_t);
+                               int32_t*, const uint8_t*, hipStream_t);
+hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*, int32_t*,
+                           hipStream_t);
+hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, hipStream_t);
 hipError_t launch_enc_parse(const uint8_t*, const EncBlock*, const uint2*, uint32_t, const uint64_t*, const uint32_t*,
                             uint32_t, uint32_t*, uint2*, SegSummary*, hipStream_t);
 hipError_t launch_enc_sizes(const EncBlock*, uint32_t, const SegSummary*, SegPlace*, uint32_t*, uint32_t*,
@@ -114,6 +118,76 @@ template <class T> static hipError_t upload(DevBuf& b, const std::vector<T>& v, 
     return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st);
 }
 
+// ------------------------------------------------- large-block decode scratch
+// Caps of the large-block path (s3hc_lb.hip) for one decode launch. They only size scratch:
+// a block beyond any cap is decoded by the one-wave decoder instead.
+struct LbCaps {
+    uint32_t lb = 0, chunks = 0;
+    void add_block(uint32_t csize) {
+        ++lb;
+        chunks += (csize + kLbChunk - 1) / kLbChunk;
+    }
+};
+static bool lb_candidate(const DecBlock& D, bool unit_single) {
+    return unit_single && !(D.flags & (DB_STORED | DB_LINKED)) && D.limit >= kLbMinLimit && D.csize > 0 &&
+           D.limit <= kLbMaxSteps * kLbStep;
+}
+
+struct LbScratch {
+    DevBuf lbt, ctl, unit_lb, chunk_blk, nzg, E, entry, bits, ntok, slsum, badrel, tokbase, outbase, total, seq4,
+        seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst;
+    LbArgs a{};
+    bool active = false;
+    hipError_t prepare(uint32_t nunits, const LbCaps& c) {
+        active = c.lb > 0 && c.chunks > 0;
+        if (!active) return hipSuccess;
+        const size_t nch = c.chunks, nlb = c.lb;
+        const size_t nseq = nch * (kLbChunk / 3 + 2);
+        hipError_t e = hipSuccess;
+#define LBE(buf, bytes) if ((e = (buf).ensure((size_t)(bytes) + 64)) != hipSuccess) return e;
+        LBE(lbt, nlb * sizeof(LbBlock)) LBE(ctl, sizeof(LbCtl)) LBE(unit_lb, nunits) LBE(chunk_blk, nch * 4)
+        LBE(nzg, nch * (kLbChunk / 64) * 4) LBE(E, nch * kLbChunk * 4) LBE(entry, nch * 4)
+        LBE(bits, nch * (kLbChunk / 32) * 4) LBE(ntok, nch * 4) LBE(slsum, nch * 4) LBE(badrel, nch * 4)
+        LBE(tokbase, nch * 8) LBE(outbase, nch * 8) LBE(total, 32) LBE(seq4, nseq * 16) LBE(seqoff, nseq * 2)
+        LBE(lb_err, nlb * 4) LBE(lb_size, nlb * 4) LBE(lb_stat, nlb * 4) LBE(lb_tok0, nlb * 4) LBE(lb_ntok, nlb * 4)
+        LBE(rfirst, nlb * kLbMaxSteps * 4)
+#undef LBE
+        a.lb_cap = c.lb;
+        a.chunk_cap = c.chunks;
+        a.lbt = lbt.as<LbBlock>(); a.ctl = ctl.as<LbCtl>(); a.unit_lb = unit_lb.as<uint8_t>();
+        a.chunk_blk = chunk_blk.as<uint32_t>(); a.nzg = nzg.as<uint32_t>(); a.E = E.as<uint32_t>();
+        a.entry = entry.as<uint32_t>(); a.bits = bits.as<uint32_t>(); a.ntok = ntok.as<uint32_t>();
+        a.slsum = slsum.as<uint32_t>(); a.badrel = badrel.as<uint32_t>(); a.tokbase = tokbase.as<uint64_t>();
+        a.outbase = outbase.as<uint64_t>(); a.total = total.as<uint64_t>(); a.seq4 = seq4.as<uint4>();
+        a.seqoff = seqoff.as<uint16_t>(); a.lb_err = lb_err.as<uint32_t>(); a.lb_size = lb_size.as<uint32_t>();
+        a.lb_stat = lb_stat.as<uint32_t>(); a.lb_tok0 = lb_tok0.as<uint32_t>(); a.lb_ntok = lb_ntok.as<uint32_t>();
+        a.rfirst = rfirst.as<uint32_t>();
+        return hipSuccess;
+    }
+};
+
+// Block decode of a batch: large blocks by the large-block path (when L is active), the rest
+// one wave per unit.
+static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, const DecBlock* blk,
+                                const DecUnit* units, uint32_t nunits, uint32_t* blk_out, int32_t* blk_status,
+                                hipStream_t st) {
+    // S3HC_LB_DISABLE (tests, comparisons): every block goes to the one-wave decoder
+    const bool lb = L && L->active && nunits && !getenv("S3HC_LB_DISABLE");
+    hipError_t e;
+    if (lb && (e = launch_lb_parse(L->a, src, blk, units, nunits, blk_out, blk_status, st)) != hipSuccess) return e;
+    if ((e = launch_decode_units(src, dst, blk, units, nunits, blk_out, blk_status, lb ? L->a.unit_lb : nullptr,
+                                 st)) != hipSuccess)
+        return e;
+    if (lb && (e = launch_lb_exec(L->a, src, dst, st)) != hipSuccess) return e;
+    if (lb && getenv("S3HC_LB_TRACE")) {  // diagnostics: blocks and chunks taken
+        LbCtl c;
+        if ((e = hipMemcpyAsync(&c, L->a.ctl, sizeof c, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        fprintf(stderr, "[s3hc lb] blocks %u chunks %u\n", c.nlb, c.nchunks);
+    }
+    return hipSuccess;
+}
+
 // --------------------------------------------------------------- context
 struct TimedSpan {
     std::string name;
@@ -142,6 +216,7 @@ struct s3hc_ctx {
     DevBuf d_in, d_out;
     s3hc_plan* host_plan = nullptr;
     DevBuf d_blocks, d_units, d_blk_out, d_blk_status, d_rng_off, d_rng_len, d_hash;
+    LbScratch lb;
     ~s3hc_ctx();
 };
 
@@ -173,6 +248,7 @@ struct s3hc_plan {
     uint32_t blk_cap = 0;
     DevBuf d_frame_off, d_frame_len, d_dst_off, d_dst_cap;
     DevBuf d_nblk, d_fstatus, d_blk_base, d_fwant, d_dblocks, d_units, d_blk_out, d_blk_status, d_got;
+    LbScratch lb;                        // large-block path scratch (frames allowing > 64 KiB blocks)
 };
 
 void KTimer::begin(const char* name) {
@@ -431,6 +507,16 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
     HIPCHK(P->d_units.ensure((size_t)P->blk_cap * sizeof(DecUnit) + 16));
     HIPCHK(P->d_blk_out.ensure((size_t)P->blk_cap * 4 + 16));
     HIPCHK(P->d_blk_status.ensure((size_t)P->blk_cap * 4 + 16));
+    // large blocks: the device walk finds them; frames with room for more than 64 KiB may hold
+    // some (well-formed frames fill every block but the last, so <= cap / 256 KiB + 1 of them)
+    LbCaps lc;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (dst_cap[i] <= 65536u) continue;
+        const uint32_t nl = dst_cap[i] / 262144u + 1u;
+        lc.lb += nl;
+        lc.chunks += frame_len[i] / kLbChunk + nl;
+    }
+    HIPCHK(P->lb.prepare(P->blk_cap, lc));
     HIPCHK(hipStreamSynchronize(st));
     *out = P.release();
     return S3HC_OK;
@@ -456,8 +542,8 @@ extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src
                               P->d_fwant.as<uint32_t>(), st));
     T.end();
     T.begin("decode");
-    HIPCHK(launch_decode_units(d_src, d_dst, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(), P->blk_cap,
-                               P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st));
+    HIPCHK(decode_launch(&P->lb, d_src, d_dst, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(), P->blk_cap,
+                         P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st));
     T.end();
     T.begin("dec_finish");
     HIPCHK(launch_dframe_finish(P->d_blk_base.as<uint64_t>(), n, P->d_nblk.as<uint32_t>(), P->d_dblocks.as<DecBlock>(),
@@ -681,9 +767,13 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         HIPCHK(upload(ctx->d_units, units, st));
         HIPCHK(ctx->d_blk_out.ensure(nb * 4));
         HIPCHK(ctx->d_blk_status.ensure(nb * 4));
-        HIPCHK(launch_decode_units(ctx->d_in.as<uint8_t>(), ctx->d_out.as<uint8_t>(), ctx->d_blocks.as<DecBlock>(),
-                                   ctx->d_units.as<DecUnit>(), (uint32_t)units.size(), ctx->d_blk_out.as<uint32_t>(),
-                                   ctx->d_blk_status.as<int32_t>(), st));
+        LbCaps lc;
+        for (auto& U : units)
+            if (lb_candidate(W.blocks[U.first], U.n == 1)) lc.add_block(W.blocks[U.first].csize);
+        HIPCHK(ctx->lb.prepare((uint32_t)units.size(), lc));
+        HIPCHK(decode_launch(&ctx->lb, ctx->d_in.as<uint8_t>(), ctx->d_out.as<uint8_t>(), ctx->d_blocks.as<DecBlock>(),
+                             ctx->d_units.as<DecUnit>(), (uint32_t)units.size(), ctx->d_blk_out.as<uint32_t>(),
+                             ctx->d_blk_status.as<int32_t>(), st));
         // block checksums (FLG bit 4) over the compressed payloads
         bool any_cs = false;
         for (auto h : W.blk_has_cs) any_cs |= h != 0;
@@ -1017,6 +1107,7 @@ struct RSlot {
     PinnedBuf h_in, h_meta, h_res, h_out;
     DevBuf d_in, d_out, d_meta, d_res, d_nblk, d_blk_base, d_fwant, d_got, d_total, d_dblocks, d_units, d_blk_out,
         d_blk_status;
+    LbScratch lb;
     uint32_t n = 0;
     std::vector<uint64_t> dst_off;
     bool ready = false;     // h_out holds the batch's decoded bytes (in stream order)
@@ -1083,6 +1174,18 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     HIPCHK(S.d_units.ensure(blk_cap * sizeof(DecUnit) + 16));
     HIPCHK(S.d_blk_out.ensure(blk_cap * 4 + 16));
     HIPCHK(S.d_blk_status.ensure(blk_cap * 4 + 16));
+    {
+        // large blocks of the batch (the host walk knows every block)
+        LbCaps lc;
+        for (uint32_t f = 0; f < n; ++f) {
+            const HFrame& F = W.frames[f];
+            for (uint32_t k = 0; k < F.nblk; ++k) {
+                const DecBlock& D = W.blocks[F.blk0 + k];
+                if (lb_candidate(D, (F.flg & 0x20) != 0)) lc.add_block(D.csize);
+            }
+        }
+        HIPCHK(S.lb.prepare((uint32_t)blk_cap, lc));
+    }
     HIPCHK(S.h_res.ensure(8ull * n));
     HIPCHK(hipMemcpyAsync(S.d_in.p, S.h_in.p, nin, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(S.d_meta.p, S.h_meta.p, 24ull * n, hipMemcpyHostToDevice, st));
@@ -1103,8 +1206,8 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
                               S.d_dblocks.as<DecBlock>(), S.d_units.as<DecUnit>(), S.d_fwant.as<uint32_t>(), st));
     T.end();
     T.begin("decode");
-    HIPCHK(launch_decode_units(src, S.d_out.as<uint8_t>(), S.d_dblocks.as<DecBlock>(), S.d_units.as<DecUnit>(),
-                               (uint32_t)blk_cap, S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), st));
+    HIPCHK(decode_launch(&S.lb, src, S.d_out.as<uint8_t>(), S.d_dblocks.as<DecBlock>(), S.d_units.as<DecUnit>(),
+                         (uint32_t)blk_cap, S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), st));
     T.end();
     T.begin("dec_finish");
     HIPCHK(launch_dframe_finish(S.d_blk_base.as<uint64_t>(), n, S.d_nblk.as<uint32_t>(), S.d_dblocks.as<DecBlock>(),

@@ -1,0 +1,232 @@
+"""Large-block decode path (csrc/s3hc_lb.hip).
+
+Frames that allow blocks above 64 KiB (BD 0x50 / 0x70) are what the reference writes for its
+own cache files (flush_batch compresses ~1 MiB batches with lz4_flex BlockSize::Auto,
+disk_cache.rs:1820-1870); their blocks are decoded by many workgroups each. Bar: decoded bytes
+bit-exact with the oracle, statuses identical to the oracle's on corrupt inputs, and identical
+to the one-wave decoder (S3HC_LB_DISABLE=1) on every input.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import synth
+
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+
+
+def _rnd(n, seed):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8).tobytes()
+
+
+def _deep_chain(n, seed):
+    # every line is a recent line with one edit: matches of matches of matches (long source chains)
+    rng = random.Random(seed)
+    lines = [b"GET /bucket/object-%06d status=200 bytes=%d\n" % (i, i * 7) for i in range(8)]
+    out = bytearray()
+    while len(out) < n:
+        base = bytearray(lines[-rng.randrange(1, 8)])
+        base[rng.randrange(len(base) - 1)] = 0x41 + rng.randrange(26)
+        lines.append(bytes(base))
+        out += base
+    return bytes(out[:n])
+
+
+def _runs(n, seed):
+    rng = random.Random(seed)
+    out = bytearray()
+    while len(out) < n:
+        out += bytes([rng.randrange(256)]) * rng.choice([1, 3, 17, 300, 5000, 70000])
+    return bytes(out[:n])
+
+
+INPUTS = {
+    "log_100k": lambda: synth.log_text(100_000, 1),      # BD 0x50, one 100 KB block
+    "log_256k": lambda: synth.log_text(256 * 1024, 2),   # BD 0x50, exactly one full block
+    "log_1MiB": lambda: synth.log_text(MiB, 3),          # BD 0x70, one 1 MiB block (reference cache frame)
+    "log_5MiB+3": lambda: synth.log_text(5 * MiB + 3, 4),  # two blocks: 4 MiB + 1 MiB
+    "json_1MiB": lambda: synth.json_records(MiB, 5),
+    "zeros_4MiB": lambda: bytes(4 * MiB),                # long 255 length runs
+    "zeros_1MiB+7": lambda: bytes(MiB + 7),
+    "p251_1MiB+1": lambda: bytes(i % 251 for i in range(MiB + 1)),
+    "runs_2MiB": lambda: _runs(2 * MiB, 6),
+    "deep_1MiB": lambda: _deep_chain(MiB, 7),
+    "half_random_1MiB": lambda: synth.log_text(MiB // 2, 8) + _rnd(MiB // 2, 9),
+    "random_300k": lambda: _rnd(300_000, 10),            # stored block: not on this path
+}
+_CACHE = {}
+
+
+def _data(name):
+    if name not in _CACHE:
+        _CACHE[name] = INPUTS[name]()
+    return _CACHE[name]
+
+
+def _wave_path(fn):
+    os.environ["S3HC_LB_DISABLE"] = "1"
+    try:
+        return fn()
+    finally:
+        del os.environ["S3HC_LB_DISABLE"]
+
+
+@pytest.mark.parametrize("name", sorted(INPUTS))
+def test_lb_decodes_oracle_frames(engine, oracle, name):
+    data = _data(name)
+    frame = oracle.lz4flex_compress_frame(data)
+    assert engine.decompress_frames(frame) == data
+
+
+@pytest.mark.parametrize("name", sorted(INPUTS))
+def test_lb_decodes_gpu_frames(engine, oracle, name):
+    data = _data(name)
+    frame = engine.compress_frame(data)
+    assert frame[5] in (0x50, 0x70)
+    assert engine.decompress_frames(frame) == data
+    assert _wave_path(lambda: engine.decompress_frames(frame)) == data
+
+
+def test_lb_liblz4_large_blocks(engine):
+    import lz4ref
+
+    data = synth.log_text(3 * MiB + 5, 12)
+    for bsid in (5, 6, 7):
+        frame = lz4ref.compress_frame(data, block_size_id=bsid, linked=False)
+        assert engine.decompress_frames(frame) == data
+
+
+def test_lb_mixed_batch(engine, oracle):
+    parts = [synth.log_text(65536, 20), _data("log_1MiB"), bytes(4 * MiB), synth.json_records(65536, 21),
+             _data("deep_1MiB"), b"tail bytes" * 100]
+    blob = b"".join(
+        engine.store_mode_frame(p) if i == 5 else (oracle.lz4flex_compress_frame(p) if i % 2 else engine.compress_frame(p))
+        for i, p in enumerate(parts))
+    assert engine.decompress_frames(blob) == b"".join(parts)
+
+
+def test_lb_random_corruption_matches_oracle_and_wave_path(engine, oracle):
+    rng = random.Random(11)
+    bases = [
+        oracle.lz4flex_compress_frame(synth.log_text(300_000, 30)),
+        engine.compress_frame(synth.json_records(200_000, 31)),
+        oracle.lz4flex_compress_frame(_deep_chain(150_000, 32)),
+        oracle.lz4flex_compress_frame(bytes(700_000)),
+    ]
+    n_err = 0
+    for t in range(96):
+        b = bytearray(bases[t % len(bases)])
+        kind = t % 4
+        if kind == 0:  # bit flip in the block payload
+            i = rng.randrange(11, len(b))
+            b[i] ^= 1 << rng.randrange(8)
+        elif kind == 1:  # truncation
+            del b[rng.randrange(11, len(b)):]
+        elif kind == 2:  # random byte
+            i = rng.randrange(11, len(b))
+            b[i] = rng.randrange(256)
+        else:  # random dword
+            i = rng.randrange(11, len(b) - 4)
+            b[i:i + 4] = bytes(rng.randrange(256) for _ in range(4))
+        blob = bytes(b)
+        st_o, out_o = oracle.decompress_status(blob)
+        st_g, out_g = engine.decompress_status(blob)
+        st_w, out_w = _wave_path(lambda: engine.decompress_status(blob))
+        assert st_g == st_o == st_w, (t, kind)
+        assert out_g == out_o == out_w
+        n_err += st_o != 0
+    assert n_err > 50
+
+
+def test_lb_block_size_errors(engine, oracle):
+    # a block that decodes to more than the frame's max block size is corrupt (lz4_flex bounds
+    # its output by the block size): BD 0x50 frame whose block expands past 256 KiB
+    data = bytes(300_000)
+    frame = bytearray(oracle.lz4flex_compress_frame(data))
+    assert frame[5] == 0x70
+    frame[5] = 0x50
+    frame[6] = _hc(frame[4:6])
+    st_o, _ = oracle.decompress_status(bytes(frame))
+    st_g, _ = engine.decompress_status(bytes(frame))
+    assert st_o != 0 and st_g == st_o
+
+
+def _hc(desc):
+    import oracle as O
+
+    return (O.xxh32(bytes(desc)) >> 8) & 0xFF
+
+
+def test_lb_device_plan(engine, oracle):
+    parts = [_data("log_1MiB"), _data("zeros_1MiB+7"), synth.log_text(65536, 40), _data("json_1MiB")]
+    frames = [oracle.lz4flex_compress_frame(p) for p in parts]
+    blob = b"".join(frames)
+    fo, o = [], 0
+    for f in frames:
+        fo.append(o)
+        o += len(f)
+    caps = [len(p) for p in parts]
+    do = [sum(caps[:i]) for i in range(len(parts))]
+    plan = engine.plan_decode(fo, [len(f) for f in frames], do, caps)
+    src = engine.upload(blob)
+    dst = engine.alloc(sum(caps) + 64)
+    olen, st = engine.alloc(4 * len(parts)), engine.alloc(4 * len(parts))
+    engine.decode_dev(plan, src, dst, olen, st)
+    engine.sync()
+    assert st.i32(len(parts)) == [0] * len(parts)
+    assert olen.u32(len(parts)) == caps
+    assert dst.read(sum(caps)) == b"".join(parts)
+
+
+def test_lb_reader_reference_frames(engine):
+    import s3hc_lz4 as S
+
+    data = _deep_chain(3 * MiB, 50) + synth.log_text(2 * MiB, 51)
+    import oracle as O
+
+    blob = b"".join(O.lz4flex_compress_frame(data[i:i + MiB]) for i in range(0, len(data), MiB))
+    r = S.RangeReader(engine, batch_bytes=2 * MiB)
+    out = bytearray()
+    for i in range(0, len(blob), 700_000):
+        r.feed(blob[i:i + 700_000])
+        while True:
+            b = r.read(1 << 20)
+            if not b:
+                break
+            out += b
+    r.finish()
+    while True:
+        b = r.read(1 << 20)
+        if not b:
+            break
+        out += b
+    assert bytes(out) == data and r.total == len(data)
+    r.close()
+
+
+def _decode_dev(engine, frames, caps):
+    blob = b"".join(frames)
+    fo = [sum(len(f) for f in frames[:i]) for i in range(len(frames))]
+    do = [sum(caps[:i]) for i in range(len(frames))]
+    plan = engine.plan_decode(fo, [len(f) for f in frames], do, caps)
+    src = engine.upload(blob)
+    dst = engine.alloc(sum(caps) + 64)
+    olen, st = engine.alloc(4 * len(frames)), engine.alloc(4 * len(frames))
+    engine.decode_dev(plan, src, dst, olen, st)
+    engine.sync()
+    return st.i32(len(frames)), olen.u32(len(frames))
+
+
+@pytest.mark.parametrize("short", [1, 1000, 300_000])
+def test_lb_dst_too_small_matches_wave_path(engine, oracle, short):
+    parts = [_data("log_1MiB"), _data("deep_1MiB"), _data("zeros_1MiB+7")]
+    frames = [oracle.lz4flex_compress_frame(p) for p in parts]
+    caps = [len(parts[0]) - short, len(parts[1]), len(parts[2]) - short]
+    got = _decode_dev(engine, frames, caps)
+    want = _wave_path(lambda: _decode_dev(engine, frames, caps))
+    assert got == want
+    assert got[0][0] == 3 and got[0][1] == 0 and got[0][2] == 3  # S3HC_DST_TOO_SMALL
