@@ -1110,7 +1110,10 @@ struct RSlot {
     LbScratch lb;
     uint32_t n = 0;
     std::vector<uint64_t> dst_off;
+    hipEvent_t ev2 = nullptr;  // the batch's D2H of decoded bytes
+    int state = 0;          // 0 decoding, 1 copying decoded bytes to h_out, 2 ready
     bool ready = false;     // h_out holds the batch's decoded bytes (in stream order)
+    uint32_t good = 0;      // frames before the first failing one
     uint64_t out_len = 0;   // bytes in h_out
     uint64_t out_pos = 0;   // bytes already read
 };
@@ -1221,6 +1224,8 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     T.end();
     HIPCHK(hipMemcpyAsync(S.h_res.p, S.d_res.p, 8ull * n, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(S.ev, st));
+    S.state = 0;
+    S.ready = false;
     r->in_head += end;
     return S3HC_OK;
 }
@@ -1270,11 +1275,9 @@ static int reader_pump(s3hc_reader* r) {
     return S3HC_OK;
 }
 
-// Wait for the oldest batch and copy its good frames' bytes (stream order) into its pinned
-// output buffer; a failing frame ends the stream after them.
-static int reader_complete(s3hc_reader* r) {
-    RSlot& S = r->slots[r->inflight.front()];
-    HIPCHK(hipEventSynchronize(S.ev));
+// Decode of slot S finished: queue the D2H of its good frames' bytes (stream order) into its
+// pinned output buffer. A failing frame ends the stream after them (applied when S is the head).
+static int reader_issue_copy(RSlot& S) {
     const uint32_t* olen = (const uint32_t*)S.h_res.p;
     const int32_t* st = (const int32_t*)(S.h_res.p + 4ull * S.n);
     uint32_t good = 0;
@@ -1295,15 +1298,48 @@ static int reader_complete(s3hc_reader* r) {
             o += olen[f];
         }
     }
-    HIPCHK(hipStreamSynchronize(S.st));
-    S.ready = true;
+    HIPCHK(hipEventRecord(S.ev2, S.st));
+    S.good = good;
     S.out_len = bytes;
     S.out_pos = 0;
-    r->total += bytes;
-    if (good < S.n) {  // earlier in stream order than any error found while walking later input
-        r->error = st[good];
+    S.state = 1;
+    return S3HC_OK;
+}
+
+// Queue the D2H of every batch whose decode has finished (any order: separate queues).
+static int reader_advance(s3hc_reader* r) {
+    for (int i : r->inflight) {
+        RSlot& S = r->slots[i];
+        if (S.state == 0 && hipEventQuery(S.ev) == hipSuccess) {
+            int rc = reader_issue_copy(S);
+            if (rc) return rc;
+        }
+    }
+    return S3HC_OK;
+}
+
+// Wait until the oldest batch's decoded bytes are in its pinned output buffer.
+static int reader_complete(s3hc_reader* r) {
+    RSlot& S = r->slots[r->inflight.front()];
+    if (S.state == 0) {
+        HIPCHK(hipEventSynchronize(S.ev));
+        int rc = reader_issue_copy(S);
+        if (rc) return rc;
+    }
+    HIPCHK(hipEventSynchronize(S.ev2));
+    S.state = 2;
+    S.ready = true;
+    r->total += S.out_len;
+    if (S.good < S.n) {  // earlier in stream order than any error found while walking later input
+        const int32_t* st = (const int32_t*)(S.h_res.p + 4ull * S.n);
+        r->error = st[S.good];
         r->error_msg = "frame decode failed";
-        for (size_t k = 1; k < r->inflight.size(); ++k) (void)hipEventSynchronize(r->slots[r->inflight[k]].ev);
+        for (size_t k = 1; k < r->inflight.size(); ++k) {
+            RSlot& L = r->slots[r->inflight[k]];
+            (void)hipStreamSynchronize(L.st);
+            L.state = 0;
+            L.ready = false;
+        }
         r->inflight.resize(1);  // drop everything after the failing frame
         r->in.clear();
         r->in_head = 0;
@@ -1322,6 +1358,7 @@ extern "C" int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3
     for (auto& S : r->slots) {
         HIPCHK(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&S.ev2, hipEventDisableTiming));
     }
     *out = r.release();
     return S3HC_OK;
@@ -1336,9 +1373,12 @@ extern "C" int s3hc_reader_feed(s3hc_reader* r, const uint8_t* src, size_t n) {
     }
     const size_t old = r->in.size();
     r->in.resize(old + n);
-    par_memcpy(r->in.data() + old, src, n);
+    if (n >= ((size_t)8 << 20)) par_memcpy(r->in.data() + old, src, n);
+    else memcpy(r->in.data() + old, src, n);  // file-read sized pieces: no thread start-up
     std::lock_guard<std::mutex> g(r->ctx->mu);
     HIPCHK(hipSetDevice(r->ctx->device));
+    int rc = reader_advance(r);
+    if (rc) return rc;
     return reader_pump(r);
 }
 extern "C" int s3hc_reader_finish(s3hc_reader* r) {
@@ -1356,7 +1396,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
         RSlot& S = r->slots[r->inflight.front()];
         if (S.out_pos < S.out_len) {
             const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
-            if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
+            if (k) memcpy(dst, S.h_out.p + S.out_pos, k);
             S.out_pos += k;
             *n = k;
             if (S.out_pos < S.out_len) return S3HC_OK;
@@ -1369,12 +1409,13 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
             RSlot& S = r->slots[r->inflight.front()];
             if (*n == 0 && S.out_pos < S.out_len) {
                 const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
-                if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
+                if (k) memcpy(dst, S.h_out.p + S.out_pos, k);
                 S.out_pos += k;
                 *n = k;
             }
             if (S.out_pos == S.out_len) {  // slot free again: queue the next batch
                 S.ready = false;
+                S.state = 0;
                 r->inflight.erase(r->inflight.begin());
                 if (!r->error) {
                     int rc = reader_pump(r);
@@ -1385,7 +1426,9 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
             continue;
         }
         if (!r->error) {
-            int rc = reader_pump(r);
+            int rc = reader_advance(r);
+            if (rc) return rc;
+            rc = reader_pump(r);
             if (rc) return rc;
         }
         if (r->inflight.empty()) {
@@ -1400,7 +1443,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
         // the oldest batch is still running: wait for it only when the pipeline is full, the
         // input is finished or it is already done; otherwise ask the caller for more input
         RSlot& H = r->slots[r->inflight.front()];
-        const bool done = hipEventQuery(H.ev) == hipSuccess;
+        const bool done = H.state == 1 && hipEventQuery(H.ev2) == hipSuccess;
         if (!done && r->inflight.size() < r->slots.size() && !r->finished && !r->error) return S3HC_OK;
         int rc = reader_complete(r);
         if (rc) return rc;
@@ -1413,6 +1456,7 @@ extern "C" void s3hc_reader_close(s3hc_reader* r) {
     for (auto& S : r->slots) {
         if (S.st) (void)hipStreamSynchronize(S.st);
         if (S.ev) (void)hipEventDestroy(S.ev);
+        if (S.ev2) (void)hipEventDestroy(S.ev2);
         if (S.st) (void)hipStreamDestroy(S.st);
     }
     delete r;
