@@ -560,6 +560,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
     __shared__ uint16_t so[kMaxSeqS];
     __shared__ uint32_t rf[kLbMaxSteps + 1];
     __shared__ uint32_t shm[16];
+    __shared__ uint32_t jflag[3];
     const uint32_t i = blockIdx.x;
     if (i >= A.ctl->nlb || A.lb_stat[i] != S3HC_OK) return;
     const LbBlock B = A.lbt[i];
@@ -714,6 +715,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
             ptr[l] = pv[j];
         }
         ((uint4*)marks)[t] = make_uint4(0, 0, 0, 0);
+        if (t == 0) jflag[0] = 0u;
         __syncthreads();
         LB_T(3);
         if (q + 1 < nsteps) LB_INSTALL(q + 1)
@@ -726,15 +728,12 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         uint32_t pend = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kXPer; ++j) pend |= (pv[j] != FIN ? 1u : 0u) << j;
+        // one barrier per round: threads still pending after the round raise jflag[it % 3];
+        // thread 0 clears the next round's flag before the barrier (nobody reads or raises it
+        // until after the barrier), jflag[0] was cleared before the stores barrier
         for (uint32_t it = 0; it < 20; ++it) {
 #ifdef S3HC_LBPROF
-            const uint64_t tb0 = __builtin_amdgcn_s_memtime();
-#endif
-            if (__syncthreads_or(pend != 0) == 0) break;
-            LB_ADD(8, 1);
-#ifdef S3HC_LBPROF
             const uint64_t tb1 = __builtin_amdgcn_s_memtime();
-            lbp[10] += tb1 - tb0;
 #endif
             if (pend) {
                 uint32_t pp[kXPer];
@@ -760,11 +759,15 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
                     }
                 }
                 pend &= ~fin;
+                if (pend) jflag[it % 3u] = 1u;
             }
+            if (t == 0) jflag[(it + 1u) % 3u] = 0u;
 #ifdef S3HC_LBPROF
             lbp[11] += __builtin_amdgcn_s_memtime() - tb1;
 #endif
             __syncthreads();
+            LB_ADD(8, 1);
+            if (!jflag[it % 3u]) break;
         }
         LB_T(5);
         // flush the step (thread t: dwords t and t + kXT of the step)
