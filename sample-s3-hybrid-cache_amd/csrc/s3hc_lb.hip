@@ -307,7 +307,9 @@ __global__ __launch_bounds__(1024) void k_lb_exit(const uint8_t* __restrict__ sr
         if (r < n) {
             const LbTok T = lb_token(v, cs + r);
             nx[r] = T.nxt;
-            J[r] = (uint16_t)(T.nxt < ce ? T.nxt - cs : r);  // END / BAD / beyond: the chain leaves here
+            const uint16_t j0 = (uint16_t)(T.nxt < ce ? T.nxt - cs : r);  // END / BAD / beyond: the chain leaves here
+            J[r] = j0;
+            A.J0[(size_t)c * kLbChunk + r] = j0;  // k_lb_mark starts from it
         }
     }
     __syncthreads();
@@ -369,15 +371,13 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
     const LbBlock B = A.lbt[A.chunk_blk[c]];
     const uint32_t cs = (c - B.chunk0) * kLbChunk;
     const uint32_t n = B.C - cs < kLbChunk ? B.C - cs : kLbChunk;
-    const uint32_t ce = cs + n;
     const LbView v = lb_view(src, B, A.nzg, cs, lb_stage(src + B.src_off, cs, B.C - cs < kStage ? B.C - cs : kStage, raw));
     if (threadIdx.x == 0) bad_s = NONE;
     __syncthreads();
     for (uint32_t k = 0; k < kPer; ++k) {
         const uint32_t r = threadIdx.x + k * kT;
         if (r < n) {
-            const LbTok T = lb_token(v, cs + r);
-            Ja[r] = (uint16_t)(T.nxt < ce ? T.nxt - cs : r);
+            Ja[r] = A.J0[(size_t)c * kLbChunk + r];
             mk[r] = r == e ? 1 : 0;
         }
     }

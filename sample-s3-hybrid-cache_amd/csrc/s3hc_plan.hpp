@@ -120,6 +120,7 @@ struct LbArgs {
     uint32_t* chunk_blk;   // chunk -> LB block
     uint32_t* nzg;         // per chunk, per 64-byte granule: first non-255 byte at or after it (chunk-local)
     uint32_t* E;           // per compressed position: chain exit of its chunk
+    uint16_t* J0;          // per compressed position: next token inside its chunk (chunk-relative; itself if none)
     uint32_t* entry;       // per chunk: first chain position (chunk-relative) or ~0
     uint32_t* bits;        // per chunk: token bitmap
     uint32_t* ntok;        // per chunk: sequences

@@ -134,7 +134,7 @@ static bool lb_candidate(const DecBlock& D, bool unit_single) {
 }
 
 struct LbScratch {
-    DevBuf lbt, ctl, unit_lb, chunk_blk, nzg, E, entry, bits, ntok, slsum, badrel, tokbase, outbase, total, seq4,
+    DevBuf lbt, ctl, unit_lb, chunk_blk, nzg, E, J0, entry, bits, ntok, slsum, badrel, tokbase, outbase, total, seq4,
         seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst;
     LbArgs a{};
     bool active = false;
@@ -146,7 +146,7 @@ struct LbScratch {
         hipError_t e = hipSuccess;
 #define LBE(buf, bytes) if ((e = (buf).ensure((size_t)(bytes) + 64)) != hipSuccess) return e;
         LBE(lbt, nlb * sizeof(LbBlock)) LBE(ctl, sizeof(LbCtl)) LBE(unit_lb, nunits) LBE(chunk_blk, nch * 4)
-        LBE(nzg, nch * (kLbChunk / 64) * 4) LBE(E, nch * kLbChunk * 4) LBE(entry, nch * 4)
+        LBE(nzg, nch * (kLbChunk / 64) * 4) LBE(E, nch * kLbChunk * 4) LBE(J0, nch * kLbChunk * 2) LBE(entry, nch * 4)
         LBE(bits, nch * (kLbChunk / 32) * 4) LBE(ntok, nch * 4) LBE(slsum, nch * 4) LBE(badrel, nch * 4)
         LBE(tokbase, nch * 8) LBE(outbase, nch * 8) LBE(total, 32) LBE(seq4, nseq * 16) LBE(seqoff, nseq * 2)
         LBE(lb_err, nlb * 4) LBE(lb_size, nlb * 4) LBE(lb_stat, nlb * 4) LBE(lb_tok0, nlb * 4) LBE(lb_ntok, nlb * 4)
@@ -155,7 +155,7 @@ struct LbScratch {
         a.lb_cap = c.lb;
         a.chunk_cap = c.chunks;
         a.lbt = lbt.as<LbBlock>(); a.ctl = ctl.as<LbCtl>(); a.unit_lb = unit_lb.as<uint8_t>();
-        a.chunk_blk = chunk_blk.as<uint32_t>(); a.nzg = nzg.as<uint32_t>(); a.E = E.as<uint32_t>();
+        a.chunk_blk = chunk_blk.as<uint32_t>(); a.nzg = nzg.as<uint32_t>(); a.E = E.as<uint32_t>(); a.J0 = J0.as<uint16_t>();
         a.entry = entry.as<uint32_t>(); a.bits = bits.as<uint32_t>(); a.ntok = ntok.as<uint32_t>();
         a.slsum = slsum.as<uint32_t>(); a.badrel = badrel.as<uint32_t>(); a.tokbase = tokbase.as<uint64_t>();
         a.outbase = outbase.as<uint64_t>(); a.total = total.as<uint64_t>(); a.seq4 = seq4.as<uint4>();
