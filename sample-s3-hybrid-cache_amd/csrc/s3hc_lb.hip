@@ -221,7 +221,7 @@ __global__ __launch_bounds__(1024) void k_lb_classify(const DecBlock* __restrict
             if (U.n == 1) {
                 bi = U.first;
                 B = blk[bi];
-                cand = !(B.flags & (DB_STORED | DB_LINKED)) && B.limit >= kLbMinLimit && B.csize > 0 &&
+                cand = !(B.flags & (DB_STORED | DB_LINKED)) && B.limit >= A.min_limit && B.csize > 0 &&
                        B.limit <= kLbMaxSteps * kLbStep;
             }
         }

@@ -95,6 +95,9 @@ constexpr uint32_t kLbChunk = 16384;      // compressed positions per tokenizing
 constexpr uint32_t kLbStep = 8192;        // output bytes per step of the executing workgroup
 constexpr uint32_t kLbMaxSteps = 512;     // steps of one block (4 MiB / kLbStep)
 constexpr uint32_t kLbMinLimit = 65537;   // frame max block size above 64 KiB selects the path
+constexpr uint32_t kLbFewBlocks = 256;    // batches with at most this many blocks: every compressed
+                                          // independent block takes the path (latency: one wave per
+                                          // 64 KiB block needs 0.85 ms)
 
 struct LbBlock {         // 48 bytes; one per block taken by the large-block path
     uint64_t src_off;    // compressed payload
@@ -114,6 +117,8 @@ struct LbCtl {           // device-side counters of one large-block launch
 // blocks beyond a cap are decoded by the one-wave decoder instead).
 struct LbArgs {
     uint32_t lb_cap, chunk_cap;
+    uint32_t min_limit;    // frame max block size that selects the path (kLbMinLimit; 1 for few-block batches)
+    uint32_t pad;
     LbBlock* lbt;
     LbCtl* ctl;
     uint8_t* unit_lb;      // per unit: 1 = decoded by this path

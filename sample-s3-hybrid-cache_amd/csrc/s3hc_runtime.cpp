@@ -123,13 +123,14 @@ template <class T> static hipError_t upload(DevBuf& b, const std::vector<T>& v, 
 // a block beyond any cap is decoded by the one-wave decoder instead.
 struct LbCaps {
     uint32_t lb = 0, chunks = 0;
+    uint32_t min_limit = kLbMinLimit;
     void add_block(uint32_t csize) {
         ++lb;
         chunks += (csize + kLbChunk - 1) / kLbChunk;
     }
 };
-static bool lb_candidate(const DecBlock& D, bool unit_single) {
-    return unit_single && !(D.flags & (DB_STORED | DB_LINKED)) && D.limit >= kLbMinLimit && D.csize > 0 &&
+static bool lb_candidate(const DecBlock& D, bool unit_single, uint32_t min_limit) {
+    return unit_single && !(D.flags & (DB_STORED | DB_LINKED)) && D.limit >= min_limit && D.csize > 0 &&
            D.limit <= kLbMaxSteps * kLbStep;
 }
 
@@ -154,6 +155,7 @@ struct LbScratch {
 #undef LBE
         a.lb_cap = c.lb;
         a.chunk_cap = c.chunks;
+        a.min_limit = c.min_limit;
         a.lbt = lbt.as<LbBlock>(); a.ctl = ctl.as<LbCtl>(); a.unit_lb = unit_lb.as<uint8_t>();
         a.chunk_blk = chunk_blk.as<uint32_t>(); a.nzg = nzg.as<uint32_t>(); a.E = E.as<uint32_t>(); a.J0 = J0.as<uint16_t>();
         a.entry = entry.as<uint32_t>(); a.bits = bits.as<uint32_t>(); a.ntok = ntok.as<uint32_t>();
@@ -510,11 +512,20 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
     // large blocks: the device walk finds them; frames with room for more than 64 KiB may hold
     // some (well-formed frames fill every block but the last, so <= cap / 256 KiB + 1 of them)
     LbCaps lc;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (dst_cap[i] <= 65536u) continue;
-        const uint32_t nl = dst_cap[i] / 262144u + 1u;
-        lc.lb += nl;
-        lc.chunks += frame_len[i] / kLbChunk + nl;
+    if (n <= kLbFewBlocks / 4) {  // few frames: every compressed block takes the path
+        lc.min_limit = 1;
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t nl = dst_cap[i] / 65536u + 1u;
+            lc.lb += nl;
+            lc.chunks += frame_len[i] / kLbChunk + nl;
+        }
+    } else {
+        for (uint32_t i = 0; i < n; ++i) {
+            if (dst_cap[i] <= 65536u) continue;
+            const uint32_t nl = dst_cap[i] / 262144u + 1u;
+            lc.lb += nl;
+            lc.chunks += frame_len[i] / kLbChunk + nl;
+        }
     }
     HIPCHK(P->lb.prepare(P->blk_cap, lc));
     HIPCHK(hipStreamSynchronize(st));
@@ -768,8 +779,9 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         HIPCHK(ctx->d_blk_out.ensure(nb * 4));
         HIPCHK(ctx->d_blk_status.ensure(nb * 4));
         LbCaps lc;
+        if (W.blocks.size() <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
         for (auto& U : units)
-            if (lb_candidate(W.blocks[U.first], U.n == 1)) lc.add_block(W.blocks[U.first].csize);
+            if (lb_candidate(W.blocks[U.first], U.n == 1, lc.min_limit)) lc.add_block(W.blocks[U.first].csize);
         HIPCHK(ctx->lb.prepare((uint32_t)units.size(), lc));
         HIPCHK(decode_launch(&ctx->lb, ctx->d_in.as<uint8_t>(), ctx->d_out.as<uint8_t>(), ctx->d_blocks.as<DecBlock>(),
                              ctx->d_units.as<DecUnit>(), (uint32_t)units.size(), ctx->d_blk_out.as<uint32_t>(),
@@ -1180,11 +1192,14 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     {
         // large blocks of the batch (the host walk knows every block)
         LbCaps lc;
+        uint32_t nb = 0;
+        for (uint32_t f = 0; f < n; ++f) nb += W.frames[f].nblk;
+        if (nb <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
         for (uint32_t f = 0; f < n; ++f) {
             const HFrame& F = W.frames[f];
             for (uint32_t k = 0; k < F.nblk; ++k) {
                 const DecBlock& D = W.blocks[F.blk0 + k];
-                if (lb_candidate(D, (F.flg & 0x20) != 0)) lc.add_block(D.csize);
+                if (lb_candidate(D, (F.flg & 0x20) != 0, lc.min_limit)) lc.add_block(D.csize);
             }
         }
         HIPCHK(S.lb.prepare((uint32_t)blk_cap, lc));
