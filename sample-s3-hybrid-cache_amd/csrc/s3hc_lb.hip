@@ -385,19 +385,25 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
     // the jump table is double-buffered; marks may be set early, they are still chain nodes)
     uint16_t* Jc = Ja;
     uint16_t* Jn = Jb;
+    // a level that adds no mark ends the marking: J_(k+1) = J_k o J_k then maps the marked set
+    // into itself too
+    __syncthreads();
     for (uint32_t lev = 0; lev < kLevels; ++lev) {
-        __syncthreads();
+        bool added = false;
         for (uint32_t k = 0; k < kPer; ++k) {
             const uint32_t r = threadIdx.x + k * kT;
             if (r < n) {
                 const uint32_t j = Jc[r];
-                if (mk[r]) mk[j] = 1;
+                if (mk[r] && !mk[j]) {
+                    mk[j] = 1;
+                    added = true;
+                }
                 Jn[r] = Jc[j];
             }
         }
         uint16_t* tmp = Jc; Jc = Jn; Jn = tmp;
+        if (!__syncthreads_or(added)) break;
     }
-    __syncthreads();
     uint32_t cnt = 0;
     uint64_t sl = 0;
     for (uint32_t k = 0; k < kPer; ++k) {
