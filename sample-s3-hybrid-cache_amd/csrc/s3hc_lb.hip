@@ -553,10 +553,10 @@ __global__ void k_lb_fin(LbArgs A, uint32_t* __restrict__ blk_out, int32_t* __re
 // One 1024-thread workgroup per block writes the block in kLbStep-byte steps, in order. LDS
 // keeps a 64 KiB ring of the block's recent output (match sources) and the step's sequences.
 // Each byte of a step gets its value right away when it is a literal or its match source lies
-// before the step (ring, or HBM for the few sources the step itself is overwriting in the
-// ring); otherwise it gets a pointer to its source inside the step, and the pointers are jumped
-// (a final source gives the value) until every byte is final: every chain ends in a literal or
-// a byte before the step, so no byte is left over. Then the step is flushed to HBM.
+// before the step (the ring still holds [R - 64 KiB, R) until the step stores its own bytes, and
+// LZ4 offsets are < 64 KiB); otherwise it gets a pointer to its source inside the step, and the
+// pointers are jumped (a final source gives the value) until every byte is final: every chain
+// ends in a literal or a byte before the step, so no byte is left over. Then the step is flushed.
 __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, LbArgs A) {
     using namespace lb;
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
