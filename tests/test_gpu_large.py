@@ -230,3 +230,30 @@ def test_lb_dst_too_small_matches_wave_path(engine, oracle, short):
     want = _wave_path(lambda: _decode_dev(engine, frames, caps))
     assert got == want
     assert got[0][0] == 3 and got[0][1] == 0 and got[0][2] == 3  # S3HC_DST_TOO_SMALL
+
+
+def test_lb_randomized_structures_match_wave_path(engine, oracle):
+    # seeded mixtures of text, byte runs, random bytes and match-of-match chains, frame sizes from
+    # just above 64 KiB to 4 MiB + 1: both paths and the oracle agree byte for byte
+    rng = random.Random(2024)
+    for case in range(20):
+        size = rng.choice([65_537, 100_000, 262_144, 700_001, MiB, 3 * MiB + 1, 4 * MiB + 1])
+        parts, n = [], 0
+        while n < size:
+            kind = rng.randrange(4)
+            k = rng.randrange(1, 200_000)
+            if kind == 0:
+                p = synth.log_text(k, rng.randrange(1 << 30))
+            elif kind == 1:
+                p = _runs(k, rng.randrange(1 << 30))
+            elif kind == 2:
+                p = _rnd(k, rng.randrange(1 << 30))
+            else:
+                p = _deep_chain(k, rng.randrange(1 << 30))
+            parts.append(p)
+            n += len(p)
+        data = b"".join(parts)[:size]
+        for frame in (oracle.lz4flex_compress_frame(data), engine.compress_frame(data)):
+            got = engine.decompress_frames(frame)
+            assert got == data, case
+            assert _wave_path(lambda: engine.decompress_frames(frame)) == data, case
