@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1071,23 +1073,100 @@ extern "C" int s3hc_memcpy_async(s3hc_ctx* ctx, void* dst, const void* src, size
 
 // Host copy of a large staging buffer split over a few threads (one thread copies ~6-10 GB/s;
 // the reader's feed/stage/deliver copies are otherwise the bottleneck of the pipeline).
+// Host copies of the range reader and the batch paths: split over a small persistent pool of
+// copy threads (no thread start-up per call). The calling thread copies too and helps with
+// queued pieces while it waits, so concurrent callers never block each other.
+namespace {
+class CopyPool {
+  public:
+    struct State {
+        std::atomic<int> left{0};
+    };
+    struct Job {
+        uint8_t* d;
+        const uint8_t* s;
+        size_t n;
+        State* st;
+    };
+    explicit CopyPool(unsigned nt) {
+        for (unsigned i = 0; i < nt; ++i) th_.emplace_back([this] { run(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    unsigned threads() const { return (unsigned)th_.size(); }
+    void copy(uint8_t* d, const uint8_t* s, size_t n, size_t parts) {
+        const size_t per = ((n + parts - 1) / parts + 63) & ~(size_t)63;
+        State st;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (size_t o = per; o < n; o += per) {
+                q_.push_back(Job{d + o, s + o, std::min(per, n - o), &st});
+                st.left.fetch_add(1, std::memory_order_relaxed);
+            }
+        }
+        cv_.notify_all();
+        memcpy(d, s, std::min(per, n));
+        while (st.left.load(std::memory_order_acquire) > 0) {
+            Job j{};
+            bool have = false;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (!q_.empty()) {
+                    j = q_.back();
+                    q_.pop_back();
+                    have = true;
+                }
+            }
+            if (have) do_job(j);
+            else std::this_thread::yield();
+        }
+    }
+
+  private:
+    static void do_job(const Job& j) {
+        memcpy(j.d, j.s, j.n);
+        j.st->left.fetch_sub(1, std::memory_order_release);
+    }
+    void run() {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                j = q_.back();
+                q_.pop_back();
+            }
+            do_job(j);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<Job> q_;
+    bool stop_ = false;
+};
+CopyPool& copy_pool() {
+    static CopyPool p(std::max(1u, std::min(7u, std::thread::hardware_concurrency() / 2)));
+    return p;
+}
+}  // namespace
+
 static void par_memcpy(void* dst, const void* src, size_t n) {
-    constexpr size_t kPiece = 512u << 10;
-    const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-    const size_t parts = std::min<size_t>(hw, n / kPiece);
+    constexpr size_t kPiece = 128u << 10;
+    CopyPool& P = copy_pool();
+    const size_t parts = std::min<size_t>(P.threads() + 1, n / kPiece);
     if (parts < 2) {
         memcpy(dst, src, n);
         return;
     }
-    const size_t per = ((n + parts - 1) / parts + 63) & ~(size_t)63;  // parts * per >= n
-    std::vector<std::thread> ts;
-    for (size_t k = 1; k < parts; ++k) {
-        const size_t o = k * per;
-        if (o >= n) break;
-        ts.emplace_back([=] { memcpy((uint8_t*)dst + o, (const uint8_t*)src + o, std::min(per, n - o)); });
-    }
-    memcpy(dst, src, std::min(per, n));
-    for (auto& t : ts) t.join();
+    P.copy((uint8_t*)dst, (const uint8_t*)src, n, parts);
 }
 
 // ------------------------------------------- pipelined range reader (config 4)
@@ -1388,8 +1467,7 @@ extern "C" int s3hc_reader_feed(s3hc_reader* r, const uint8_t* src, size_t n) {
     }
     const size_t old = r->in.size();
     r->in.resize(old + n);
-    if (n >= ((size_t)8 << 20)) par_memcpy(r->in.data() + old, src, n);
-    else memcpy(r->in.data() + old, src, n);  // file-read sized pieces: no thread start-up
+    par_memcpy(r->in.data() + old, src, n);
     std::lock_guard<std::mutex> g(r->ctx->mu);
     HIPCHK(hipSetDevice(r->ctx->device));
     int rc = reader_advance(r);
@@ -1411,7 +1489,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
         RSlot& S = r->slots[r->inflight.front()];
         if (S.out_pos < S.out_len) {
             const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
-            if (k) memcpy(dst, S.h_out.p + S.out_pos, k);
+            if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
             S.out_pos += k;
             *n = k;
             if (S.out_pos < S.out_len) return S3HC_OK;
@@ -1424,7 +1502,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
             RSlot& S = r->slots[r->inflight.front()];
             if (*n == 0 && S.out_pos < S.out_len) {
                 const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
-                if (k) memcpy(dst, S.h_out.p + S.out_pos, k);
+                if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
                 S.out_pos += k;
                 *n = k;
             }
