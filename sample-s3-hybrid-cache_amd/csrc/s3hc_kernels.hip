@@ -233,7 +233,11 @@ constexpr uint32_t kCmask = kCring - 1;
 constexpr uint32_t kChunk = 256;   // ring refill granule: one dword per lane
 constexpr uint32_t kAhead = 1024;  // input kept staged ahead of the parse position
 constexpr uint32_t kInit = 5;      // chunks loaded up front (>= kAhead + 3 bytes)
-constexpr uint32_t kPos = 256;     // token positions examined per window (4 per lane)
+#ifndef S3HC_DEC_PK
+#define S3HC_DEC_PK 4
+#endif
+constexpr uint32_t kPK = S3HC_DEC_PK;  // token positions per lane and window
+constexpr uint32_t kPos = 64 * kPK;    // token positions examined per window
 constexpr uint32_t kMaxMem = 128;  // members (sequences) per window
 constexpr uint32_t kRing = 4096;   // recent output kept in LDS per wave (match sources)
 constexpr uint32_t kMask = kRing - 1;
@@ -660,6 +664,10 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
         const uint32_t nx1 = dec_step(w.cin, q + 64 + lane, q, mis, C, fill);
         const uint32_t nx2 = dec_step(w.cin, q + 128 + lane, q, mis, C, fill);
         const uint32_t nx3 = dec_step(w.cin, q + 192 + lane, q, mis, C, fill);
+#if S3HC_DEC_PK == 5
+        const uint32_t nx4 = dec_step(w.cin, q + 256 + lane, q, mis, C, fill);
+        uint64_t m4 = 0;
+#endif
         uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
         uint32_t l = 0, lastl = 0;
         WALK_PRIO_ON();
@@ -667,25 +675,35 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
         while (l < 128u) { lastl = l; m1 |= 1ull << (l - 64u); l = rdl(nx1, l - 64u); }
         while (l < 192u) { lastl = l; m2 |= 1ull << (l - 128u); l = rdl(nx2, l - 128u); }
         while (l < 256u) { lastl = l; m3 |= 1ull << (l - 192u); l = rdl(nx3, l - 192u); }
+#if S3HC_DEC_PK == 5
+        while (l < 320u) { lastl = l; m4 |= 1ull << (l - 256u); l = rdl(nx4, l - 256u); }
+#endif
         WALK_PRIO_OFF();
-        // members are >= 3 bytes apart except the last, so at most 86 of them (< kMaxMem)
+        // members are >= 3 bytes apart except the last, so at most kPos / 3 + 1 of them (< kMaxMem)
         const uint32_t c1 = (uint32_t)__builtin_popcountll(m0), c2 = c1 + (uint32_t)__builtin_popcountll(m1);
         const uint32_t c3 = c2 + (uint32_t)__builtin_popcountll(m2);
         uint32_t n = c3 + (uint32_t)__builtin_popcountll(m3);
+#if S3HC_DEC_PK == 5
+        const uint32_t c4 = n;
+        n += (uint32_t)__builtin_popcountll(m4);
+#endif
         {
-            uint8_t* slots = (uint8_t*)w.refs;  // refs are free between passes
+            uint16_t* slots = w.refs;  // refs are free between passes
             auto put = [&](uint64_t m, uint32_t base, uint32_t k) {
                 const uint32_t rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                *(((m >> lane) & 1ull) ? slots + rank : w.sink + lane) = (uint8_t)(64u * k + (uint32_t)lane);
+                *(((m >> lane) & 1ull) ? slots + rank : (uint16_t*)w.sink + (lane & 31)) = (uint16_t)(64u * k + (uint32_t)lane);
             };
             put(m0, 0, 0);
             if (m1) put(m1, c1, 1);
             if (m2) put(m2, c2, 2);
             if (m3) put(m3, c3, 3);
+#if S3HC_DEC_PK == 5
+            if (m4) put(m4, c4, 4);
+#endif
             wave_sync();
         }
-        const uint32_t rp0 = ((const uint8_t*)w.refs)[lane];
-        const uint32_t rp1 = n > 64u ? ((const uint8_t*)w.refs)[64 + lane] : 0u;
+        const uint32_t rp0 = w.refs[lane];
+        const uint32_t rp1 = n > 64u ? w.refs[64 + lane] : 0u;
         // ---- members decoded densely: member m's token in lane m (set 0) / m - 64 (set 1)
         const DecTok t0 = dec_spec(w.cin, q + rp0, mis, C, fill);
         DecTok t1 = {0u, 0u, 0u, 0u, 0u, 0u};
