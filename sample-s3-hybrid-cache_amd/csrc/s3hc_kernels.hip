@@ -169,7 +169,7 @@ __device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t in) {
 
 // out[r] = xxh32(base + off[r], len[r], seed 0). Lanes 4r..4r+3 run the 4 accumulator chains
 // (gid = global thread index of the calling grid's xxh32 threads).
-template <uint32_t kIF>  // loads in flight per lane (VGPRs: the match finder's copy uses fewer)
+template <uint32_t kIF, bool kPipe>  // loads per batch (VGPRs: the match finder's copy uses fewer)
 __device__ __forceinline__ void xxh32_ranges_dev(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
                                                  const uint32_t* __restrict__ len, uint32_t n,
                                                  uint32_t* __restrict__ out, uint32_t gid) {
@@ -182,7 +182,32 @@ __device__ __forceinline__ void xxh32_ranges_dev(const uint8_t* __restrict__ bas
     uint32_t acc = a == 0 ? XP1 + XP2 : (a == 1 ? XP2 : (a == 2 ? 0u : 0u - XP1));
     const uint8_t* q = p + 4 * a;
     uint32_t s = 0;
-    if ((((uintptr_t)p) & 3) == 0) {
+    if (kPipe && (((uintptr_t)p) & 3) == 0) {
+        // software-pipelined: three buffers of kIF stripes, the loads of the next two in flight
+        // while one is hashed (the chain add, rotate, multiply is the only serial part)
+        const uint32_t* w = (const uint32_t*)q;
+        uint32_t b0[kIF], b1[kIF], b2[kIF];
+        const uint32_t nbt = ns / kIF;
+#define XLD(buf, bidx)                                                        \
+    {                                                                         \
+        const uint32_t bb_ = (bidx) < nbt ? (bidx) : 0u;                      \
+        _Pragma("unroll") for (uint32_t k = 0; k < kIF; ++k) buf[k] = w[4 * (bb_ * kIF + k)]; \
+    }
+#define XUSE(buf) _Pragma("unroll") for (uint32_t k = 0; k < kIF; ++k) acc = xround(acc, buf[k]);
+        XLD(b0, 0u)
+        XLD(b1, 1u)
+        for (uint32_t b = 0; b < nbt; b += 3) {
+            XLD(b2, b + 2)
+            XUSE(b0)
+            XLD(b0, b + 3)
+            if (b + 1 < nbt) { XUSE(b1) }
+            XLD(b1, b + 4)
+            if (b + 2 < nbt) { XUSE(b2) }
+        }
+#undef XLD
+#undef XUSE
+        for (s = nbt * kIF; s < ns; ++s) acc = xround(acc, w[4 * s]);
+    } else if ((((uintptr_t)p) & 3) == 0) {
         const uint32_t* w = (const uint32_t*)q;
         // kIF loads in flight per lane: the chain (add, rotate, multiply) is the only serial part
         for (; s + kIF <= ns; s += kIF) {
@@ -223,7 +248,7 @@ __global__ __launch_bounds__(64) void k_xxh32_ranges(const uint8_t* __restrict__
                                                       const uint64_t* __restrict__ off,
                                                       const uint32_t* __restrict__ len, uint32_t n,
                                                       uint32_t* __restrict__ out) {
-    xxh32_ranges_dev<64>(base, off, len, n, out, blockIdx.x * blockDim.x + threadIdx.x);
+    xxh32_ranges_dev<32, true>(base, off, len, n, out, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // ================================================================== decode
@@ -996,7 +1021,7 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
     // The first nxx workgroups compute the frames' content xxh32 (they are dispatched first and
     // overlap the match finding; the emitter reads the hashes).
     if (blockIdx.x < nxx) {
-        xxh32_ranges_dev<32>(src, fsrc_off, fsrc_len, nframes, fhash, blockIdx.x * kGThreads + threadIdx.x);
+        xxh32_ranges_dev<32, false>(src, fsrc_off, fsrc_len, nframes, fhash, blockIdx.x * kGThreads + threadIdx.x);
         return;
     }
     const uint32_t gi = blockIdx.x - nxx;
