@@ -37,6 +37,8 @@ extern "C" {
 /* Frame layout policies for s3hc_compress_frame. */
 #define S3HC_BLK_AUTO_LZ4FLEX 0  /* lz4_flex FrameEncoder BlockSize::Auto: one frame, BD by input size */
 #define S3HC_BLK_64K_PER_FRAME 1 /* one BD=0x40 frame per 64 KiB of input (GPU batch format) */
+#define S3HC_BLK_LZ4FLEX_COMPAT 2 /* Auto layout with block payloads byte-identical to lz4_flex's
+                                     greedy compressor as restated in oracle/ (slower; see below) */
 
 typedef struct s3hc_ctx s3hc_ctx;
 typedef struct s3hc_stream s3hc_stream;
@@ -116,6 +118,17 @@ int s3hc_plan_encode(s3hc_ctx* ctx, const uint64_t* src_off, const uint32_t* len
 int s3hc_encode_dev(s3hc_ctx* ctx, s3hc_plan* plan, const uint8_t* d_src, uint8_t* d_dst,
                     uint64_t dst_cap, uint64_t* d_item_off, uint32_t* d_item_len, void* stream);
 uint64_t s3hc_plan_dst_bound(const s3hc_plan* plan);
+
+/* lz4_flex-compatible encoder: the frame FrameEncoder writes in
+ * compress_with_algorithm (compression.rs:539-557) and flush_batch (disk_cache.rs:1829-1846),
+ * block payloads from lz4_flex's own greedy parse (block/compress.rs compress_internal as
+ * restated in oracle/lz4_oracle.c:173-279; compressed-byte parity with the crate itself is
+ * unpinned). One frame per item, one wave per frame. src_off/len/dst_off are
+ * host arrays; dst_off[i+1] - dst_off[i] >= s3hc_frame_bound(len[i]). d_frame_len (device)
+ * receives each frame's length. Returns after the frames are written. */
+int s3hc_compat_encode_dev(s3hc_ctx* ctx, const uint8_t* d_src, const uint64_t* src_off, const uint32_t* len,
+                           uint32_t n, uint8_t* d_dst, const uint64_t* dst_off, uint32_t* d_frame_len,
+                           void* stream);
 
 /* Decode n frames in HBM: frame i = d_src[frame_off[i] .. +frame_len[i]) decodes to
  * d_dst[dst_off[i] ..) with room dst_cap[i]. Per-frame decoded length and status

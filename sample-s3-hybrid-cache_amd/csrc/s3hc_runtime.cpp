@@ -26,6 +26,8 @@
 
 namespace s3hc {
 hipError_t launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*, hipStream_t);
+hipError_t launch_compat_frames(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint8_t*, const uint64_t*,
+                                const uint32_t*, uint32_t*, hipStream_t);
 hipError_t launch_decode_units(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*,
                                int32_t*, const uint8_t*, hipStream_t);
 hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*, int32_t*,
@@ -220,6 +222,7 @@ struct s3hc_ctx {
     DevBuf d_in, d_out;
     s3hc_plan* host_plan = nullptr;
     DevBuf d_blocks, d_units, d_blk_out, d_blk_status, d_rng_off, d_rng_len, d_hash;
+    DevBuf d_c_soff, d_c_len, d_c_doff, d_c_hash, d_c_flen;  // compat encoder descriptors
     LbScratch lb;
     ~s3hc_ctx();
 };
@@ -613,8 +616,79 @@ static int host_encode(s3hc_ctx* ctx, const uint8_t* src, size_t n, int mode, in
     return S3HC_OK;
 }
 
+// ------------------------------------- lz4_flex-compatible encoder (§8(f) row 4)
+// One frame per input range, laid out as FrameEncoder writes it, block payloads from the
+// s3hc_compat.hip kernel (one wave per frame). Descriptors are host arrays; the caller's dst
+// offsets must leave s3hc_frame_bound(len[i]) bytes per frame. Caller holds ctx->mu.
+static int run_compat(s3hc_ctx* ctx, const uint8_t* d_src, const uint64_t* src_off, const uint32_t* len, uint32_t n,
+                      uint8_t* d_dst, const uint64_t* dst_off, uint32_t* d_frame_len, hipStream_t st) {
+    if (!n) return S3HC_OK;
+    std::vector<uint64_t> so(src_off, src_off + n), dof(dst_off, dst_off + n);
+    std::vector<uint32_t> ln(len, len + n);
+    for (uint32_t i = 0; i + 1 < n; ++i)
+        if (dof[i + 1] < dof[i] || dof[i + 1] - dof[i] < s3hc_frame_bound(ln[i]))
+            return fail(S3HC_INVALID_ARG, "dst_off leaves less than s3hc_frame_bound(len) per frame");
+    HIPCHK(upload(ctx->d_c_soff, so, st));
+    HIPCHK(upload(ctx->d_c_len, ln, st));
+    HIPCHK(upload(ctx->d_c_doff, dof, st));
+    HIPCHK(ctx->d_c_hash.ensure((size_t)n * 4));
+    KTimer T(ctx, st);
+    T.begin("xxh32");
+    HIPCHK(launch_xxh32(d_src, ctx->d_c_soff.as<uint64_t>(), ctx->d_c_len.as<uint32_t>(), n, ctx->d_c_hash.as<uint32_t>(), st));
+    T.end();
+    T.begin("compat");
+    HIPCHK(launch_compat_frames(d_src, ctx->d_c_soff.as<uint64_t>(), ctx->d_c_len.as<uint32_t>(), n, d_dst,
+                                ctx->d_c_doff.as<uint64_t>(), ctx->d_c_hash.as<uint32_t>(), d_frame_len, st));
+    T.end();
+    // the descriptors live in ctx scratch: the next call may not overwrite them early
+    HIPCHK(hipStreamSynchronize(st));
+    return S3HC_OK;
+}
+
+extern "C" int s3hc_compat_encode_dev(s3hc_ctx* ctx, const uint8_t* d_src, const uint64_t* src_off, const uint32_t* len,
+                                      uint32_t n, uint8_t* d_dst, const uint64_t* dst_off, uint32_t* d_frame_len,
+                                      void* stream) {
+    if (!ctx || (n && (!d_src || !src_off || !len || !d_dst || !dst_off || !d_frame_len)))
+        return fail(S3HC_INVALID_ARG, "bad arguments");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    return run_compat(ctx, d_src, src_off, len, n, d_dst, dst_off, d_frame_len, stream ? (hipStream_t)stream : ctx->stream);
+}
+
+static int host_compat(s3hc_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
+    if (!ctx || (!src && n) || !out_len) return fail(S3HC_INVALID_ARG, "bad arguments");
+    if (n > 0xFFFFFFFFull) return fail(S3HC_INVALID_ARG, "single-frame input above 4 GiB");
+    const size_t bound = s3hc_frame_bound(n);
+    if (cap < bound) return fail(S3HC_DST_TOO_SMALL, "dst capacity below frame bound");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    HIPCHK(ctx->d_in.ensure(n + 64));
+    HIPCHK(ctx->d_out.ensure(bound + 64));
+    HIPCHK(ctx->d_c_flen.ensure(16));
+    if (n) HIPCHK(hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
+    const uint64_t so = 0, dof = 0;
+    const uint32_t ln = (uint32_t)n;
+    int rc = run_compat(ctx, ctx->d_in.as<uint8_t>(), &so, &ln, 1, ctx->d_out.as<uint8_t>(), &dof,
+                        ctx->d_c_flen.as<uint32_t>(), st);
+    if (rc) return rc;
+    uint32_t flen = 0;
+    HIPCHK(hipMemcpyAsync(&flen, ctx->d_c_flen.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (flen > bound) return fail(S3HC_DEVICE, "compat frame longer than its bound");
+    HIPCHK(hipMemcpyAsync(dst, ctx->d_out.p, flen, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *out_len = flen;
+    return S3HC_OK;
+}
+
 extern "C" int s3hc_compress_frame(s3hc_ctx* ctx, const uint8_t* src, size_t n, int policy, uint8_t* dst, size_t cap,
                                    size_t* out_len, int* was_compressed) {
+    if (policy == S3HC_BLK_LZ4FLEX_COMPAT) {
+        int rc = host_compat(ctx, src, n, dst, cap, out_len);
+        if (was_compressed) *was_compressed = rc == S3HC_OK;
+        return rc;
+    }
     if (policy != S3HC_BLK_AUTO_LZ4FLEX && policy != S3HC_BLK_64K_PER_FRAME) return fail(S3HC_INVALID_ARG, "policy");
     int rc = host_encode(ctx, src, n, 0, policy, dst, cap, out_len);
     if (was_compressed) *was_compressed = rc == S3HC_OK;

@@ -21,7 +21,7 @@ LIB_PATH = os.environ.get("S3HC_LIB_PATH") or os.path.join(_HERE, "libs3hc_lz4.s
 S3HC_OK, S3HC_CORRUPT, S3HC_CHECKSUM, S3HC_DST_TOO_SMALL = 0, 1, 2, 3
 S3HC_UNSUPPORTED, S3HC_DEVICE, S3HC_INVALID_ARG = 4, 5, 6
 STATUS_NAMES = {0: "OK", 1: "CORRUPT", 2: "CHECKSUM", 3: "DST_TOO_SMALL", 4: "UNSUPPORTED", 5: "DEVICE", 6: "INVALID_ARG"}
-BLK_AUTO_LZ4FLEX, BLK_64K_PER_FRAME = 0, 1
+BLK_AUTO_LZ4FLEX, BLK_64K_PER_FRAME, BLK_LZ4FLEX_COMPAT = 0, 1, 2
 ALG_LZ4, ALG_NONE = 0, 1
 
 
@@ -58,6 +58,7 @@ def _load():
         "s3hc_last_error": (ctypes.c_char_p, []),
         "s3hc_version": (ctypes.c_char_p, []),
         "s3hc_frame_bound": (sz, [sz]),
+        "s3hc_compat_encode_dev": (i32, [vp, vp, vp, vp, u32, vp, vp, vp, vp]),
         "s3hc_compress_frame": (i32, [vp, u8p, sz, i32, u8p, sz, szp, ip]),
         "s3hc_store_mode_frame": (i32, [vp, u8p, sz, u8p, sz, szp]),
         "s3hc_decompressed_bound": (i32, [u8p, sz, szp]),
@@ -224,7 +225,8 @@ class Engine:
         """{kernel name: (total ms, launches)} since the last reset."""
         _check(lib.s3hc_timing_collect(self.h))
         out = {}
-        for name in ("xxh32_side", "xxh32", "enc_parse", "enc_sizes", "enc_emit", "dec_plan", "decode", "dec_finish"):
+        for name in ("xxh32_side", "xxh32", "enc_parse", "enc_sizes", "enc_emit", "dec_plan", "decode", "dec_finish",
+                     "compat"):
             n = lib.s3hc_kernel_count(self.h, name.encode())
             if n:
                 out[name] = (lib.s3hc_last_kernel_ms(self.h, name.encode()), n)
@@ -267,6 +269,27 @@ class Engine:
     def encode_dev(self, plan: "Plan", d_src, d_dst, d_item_off, d_item_len, stream=None):
         _check(lib.s3hc_encode_dev(self.h, plan.h, d_src.data_ptr(), d_dst.data_ptr(), d_dst.numel(),
                                    d_item_off.data_ptr(), d_item_len.data_ptr(), _q(stream)))
+
+    def compat_dst_offsets(self, lengths) -> list:
+        """Frame slots for compat_encode_dev: s3hc_frame_bound(len) bytes per item."""
+        out, o = [], 0
+        for n in lengths:
+            out.append(o)
+            o += frame_bound(n)
+        return out + [o]
+
+    def compat_encode_dev(self, src_off, lengths, d_src, d_dst, d_frame_len, dst_off=None, stream=None) -> list:
+        """lz4_flex-compatible frames (S3HC_BLK_LZ4FLEX_COMPAT), one per item, into slots of
+        frame_bound(len) bytes (dst_off[i]); returns dst_off. Frame lengths land in d_frame_len."""
+        n = len(src_off)
+        if dst_off is None:
+            dst_off = self.compat_dst_offsets(lengths)[:n]
+        a_off = (ctypes.c_uint64 * n)(*src_off)
+        a_len = (ctypes.c_uint32 * n)(*lengths)
+        a_dof = (ctypes.c_uint64 * n)(*dst_off)
+        _check(lib.s3hc_compat_encode_dev(self.h, d_src.data_ptr(), a_off, a_len, n, d_dst.data_ptr(), a_dof,
+                                          d_frame_len.data_ptr(), _q(stream)))
+        return list(dst_off)
 
     def plan_decode(self, frame_off, frame_len, dst_off, dst_cap) -> "Plan":
         n = len(frame_off)
