@@ -85,7 +85,8 @@ struct Sink {
 
 // lzf_compress_internal (oracle/lz4_oracle.c:173-231) for one block; returns false when the
 // payload would not be smaller than the block (or the table rejects nothing but it overflows).
-__device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uint32_t so, uint32_t* dict,
+template <typename TE>
+__device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uint32_t so, TE* dict,
                                uint8_t* tag, Sink& s, int lane) {
     if (len < kMfLimit + 1) return s.last_literals(in, len, 0, lane);
     const uint32_t end_pos_check = len - kMfLimit;
@@ -104,15 +105,22 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
             const bool valid = p <= end_pos_check;
             const uint32_t h = valid ? hash5(in + p) : 0u;
             // volatile: the read-back must see other lanes' tag writes, not this lane's own
-            volatile uint32_t* vd = dict;
+            volatile TE* vd = dict;
             volatile uint8_t* vt = tag;
-            const uint32_t old = valid ? vd[h] : 0u;
+            const uint32_t old = valid ? (uint32_t)vd[h] : 0u;
             if (valid) vt[h] = (uint8_t)lane;
             __builtin_amdgcn_wave_barrier();
-            const bool coll = valid && vt[h] != (uint8_t)lane;
+            const uint64_t cm = __ballot(valid && vt[h] != (uint8_t)lane);
+            // Every lane whose candidate an earlier in-batch duplicate changes sits at or after the
+            // first flagged lane `lo`: a match found before `lo` with the table's candidates is the
+            // serial loop's, and no two lanes up to it share a hash.
+            const uint32_t lo = cm ? (uint32_t)__builtin_ctzll(cm) : 64u;
             uint32_t cand = old;
+            bool m = valid && (so + p - cand <= kMaxDist) && (cand >= so) && ld32(in + (cand - so)) == ld32(in + p);
+            uint64_t mb = __ballot(m);
+            uint32_t k = mb ? (uint32_t)__builtin_ctzll(mb) : 64u;
             int next_dup = 64;  // first later lane of the batch with the same hash
-            if (__ballot(coll)) {
+            if (cm && k >= lo) {
                 int prev_dup = -1;
                 for (int d = 1; d < 64; ++d) {
                     const uint32_t hp = shfl(h, lane - d), vp = shfl(valid ? 1u : 0u, lane - d);
@@ -121,14 +129,16 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
                     if (next_dup == 64 && lane + d < 64 && vn && hn == h) next_dup = lane + d;
                 }
                 const uint32_t pp = shfl(p, prev_dup < 0 ? lane : prev_dup);
-                if (valid && prev_dup >= 0) cand = pp + so;
+                if (valid && prev_dup >= 0) {
+                    cand = pp + so;
+                    m = (so + p - cand <= kMaxDist) && (cand >= so) && ld32(in + (cand - so)) == ld32(in + p);
+                }
+                mb = __ballot(m);
+                k = mb ? (uint32_t)__builtin_ctzll(mb) : 64u;
             }
             const uint32_t cb = cand - so;
-            const bool m = valid && (so + p - cand <= kMaxDist) && (cand >= so) && ld32(in + cb) == ld32(in + p);
-            const uint64_t mb = __ballot(m);
-            const uint32_t k = mb ? (uint32_t)__builtin_ctzll(mb) : 64u;
             // commit the table writes of attempts <= k (the last of equal hashes wins)
-            if (valid && (uint32_t)lane <= k && (next_dup == 64 || next_dup > (int)k)) vd[h] = p + so;
+            if (valid && (uint32_t)lane <= k && (next_dup == 64 || next_dup > (int)k)) vd[h] = (TE)(p + so);
             __builtin_amdgcn_wave_barrier();
             if (mb) {
                 mpos = rdl(p, k);
@@ -169,7 +179,7 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
             dup = dup < lim ? dup : lim;
         }
         c += dup;
-        if (lane == 0) ((volatile uint32_t*)dict)[hash5(in + c - 2)] = c - 2 + so;
+        if (lane == 0) ((volatile TE*)dict)[hash5(in + c - 2)] = (TE)(c - 2 + so);
         __builtin_amdgcn_wave_barrier();
         // ---- sequence
         const uint32_t token = ((lit_len < 15u ? lit_len : 15u) << 4) | (dup < 15u ? dup : 15u);
@@ -185,17 +195,22 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
 
 // One wave per frame: FrameEncoder(FrameInfo{content_checksum, Independent}) + write_all +
 // finish (oracle/lz4_oracle.c:242-279). fhash[f] = xxh32 of the frame's input (seed 0).
+// TE = table entry: u16 for frames of <= 64 KiB (positions < 2^16; 12 KiB of LDS per wave,
+// 13 waves/CU), u32 otherwise (positions + stream offset; 20 KiB, 8 waves/CU). A launch
+// encodes the frames of its class and skips the others.
+template <typename TE>
 __global__ __launch_bounds__(64) void k_compat_frames(const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
                                                       const uint32_t* __restrict__ len, uint32_t n, uint8_t* __restrict__ dst,
                                                       const uint64_t* __restrict__ dst_off,
                                                       const uint32_t* __restrict__ fhash, uint32_t* __restrict__ frame_len) {
-    __shared__ uint32_t dict[kTbl];
+    __shared__ TE dict[kTbl];
     __shared__ uint8_t tag[kTbl];
     const uint32_t f = blockIdx.x;
     if (f >= n) return;
+    const uint32_t N = len[f];
+    if ((N <= 65536u) != (sizeof(TE) == 2)) return;
     const int lane = lane_id();
     const uint8_t* in0 = src + src_off[f];
-    const uint32_t N = len[f];
     uint8_t* o = dst + dst_off[f];
     for (uint32_t t = (uint32_t)lane; t < kTbl; t += 64) dict[t] = 0;  // calloc'd table
     // BlockSize::from_buf_length: <= 64 KiB -> Max64KB, <= 256 KiB -> Max256KB, else Max4MB
@@ -236,10 +251,14 @@ __global__ __launch_bounds__(64) void k_compat_frames(const uint8_t* __restrict_
 
 hipError_t launch_compat_frames(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, uint32_t n,
                                 uint8_t* dst, const uint64_t* dst_off, const uint32_t* fhash, uint32_t* frame_len,
-                                hipStream_t st) {
+                                uint32_t n_small, hipStream_t st) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(compat::k_compat_frames, dim3(n), dim3(64), 0, st, src, src_off, len, n, dst, dst_off, fhash,
-                       frame_len);
+    if (n_small)
+        hipLaunchKernelGGL(compat::k_compat_frames<uint16_t>, dim3(n), dim3(64), 0, st, src, src_off, len, n, dst,
+                           dst_off, fhash, frame_len);
+    if (n_small < n)
+        hipLaunchKernelGGL(compat::k_compat_frames<uint32_t>, dim3(n), dim3(64), 0, st, src, src_off, len, n, dst,
+                           dst_off, fhash, frame_len);
     return hipGetLastError();
 }
 

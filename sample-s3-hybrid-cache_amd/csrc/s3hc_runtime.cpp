@@ -27,7 +27,7 @@
 namespace s3hc {
 hipError_t launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_compat_frames(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint8_t*, const uint64_t*,
-                                const uint32_t*, uint32_t*, hipStream_t);
+                                const uint32_t*, uint32_t*, uint32_t, hipStream_t);
 hipError_t launch_decode_units(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*,
                                int32_t*, const uint8_t*, hipStream_t);
 hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*, int32_t*,
@@ -625,6 +625,8 @@ static int run_compat(s3hc_ctx* ctx, const uint8_t* d_src, const uint64_t* src_o
     if (!n) return S3HC_OK;
     std::vector<uint64_t> so(src_off, src_off + n), dof(dst_off, dst_off + n);
     std::vector<uint32_t> ln(len, len + n);
+    uint32_t n_small = 0;  // frames of <= 64 KiB (16-bit hash-table kernel)
+    for (uint32_t i = 0; i < n; ++i) n_small += ln[i] <= 65536u;
     for (uint32_t i = 0; i + 1 < n; ++i)
         if (dof[i + 1] < dof[i] || dof[i + 1] - dof[i] < s3hc_frame_bound(ln[i]))
             return fail(S3HC_INVALID_ARG, "dst_off leaves less than s3hc_frame_bound(len) per frame");
@@ -638,7 +640,7 @@ static int run_compat(s3hc_ctx* ctx, const uint8_t* d_src, const uint64_t* src_o
     T.end();
     T.begin("compat");
     HIPCHK(launch_compat_frames(d_src, ctx->d_c_soff.as<uint64_t>(), ctx->d_c_len.as<uint32_t>(), n, d_dst,
-                                ctx->d_c_doff.as<uint64_t>(), ctx->d_c_hash.as<uint32_t>(), d_frame_len, st));
+                                ctx->d_c_doff.as<uint64_t>(), ctx->d_c_hash.as<uint32_t>(), d_frame_len, n_small, st));
     T.end();
     // the descriptors live in ctx scratch: the next call may not overwrite them early
     HIPCHK(hipStreamSynchronize(st));
