@@ -40,14 +40,24 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
 __device__ __forceinline__ uint32_t shfl(uint32_t v, int src) {
     return (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)v);
 }
-__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+// Unaligned reads from two aligned dwords (the dword holding p and the next one: never past
+// p + 7, which every caller keeps inside its block).
+struct W5 {
+    uint32_t lo, b4;  // bytes p..p+3 (LE), byte p+4
+};
+__device__ __forceinline__ W5 ld5(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3), w0 = w[0], w1 = w[1];
+    return W5{__builtin_amdgcn_alignbyte(w1, w0, sh), (w1 >> (8 * sh)) & 0xFFu};
 }
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return ld5(p).lo; }
 // hash5 >> HASHTABLE_BIT_SHIFT_4K over the 5 low bytes of the u64 at p (oracle hash5_idx)
-__device__ __forceinline__ uint32_t hash5(const uint8_t* p) {
-    const uint64_t seq = (uint64_t)ld32(p) | ((uint64_t)p[4] << 32);
+__device__ __forceinline__ uint32_t hash5w(W5 v) {
+    const uint64_t seq = (uint64_t)v.lo | ((uint64_t)v.b4 << 32);
     return (uint32_t)((((seq << 24) * 889523592379ull) >> 48) >> 4);
 }
+__device__ __forceinline__ uint32_t hash5(const uint8_t* p) { return hash5w(ld5(p)); }
 
 // Output sink of one block: `sp` bytes written, `cap` = largest payload still worth keeping
 // (one less than the block), uniform across the wave. false = overflow (the block is stored).
@@ -103,7 +113,8 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
             const uint32_t i = i0 + (uint32_t)lane, q = i >> 5, r = i & 31u;
             const uint32_t p = cur + i + 16u * q * (q ? q - 1u : 0u) + q * r;
             const bool valid = p <= end_pos_check;
-            const uint32_t h = valid ? hash5(in + p) : 0u;
+            const W5 wp = valid ? ld5(in + p) : W5{0u, 0u};
+            const uint32_t h = hash5w(wp);
             // volatile: the read-back must see other lanes' tag writes, not this lane's own
             volatile TE* vd = dict;
             volatile uint8_t* vt = tag;
@@ -116,7 +127,7 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
             // serial loop's, and no two lanes up to it share a hash.
             const uint32_t lo = cm ? (uint32_t)__builtin_ctzll(cm) : 64u;
             uint32_t cand = old;
-            bool m = valid && (so + p - cand <= kMaxDist) && (cand >= so) && ld32(in + (cand - so)) == ld32(in + p);
+            bool m = valid && (so + p - cand <= kMaxDist) && (cand >= so) && ld32(in + (cand - so)) == wp.lo;
             uint64_t mb = __ballot(m);
             uint32_t k = mb ? (uint32_t)__builtin_ctzll(mb) : 64u;
             int next_dup = 64;  // first later lane of the batch with the same hash
@@ -131,7 +142,7 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
                 const uint32_t pp = shfl(p, prev_dup < 0 ? lane : prev_dup);
                 if (valid && prev_dup >= 0) {
                     cand = pp + so;
-                    m = (so + p - cand <= kMaxDist) && (cand >= so) && ld32(in + (cand - so)) == ld32(in + p);
+                    m = (so + p - cand <= kMaxDist) && (cand >= so) && ld32(in + (cand - so)) == wp.lo;
                 }
                 mb = __ballot(m);
                 k = mb ? (uint32_t)__builtin_ctzll(mb) : 64u;
@@ -147,38 +158,45 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
             }
             if (~__ballot(valid)) return s.last_literals(in, len, lit_start, lane);  // cur > end_pos_check
         }
-        // ---- backtrack_match
+        // ---- backtrack_match and count_same_bytes, both probed in the same round trip.
+        // The count starts at the backtracked position + 4; its first b bytes lie in the
+        // backtracked + verified run, so dup = b + F with F the equal run from mpos + 4.
         uint32_t c = mpos, cd = mcand;
+        const uint32_t blim = cd < c - lit_start ? cd : c - lit_start;
+        const uint32_t flim = len - kEndOffset > c + kMinMatch ? len - kEndOffset - (c + kMinMatch) : 0u;
+        uint32_t b, F;
         {
-            const uint32_t lim = cd < c - lit_start ? cd : c - lit_start;
-            uint32_t b = 0;
-            while (b < lim) {
+            const uint32_t t = (uint32_t)lane;
+            const bool bne = t < blim && in[c - 1 - t] != in[cd - 1 - t];
+            const bool fne = t < flim && in[c + kMinMatch + t] != in[cd + kMinMatch + t];
+            const uint64_t nb = __ballot(bne), nf = __ballot(fne);
+            b = nb ? (uint32_t)__builtin_ctzll(nb) : 64u;
+            F = nf ? (uint32_t)__builtin_ctzll(nf) : 64u;
+        }
+        if (b == 64u) {  // backtrack run of 64+ bytes
+            while (b < blim) {
                 const uint32_t t = b + (uint32_t)lane;
-                const uint64_t neq = __ballot(t < lim && in[c - 1 - t] != in[cd - 1 - t]);
+                const uint64_t neq = __ballot(t < blim && in[c - 1 - t] != in[cd - 1 - t]);
                 if (neq) { b += (uint32_t)__builtin_ctzll(neq); break; }
                 b += 64;
             }
-            b = b < lim ? b : lim;
-            c -= b;
-            cd -= b;
         }
+        b = b < blim ? b : blim;
+        if (F == 64u) {  // match of 68+ bytes
+            while (F < flim) {
+                const uint32_t t = F + (uint32_t)lane;
+                const uint64_t neq = __ballot(t < flim && in[c + kMinMatch + t] != in[cd + kMinMatch + t]);
+                if (neq) { F += (uint32_t)__builtin_ctzll(neq); break; }
+                F += 64;
+            }
+        }
+        F = F < flim ? F : flim;
+        c -= b;
+        cd -= b;
         const uint32_t lit_len = c - lit_start;
         const uint32_t offset = c - cd;
-        c += kMinMatch;
-        cd += kMinMatch;
-        // ---- count_same_bytes up to len - END_OFFSET
-        uint32_t dup = 0;
-        {
-            const uint32_t lim = len - kEndOffset > c ? len - kEndOffset - c : 0u;
-            while (dup < lim) {
-                const uint32_t t = dup + (uint32_t)lane;
-                const uint64_t neq = __ballot(t < lim && in[c + t] != in[cd + t]);
-                if (neq) { dup += (uint32_t)__builtin_ctzll(neq); break; }
-                dup += 64;
-            }
-            dup = dup < lim ? dup : lim;
-        }
-        c += dup;
+        const uint32_t dup = b + F;
+        c += kMinMatch + dup;
         if (lane == 0) ((volatile TE*)dict)[hash5(in + c - 2)] = (TE)(c - 2 + so);
         __builtin_amdgcn_wave_barrier();
         // ---- sequence
