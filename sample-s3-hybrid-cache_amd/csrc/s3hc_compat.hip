@@ -32,6 +32,10 @@ constexpr uint32_t kMinMatch = 4;   // MINMATCH
 constexpr uint32_t kMfLimit = 12;   // MFLIMIT
 constexpr uint32_t kEndOffset = 6;  // LAST_LITERALS + 1
 constexpr uint32_t kMaxDist = 65535;
+#ifndef S3HC_COMPAT_BATCH
+#define S3HC_COMPAT_BATCH 32
+#endif
+constexpr uint32_t kBatch = S3HC_COMPAT_BATCH;  // attempts speculated per wave step (<= 64)
 
 __device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0)); }
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) {
@@ -109,10 +113,10 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
     for (;;) {
         // ---- scan (speculative over 64 attempts of the skip schedule)
         uint32_t mpos = 0, mcand = 0;
-        for (uint32_t i0 = 0;; i0 += 64) {
+        for (uint32_t i0 = 0;; i0 += kBatch) {
             const uint32_t i = i0 + (uint32_t)lane, q = i >> 5, r = i & 31u;
             const uint32_t p = cur + i + 16u * q * (q ? q - 1u : 0u) + q * r;
-            const bool valid = p <= end_pos_check;
+            const bool valid = (uint32_t)lane < kBatch && p <= end_pos_check;
             const W5 wp = valid ? ld5(in + p) : W5{0u, 0u};
             const uint32_t h = hash5w(wp);
             // volatile: the read-back must see other lanes' tag writes, not this lane's own
@@ -130,14 +134,14 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
             bool m = valid && (so + p - cand <= kMaxDist) && (cand >= so) && ld32(in + (cand - so)) == wp.lo;
             uint64_t mb = __ballot(m);
             uint32_t k = mb ? (uint32_t)__builtin_ctzll(mb) : 64u;
-            int next_dup = 64;  // first later lane of the batch with the same hash
             if (cm && k >= lo) {
+                // previous lane of the batch with the same hash (invalid lanes carry a sentinel
+                // that matches nothing)
+                const uint32_t hv = valid ? h : 0x10000u | (uint32_t)lane;
                 int prev_dup = -1;
-                for (int d = 1; d < 64; ++d) {
-                    const uint32_t hp = shfl(h, lane - d), vp = shfl(valid ? 1u : 0u, lane - d);
-                    const uint32_t hn = shfl(h, lane + d), vn = shfl(valid ? 1u : 0u, lane + d);
-                    if (prev_dup < 0 && lane - d >= 0 && vp && hp == h) prev_dup = lane - d;
-                    if (next_dup == 64 && lane + d < 64 && vn && hn == h) next_dup = lane + d;
+                for (int d = 1; d < (int)kBatch; ++d) {
+                    const uint32_t hp = shfl(hv, lane - d);
+                    if (prev_dup < 0 && lane - d >= 0 && hp == hv) prev_dup = lane - d;
                 }
                 const uint32_t pp = shfl(p, prev_dup < 0 ? lane : prev_dup);
                 if (valid && prev_dup >= 0) {
@@ -148,15 +152,27 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
                 k = mb ? (uint32_t)__builtin_ctzll(mb) : 64u;
             }
             const uint32_t cb = cand - so;
-            // commit the table writes of attempts <= k (the last of equal hashes wins)
-            if (valid && (uint32_t)lane <= k && (next_dup == 64 || next_dup > (int)k)) vd[h] = (TE)(p + so);
+            // commit the table writes of attempts <= k. Equal hashes: every committing lane
+            // stores, then lanes still seeing a smaller position of their group store again, so
+            // the slot ends with the group's last (largest) position, as the serial writes leave it
+            const bool commit = valid && (uint32_t)lane <= k;
+            if (commit) vd[h] = (TE)(p + so);
+            if (cm) {
+                for (;;) {
+                    __builtin_amdgcn_wave_barrier();
+                    const bool fix = commit && (uint32_t)vd[h] < p + so;
+                    if (!__ballot(fix)) break;
+                    if (fix) vd[h] = (TE)(p + so);
+                }
+            }
             __builtin_amdgcn_wave_barrier();
             if (mb) {
                 mpos = rdl(p, k);
                 mcand = rdl(cb, k);
                 break;
             }
-            if (~__ballot(valid)) return s.last_literals(in, len, lit_start, lane);  // cur > end_pos_check
+            if (__ballot(!valid && (uint32_t)lane < kBatch))  // cur > end_pos_check
+                return s.last_literals(in, len, lit_start, lane);
         }
         // ---- backtrack_match and count_same_bytes, both probed in the same round trip.
         // The count starts at the backtracked position + 4; its first b bytes lie in the
