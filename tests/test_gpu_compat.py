@@ -115,3 +115,48 @@ def test_compat_rejects_short_slots(engine):
     with pytest.raises(S.CodecError) as e:
         engine.compat_encode_dev([0, 500], [500, 500], d_src, d_dst, d_len, dst_off=[0, 100])
     assert e.value.status == 6  # S3HC_INVALID_ARG
+
+
+@pytest.mark.parametrize("n", [4 * MiB, 4 * MiB + 1, 256 * KiB + 1])
+def test_compat_block_boundaries(engine, oracle, n):
+    # exactly one Max4MB block, a second block of 1 byte, and the smallest BD 0x70 frame
+    data = synth.log_text(n, 23)
+    got = engine.compress_frame(data, S.BLK_LZ4FLEX_COMPAT)
+    assert got == oracle.lz4flex_compress_frame(data)
+    assert engine.decompress_frames(got) == data
+
+
+def test_compat_random_batch(engine, oracle):
+    # 300 seeded items of 0..6000 bytes mixing runs, text, random bytes and repeats (one launch)
+    rng = np.random.default_rng(2024)
+    parts = []
+    for i in range(300):
+        n = int(rng.integers(0, 6000))
+        kind = i % 5
+        if kind == 0:
+            b = rnd(n, 100 + i)
+        elif kind == 1:
+            b = synth.log_text(n, 200 + i) if n else b""
+        elif kind == 2:
+            b = bytes(rng.integers(0, 3, n, dtype=np.uint8) * 85)
+        elif kind == 3:
+            unit = rnd(int(rng.integers(1, 40)), 300 + i)
+            b = (unit * (n // max(len(unit), 1) + 1))[:n]
+        else:
+            b = small_alphabet(n, 400 + i)
+        parts.append(b)
+    data = b"".join(parts)
+    src_off, o = [], 0
+    for p in parts:
+        src_off.append(o)
+        o += len(p)
+    lens = [len(p) for p in parts]
+    d_src = engine.upload(data + b"\0" * 16)
+    slots = engine.compat_dst_offsets(lens)
+    d_dst, d_len = engine.alloc(slots[-1]), engine.alloc(4 * len(parts))
+    dst_off = engine.compat_encode_dev(src_off, lens, d_src, d_dst, d_len)
+    engine.sync()
+    flen = d_len.u32(len(parts))
+    raw = d_dst.read()
+    bad = [i for i, p in enumerate(parts) if raw[dst_off[i]: dst_off[i] + flen[i]] != oracle.lz4flex_compress_frame(p)]
+    assert not bad, f"items differing from the oracle: {bad[:10]}"
