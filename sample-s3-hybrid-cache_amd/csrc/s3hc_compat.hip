@@ -28,6 +28,7 @@ namespace s3hc {
 namespace compat {
 
 constexpr uint32_t kTbl = 4096;     // HashTable4K
+constexpr uint32_t kTagShift = 1;   // duplicate-detection tags: one per 2 table slots (false flags only cost the resolution pass)
 constexpr uint32_t kMinMatch = 4;   // MINMATCH
 constexpr uint32_t kMfLimit = 12;   // MFLIMIT
 constexpr uint32_t kEndOffset = 6;  // LAST_LITERALS + 1
@@ -123,9 +124,9 @@ __device__ bool compress_block(const uint8_t* __restrict__ in, uint32_t len, uin
             volatile TE* vd = dict;
             volatile uint8_t* vt = tag;
             const uint32_t old = valid ? (uint32_t)vd[h] : 0u;
-            if (valid) vt[h] = (uint8_t)lane;
+            if (valid) vt[h >> kTagShift] = (uint8_t)lane;
             __builtin_amdgcn_wave_barrier();
-            const uint64_t cm = __ballot(valid && vt[h] != (uint8_t)lane);
+            const uint64_t cm = __ballot(valid && vt[h >> kTagShift] != (uint8_t)lane);
             // Every lane whose candidate an earlier in-batch duplicate changes sits at or after the
             // first flagged lane `lo`: a match found before `lo` with the table's candidates is the
             // serial loop's, and no two lanes up to it share a hash.
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(64) void k_compat_frames(const uint8_t* __restrict_
                                                       const uint64_t* __restrict__ dst_off,
                                                       const uint32_t* __restrict__ fhash, uint32_t* __restrict__ frame_len) {
     __shared__ TE dict[kTbl];
-    __shared__ uint8_t tag[kTbl];
+    __shared__ uint8_t tag[kTbl >> kTagShift];
     const uint32_t f = blockIdx.x;
     if (f >= n) return;
     const uint32_t N = len[f];
