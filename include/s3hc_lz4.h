@@ -219,7 +219,9 @@ int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t flush_bytes,
 int s3hc_aggregator_flush(s3hc_aggregator* a);
 /* Layout of compressed batches: S3HC_BLK_AUTO_LZ4FLEX (default, one frame per batch as
  * flush_batch writes it) or S3HC_BLK_64K_PER_FRAME (64 KiB frames: a reference reader decodes
- * them the same, the GPU decoder runs one wave per 64 KiB instead of per batch). */
+ * them the same, the GPU decoder runs one wave per 64 KiB instead of per batch), or
+ * S3HC_BLK_LZ4FLEX_COMPAT (flush_batch's frames with lz4_flex's own block bytes, via
+ * s3hc_compat_encode_dev; store-mode batches of the same flush still share one launch). */
 int s3hc_aggregator_set_frame_policy(s3hc_aggregator* a, int policy);
 /* Encode launches and batches encoded so far. */
 void s3hc_aggregator_counters(const s3hc_aggregator* a, uint64_t* launches, uint64_t* batches);

@@ -42,6 +42,10 @@ struct Batch {
 };
 
 // Device + pinned host staging reused across flushes (grown on demand).
+// Batch mode of S3HC_BLK_LZ4FLEX_COMPAT (not a plan mode: those batches go through
+// s3hc_compat_encode_dev, the rest of the flush through one s3hc_encode_dev launch).
+constexpr uint8_t kModeCompat = 3;
+
 struct Staging {
     void* h_in = nullptr;
     size_t h_in_cap = 0;
@@ -55,6 +59,10 @@ struct Staging {
     size_t d_out_cap = 0;
     void* d_meta = nullptr;
     size_t d_meta_cap = 0;
+    void* d_cout = nullptr;  // compat frames (slots of s3hc_frame_bound bytes) and lengths
+    size_t d_cout_cap = 0;
+    void* h_cout = nullptr;
+    size_t h_cout_cap = 0;
 };
 
 int grow_host(s3hc_ctx* ctx, void** p, size_t* cap, size_t n) {
@@ -86,7 +94,7 @@ struct s3hc_aggregator {
     size_t flush_bytes;
     uint32_t flush_batches;
     s3hc_handler* stats;     // optional shared counters (the writers' Arc<CompressionStatsAtomic>)
-    uint8_t compress_mode = 0;  // plan mode of compressed batches: 0 lz4_flex Auto, 2 64 KiB frames
+    uint8_t compress_mode = 0;  // compressed batches: 0 lz4_flex Auto, 2 64 KiB frames, kModeCompat
     void* queue = nullptr;   // the aggregator's HIP queue
     std::mutex mu;           // guards pending / pending_bytes / counters
     std::mutex flush_mu;     // one aggregated flush at a time (keeps per-writer frame order)
@@ -154,28 +162,65 @@ static int aggregated_flush(s3hc_aggregator* a) {
     if (!rc) rc = grow_dev(ctx, &S.d_in, &S.d_in_cap, total + 64);
     if (rc) return fail_all(rc, "staging allocation");
     for (uint32_t i = 0; i < n; ++i) memcpy((uint8_t*)S.h_in + off[i], work[i].data.data(), len[i]);
-    s3hc_plan* plan = nullptr;
-    rc = s3hc_plan_encode(ctx, off.data(), len.data(), mode.data(), n, &plan);
-    if (rc) return fail_all(rc, "plan");
-    const uint64_t bound = s3hc_plan_dst_bound(plan);
-    rc = grow_dev(ctx, &S.d_out, &S.d_out_cap, bound + 64);
-    if (!rc) rc = grow_host(ctx, &S.h_out, &S.h_out_cap, bound + 64);
-    if (!rc) rc = grow_dev(ctx, &S.d_meta, &S.d_meta_cap, 12ull * n + 64);
-    if (!rc) rc = grow_host(ctx, &S.h_meta, &S.h_meta_cap, 12ull * n + 64);
-    uint64_t* d_ioff = (uint64_t*)S.d_meta;
-    uint32_t* d_ilen = (uint32_t*)((uint8_t*)S.d_meta + 8ull * n);
+    // plan-encoded batches (Auto / 64 KiB frames / store-mode) and compat batches
+    std::vector<uint32_t> ia, ic;
+    for (uint32_t i = 0; i < n; ++i) (mode[i] == kModeCompat ? ic : ia).push_back(i);
     if (!rc && total) rc = s3hc_memcpy_async(ctx, S.d_in, S.h_in, total, 1, a->queue);
-    if (!rc) rc = s3hc_encode_dev(ctx, plan, (const uint8_t*)S.d_in, (uint8_t*)S.d_out, S.d_out_cap, d_ioff, d_ilen, a->queue);
-    if (!rc) rc = s3hc_memcpy_async(ctx, S.h_meta, S.d_meta, 12ull * n, 2, a->queue);
-    if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
-    s3hc_plan_free(plan);
-    if (rc) return fail_all(rc, "encode");
-    const uint64_t* io = (const uint64_t*)S.h_meta;
-    const uint32_t* il = (const uint32_t*)((const uint8_t*)S.h_meta + 8ull * n);
-    const uint64_t frames = io[n - 1] + il[n - 1];  // frames are packed in item order
-    rc = s3hc_memcpy_async(ctx, S.h_out, S.d_out, frames, 2, a->queue);
-    if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
-    if (rc) return fail_all(rc, "frame copy");
+    if (rc) return fail_all(rc, "staging copy");
+    std::vector<const uint8_t*> frame(n);
+    std::vector<uint32_t> flen(n);
+    if (!ia.empty()) {
+        const uint32_t na = (uint32_t)ia.size();
+        std::vector<uint64_t> offa(na);
+        std::vector<uint32_t> lena(na);
+        std::vector<uint8_t> modea(na);
+        for (uint32_t j = 0; j < na; ++j) { offa[j] = off[ia[j]]; lena[j] = len[ia[j]]; modea[j] = mode[ia[j]]; }
+        s3hc_plan* plan = nullptr;
+        rc = s3hc_plan_encode(ctx, offa.data(), lena.data(), modea.data(), na, &plan);
+        if (rc) return fail_all(rc, "plan");
+        const uint64_t bound = s3hc_plan_dst_bound(plan);
+        rc = grow_dev(ctx, &S.d_out, &S.d_out_cap, bound + 64);
+        if (!rc) rc = grow_host(ctx, &S.h_out, &S.h_out_cap, bound + 64);
+        if (!rc) rc = grow_dev(ctx, &S.d_meta, &S.d_meta_cap, 12ull * na + 64);
+        if (!rc) rc = grow_host(ctx, &S.h_meta, &S.h_meta_cap, 12ull * na + 64);
+        uint64_t* d_ioff = (uint64_t*)S.d_meta;
+        uint32_t* d_ilen = (uint32_t*)((uint8_t*)S.d_meta + 8ull * na);
+        if (!rc) rc = s3hc_encode_dev(ctx, plan, (const uint8_t*)S.d_in, (uint8_t*)S.d_out, S.d_out_cap, d_ioff, d_ilen, a->queue);
+        if (!rc) rc = s3hc_memcpy_async(ctx, S.h_meta, S.d_meta, 12ull * na, 2, a->queue);
+        if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
+        s3hc_plan_free(plan);
+        if (rc) return fail_all(rc, "encode");
+        const uint64_t* io = (const uint64_t*)S.h_meta;
+        const uint32_t* il = (const uint32_t*)((const uint8_t*)S.h_meta + 8ull * na);
+        const uint64_t bytes = io[na - 1] + il[na - 1];  // frames are packed in item order
+        rc = s3hc_memcpy_async(ctx, S.h_out, S.d_out, bytes, 2, a->queue);
+        if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
+        if (rc) return fail_all(rc, "frame copy");
+        for (uint32_t j = 0; j < na; ++j) { frame[ia[j]] = (const uint8_t*)S.h_out + io[j]; flen[ia[j]] = il[j]; }
+    }
+    if (!ic.empty()) {
+        const uint32_t nc = (uint32_t)ic.size();
+        std::vector<uint64_t> offc(nc), dof(nc);
+        std::vector<uint32_t> lenc(nc);
+        uint64_t slots = 0;
+        for (uint32_t j = 0; j < nc; ++j) {
+            offc[j] = off[ic[j]];
+            lenc[j] = len[ic[j]];
+            dof[j] = slots;
+            slots += s3hc_frame_bound(lenc[j]);
+        }
+        const uint64_t lens_at = (slots + 15) & ~15ull;
+        rc = grow_dev(ctx, &S.d_cout, &S.d_cout_cap, lens_at + 4ull * nc + 64);
+        if (!rc) rc = grow_host(ctx, &S.h_cout, &S.h_cout_cap, lens_at + 4ull * nc + 64);
+        uint32_t* d_clen = (uint32_t*)((uint8_t*)S.d_cout + lens_at);
+        if (!rc) rc = s3hc_compat_encode_dev(ctx, (const uint8_t*)S.d_in, offc.data(), lenc.data(), nc,
+                                             (uint8_t*)S.d_cout, dof.data(), d_clen, a->queue);
+        if (!rc) rc = s3hc_memcpy_async(ctx, S.h_cout, S.d_cout, lens_at + 4ull * nc, 2, a->queue);
+        if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
+        if (rc) return fail_all(rc, "compat encode");
+        const uint32_t* cl = (const uint32_t*)((const uint8_t*)S.h_cout + lens_at);
+        for (uint32_t j = 0; j < nc; ++j) { frame[ic[j]] = (const uint8_t*)S.h_cout + dof[j]; flen[ic[j]] = cl[j]; }
+    }
     {
         std::lock_guard<std::mutex> g(a->mu);
         a->launches++;
@@ -184,14 +229,14 @@ static int aggregated_flush(s3hc_aggregator* a) {
     // deliver in queue order: each writer's frames keep their batch order
     for (uint32_t i = 0; i < n; ++i) {
         s3hc_writer* w = work[i].w;
-        const uint8_t* fr = (const uint8_t*)S.h_out + io[i];
+        const uint8_t* fr = frame[i];
         int src = S3HC_OK;
         if (!w->error) {
-            if (w->sink && w->sink(w->user, fr, il[i]) != 0) {
+            if (w->sink && w->sink(w->user, fr, flen[i]) != 0) {
                 src = S3HC_INVALID_ARG;
             } else {
-                w->compressed_bytes_written += il[i];
-                if (a->stats) s3hc_handler_record_batch_bytes(a->stats, len[i], il[i]);
+                w->compressed_bytes_written += flen[i];
+                if (a->stats) s3hc_handler_record_batch_bytes(a->stats, len[i], flen[i]);
             }
         }
         std::lock_guard<std::mutex> g(a->mu);
@@ -254,10 +299,11 @@ extern "C" int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t f
 }
 
 extern "C" int s3hc_aggregator_set_frame_policy(s3hc_aggregator* a, int policy) {
-    if (!a || (policy != S3HC_BLK_AUTO_LZ4FLEX && policy != S3HC_BLK_64K_PER_FRAME))
+    if (!a || (policy != S3HC_BLK_AUTO_LZ4FLEX && policy != S3HC_BLK_64K_PER_FRAME &&
+               policy != S3HC_BLK_LZ4FLEX_COMPAT))
         return werr(S3HC_INVALID_ARG, "bad arguments");
     std::lock_guard<std::mutex> g(a->mu);
-    a->compress_mode = policy == S3HC_BLK_64K_PER_FRAME ? 2 : 0;
+    a->compress_mode = policy == S3HC_BLK_64K_PER_FRAME ? 2 : (policy == S3HC_BLK_LZ4FLEX_COMPAT ? kModeCompat : 0);
     return S3HC_OK;
 }
 
@@ -287,6 +333,8 @@ extern "C" void s3hc_aggregator_destroy(s3hc_aggregator* a) {
     if (S.d_in) s3hc_dev_free(ctx, S.d_in);
     if (S.d_out) s3hc_dev_free(ctx, S.d_out);
     if (S.d_meta) s3hc_dev_free(ctx, S.d_meta);
+    if (S.h_cout) s3hc_host_free(ctx, S.h_cout);
+    if (S.d_cout) s3hc_dev_free(ctx, S.d_cout);
     if (a->queue) s3hc_queue_destroy(ctx, a->queue);
     delete a;
 }

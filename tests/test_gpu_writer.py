@@ -260,3 +260,37 @@ def test_64k_frame_policy(engine, oracle):
         assert got == want
         k += len(_frames(want))
         o += n
+
+
+def test_compat_frame_policy(engine, oracle):
+    # S3HC_BLK_LZ4FLEX_COMPAT: each batch becomes the frame lz4_flex's FrameEncoder writes in
+    # flush_batch (disk_cache.rs:1829-1846), byte for byte as the oracle restates it; a
+    # compression-disabled writer in the same flush still gets store-mode frames
+    import s3hc_lz4 as S
+
+    agg = _agg(engine, 256 * 1024, flush_batches=8, frame_policy=S.BLK_LZ4FLEX_COMPAT)
+    data = synth.log_text(3 * 256 * 1024 + 54_321, 41)
+    raw = synth.jpeg_like(300_000, 42)
+    w = agg.begin(0, len(data) - 1, True)
+    w2 = agg.begin(0, len(raw) - 1, False)
+    for i in range(0, len(data), 70_000):
+        w.write(data[i:i + 70_000])
+    for i in range(0, len(raw), 70_000):
+        w2.write(raw[i:i + 70_000])
+    f1, f2 = w.file, w2.file
+    w.commit()
+    w2.commit()
+    file, file2 = bytes(f1), bytes(f2)
+    assert oracle.decompress_data(file) == data and oracle.decompress_data(file2) == raw
+    assert engine.decompress_frames(file) == data
+    o = 0
+    for fr in _frames(file):
+        u = len(oracle.decompress_data(fr))
+        assert fr == oracle.lz4flex_compress_frame(data[o:o + u])
+        o += u
+    assert o == len(data)
+    o = 0
+    for fr in _frames(file2):
+        u = len(oracle.decompress_data(fr))
+        assert fr == oracle.store_mode_frame(raw[o:o + u])
+        o += u
