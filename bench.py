@@ -8,34 +8,42 @@ FLG 0x64, BD 0x40, xxh32 content checksum; frames packed contiguously) then deco
 frame back (frame walk, block decode, xxh32 verify). value = uncompressed bytes of all
 ranks / (max over ranks of the timed wall time), i.e. U / (t_enc + t_dec).
 
-Multi-GPU: one process per GPU (torch.distributed.run), blocks sharded across ranks with
-no data-path collective (weak scaling: 4096 blocks per GPU); a gloo (CPU) group provides
-the barrier and the max-over-ranks reduction of the timed interval.
+Multi-GPU: one process per GPU, blocks sharded across ranks with no
+data-path collective; a gloo (CPU) group provides the barrier and the max-over-ranks
+reduction of the timed interval. `--gpus N` works both ways:
+  * under torch.distributed.run (WORLD_SIZE set): this process is one rank; WORLD_SIZE must
+    equal N;
+  * standalone: this process spawns N fresh rank processes (RANK/LOCAL_RANK/WORLD_SIZE,
+    rendezvous on 127.0.0.1) before anything touches the GPU, waits for them and relays
+    rank 0's line.
+Default weak scaling: 4096 blocks per GPU (config 2 per GPU). `--total-blocks 1048576` is
+config 5's strong-scaling split (131,072 blocks = 8 GiB per GPU at N = 8).
 
-The roofline object is for the dominant kernel of the step, from HIP events recorded inside
-the library on the launch stream over the timed steps. cpu_baseline times the CPU port of
-the reference path (oracle/: the lz4_flex FrameEncoder/FrameDecoder restatement) on the
-host's cores over a bounded sample of the same workload (rank 0, N=1 only).
+The `roofline` object is for the dominant kernel of the step; `roofline_decode` is the
+north_star's decode figure (C + U per launch of the decoder over its launch time). Kernel
+times come from HIP events recorded inside the library on the launch stream over the timed
+steps. `cpu_baseline` times the CPU port of the reference path (oracle/: the lz4_flex
+FrameEncoder/FrameDecoder restatement) on every host core over a bounded sample of the same
+workload (rank 0, N = 1 only): median of 5 runs of >= 1 s.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "sample-s3-hybrid-cache_amd")]
 
-import s3hc_lz4 as S  # noqa: E402
-import shard  # noqa: E402
-import synth  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s spec, 6.3 measured)
 METRIC = "LZ4 encode+decode GiB/s (device-resident), 64 KiB blocks, 1/2/4/8 GPU"
 GiB = float(1 << 30)
+CHUNK_BLOCKS = 4096  # synthetic input is generated / uploaded / checked 256 MiB at a time
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -45,70 +53,147 @@ def parse_args():
                     help="strong scaling instead: split this many blocks over the ranks (config 5: 1048576)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--skip-check", action="store_true", help="diagnostic builds only: skip output checks")
-    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall seconds of the CPU baseline sample")
-    return ap.parse_args()
+    ap.add_argument("--cpu-seconds", type=float, default=1.0, help="wall seconds of each of the 5 CPU baseline runs")
+    ap.add_argument("--selftest", action="store_true",
+                    help="launcher/rank plumbing only (no GPU): every rank reports in, rank 0 prints the summary")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(data: bytes, block: int, seconds: float):
-    """Oracle (C port of the reference path) on the host cores, encode+decode per block."""
+# ------------------------------------------------------------------ launcher (no GPU in here)
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Run this script as n rank processes (fresh interpreters, never an exec of this one);
+    relay rank 0's stdout. Returns the exit code (first failing rank's, else 0)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = procs[0].communicate()[0]
+    rc = procs[0].returncode
+    for p in procs[1:]:
+        try:
+            p.wait(timeout=600)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+        rc = rc or p.returncode
+    if rc:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    sys.stdout.write(out0.decode())
+    sys.stdout.flush()
+    return rc
+
+
+def launch_decision(args):
+    """None = run as a rank in this process; int = exit code of the spawned ranks."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}: refusing to mislabel the run\n")
+            return 2
+        return None
+    if args.gpus > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:])
+    return None
+
+
+def selftest(args):
+    import shard
+
+    g = shard.Group()
+    total = args.total_blocks or args.blocks * g.world
+    lo, hi = shard.shard_range(total, g.world, g.rank) if args.total_blocks else (g.rank * args.blocks, (g.rank + 1) * args.blocks)
+    g.barrier()
+    ranks = g.sum(1.0)
+    blocks = g.sum(float(hi - lo))
+    if g.rank == 0:
+        print(json.dumps({"selftest": True, "n_gpus": g.world, "ranks_reporting": int(ranks),
+                          "blocks_total": int(blocks), "scaling": "strong" if args.total_blocks else "weak"}))
+    g.close()
+
+
+# ------------------------------------------------------------------ CPU baseline (rank 0, N = 1)
+def host_cpu_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
+    return model, quota
+
+
+def cpu_baseline(data_chunk: bytes, block: int, seconds: float):
+    """Oracle (C port of the reference path) on every host core, encode+decode per block:
+    median of 5 runs of >= `seconds` wall each, plus a single-thread run."""
     import ctypes
-    from concurrent.futures import ThreadPoolExecutor
+    import statistics
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # CPU baseline leg only
 
     L = O.lib()
-    threads = max(1, min(16, os.cpu_count() or 1))
-    nb = len(data) // block
-    buf = ctypes.create_string_buffer(data, len(data))
-    base = ctypes.addressof(buf)
-    cap = O.lib().or_frame_bound(block)
+    L.or_bench_blocks.restype = ctypes.c_int
+    L.or_bench_blocks.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.c_double,
+                                  ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
+    nb = len(data_chunk) // block
+    buf = ctypes.create_string_buffer(data_chunk, len(data_chunk))
 
-    def work(lo, count):
-        fr = ctypes.create_string_buffer(cap)
-        out = ctypes.create_string_buffer(block)
-        n = ctypes.c_size_t()
-        te = td = 0.0
-        for k in range(count):
-            i = (lo + k) % nb
-            t0 = time.perf_counter()
-            L.or_lz4flex_compress_frame(base + i * block, block, fr, cap, ctypes.byref(n))
-            t1 = time.perf_counter()
-            m = ctypes.c_size_t()
-            rc = L.or_decompress_data(fr, n.value, out, block, ctypes.byref(m))
-            t2 = time.perf_counter()
-            assert rc == 0 and m.value == block
-            te += t1 - t0
-            td += t2 - t1
-        return te, td, count
+    def run(threads, secs, fixed=0):
+        done, wall, es, ds = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        rc = L.or_bench_blocks(buf, nb, block, threads, secs, fixed, ctypes.byref(done), ctypes.byref(wall),
+                               ctypes.byref(es), ctypes.byref(ds))
+        assert rc == 0, f"cpu baseline round trip failed ({rc})"
+        return done.value, wall.value, es.value, ds.value
 
-    # single thread: seconds per block (encode + decode)
-    te, td, k = work(0, min(nb, 64))
-    per_blk = (te + td) / k
-    # all threads, each on its own contiguous block range (one request per blocking thread),
-    # sized to ~`seconds` of wall time
-    per_thread = max(1, int(seconds / per_blk))
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        futs = [ex.submit(work, (t * nb) // threads, per_thread) for t in range(threads)]
-        res = [f.result() for f in futs]
-    wall = time.perf_counter() - t0
-    blocks = sum(r[2] for r in res)
+    n1, w1, e1, d1 = run(1, seconds)
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    runs = []
+    for _ in range(5):
+        n, w, _, _ = run(threads, seconds)
+        runs.append(n * block / w / GiB)
+    model, quota = host_cpu_info()
     return {
-        "value": round(blocks * block / wall / GiB, 4),
+        "value": round(statistics.median(runs), 4),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{blocks} x 64 KiB blocks of the same log-text batch (lz4_flex-faithful frame encode + decompress_data "
-                  f"per block, oracle/ C port -O3), {threads} threads over contiguous block ranges, {wall:.2f} s wall "
-                  f"= {wall * threads:.1f} CPU-s",
-        "single_thread_gibps": round(block / per_blk / GiB, 4),
-        "single_thread_encode_gibps": round(k * block / te / GiB, 4),
-        "single_thread_decode_gibps": round(k * block / td / GiB, 4),
+        "sample": f"64 KiB blocks of the bench's own log-text batch ({nb} distinct blocks, cycled), lz4_flex-faithful "
+                  f"frame encode + decompress_data per block (oracle/ C port, -O3), {threads} threads over contiguous "
+                  f"block ranges; median of 5 runs of >= {seconds:g} s wall",
+        "runs_gibps": [round(x, 4) for x in runs],
+        "single_thread_gibps": round(n1 * block / w1 / GiB, 4),
+        "single_thread_encode_gibps": round(n1 * block / e1 / GiB, 4),
+        "single_thread_decode_gibps": round(n1 * block / d1 / GiB, 4),
         "host_nproc": os.cpu_count(),
+        "cpu_affinity": threads,
+        "cgroup_cpu_quota": quota,
+        "cpu_model": model,
     }
 
 
+# ------------------------------------------------------------------ the GPU bench (one rank)
 KERNEL_SYMBOL = {"enc_parse": "k_enc_parse", "enc_emit": "k_enc_emit", "decode": "k_decode_units",
                  "xxh32": "k_xxh32_ranges"}
 
@@ -129,8 +214,32 @@ def pmc_traffic(kernel):
     return int((2 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024), os.path.relpath(files[-1], ROOT)
 
 
-def main():
-    args = parse_args()
+def roofline_obj(kt, name, alg_bytes, profiled_shape: bool):
+    ms, n = kt[name]
+    per_launch_s = ms / n / 1e3
+    achieved = alg_bytes / per_launch_s / 1e9
+    # the committed PMC summary is of the default command (4096 blocks); other shapes get none
+    traffic, tsrc = pmc_traffic(name) if profiled_shape else (None, None)
+    roof = {
+        "bound": "hbm", "kernel": KERNEL_SYMBOL.get(name, name), "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+        "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(ms / n, 4),
+    }
+    if tsrc:
+        roof["traffic_source"] = tsrc + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same bench command)"
+    return roof
+
+
+def chunk_seed(rank: int, c: int) -> int:
+    import synth
+    return synth.SEED_BASE + 1 + 1000 * rank + 7919 * c
+
+
+def run_rank(args):
+    import s3hc_lz4 as S
+    import shard
+    import synth
+
     g = shard.Group()
     world, rank, local = g.world, g.rank, g.local
     block = 65536
@@ -139,12 +248,19 @@ def main():
         nb = hi - lo
     else:
         nb = args.blocks
-    eng = S.Engine(local % max(1, S.device_count()))  # one process per GPU (shared GPU only in CPU-box rehearsals)
+    eng = S.Engine(local % max(1, S.device_count()))  # one process per GPU (shared GPU only in 1-GPU rehearsals)
 
-    # ---- synthetic batch, resident in HBM before timing (distinct data per rank)
-    data = synth.log_text(nb * block, synth.SEED_BASE + 1 + 1000 * rank)
+    # ---- synthetic batch (distinct content, 256 MiB chunks), resident in HBM before timing
+    nchunks = -(-nb // CHUNK_BLOCKS)
+    d_src = eng.alloc(nb * block)
+    first_chunk = None
+    for c in range(nchunks):
+        k = min(CHUNK_BLOCKS, nb - c * CHUNK_BLOCKS)
+        part = synth.log_text(k * block, chunk_seed(rank, c))
+        d_src.write(part, c * CHUNK_BLOCKS * block)
+        if c == 0:
+            first_chunk = part
     offs = [i * block for i in range(nb)]
-    d_src = eng.upload(data)
     plan = eng.plan_encode(offs, [block] * nb)
     d_frames = eng.alloc(plan.dst_bound)
     d_ioff, d_ilen = eng.alloc(8 * nb), eng.alloc(4 * nb)
@@ -169,7 +285,7 @@ def main():
     if not args.skip_check:
         st = d_ost.i32(nb)
         assert st == [0] * nb, f"decode status {set(st)}"
-        assert d_out.read(2 * block) == data[: 2 * block]
+        assert d_out.read(2 * block) == first_chunk[: 2 * block]
 
     eng.timing_reset()
     eng.set_timing(True)
@@ -185,42 +301,46 @@ def main():
     elapsed = g.max(t1 - t0)
     kt = eng.timing()
 
-    # full-output check after the timed steps
+    # full-output check after the timed steps: every block, every byte, chunk by chunk
+    checked = 0
     if not args.skip_check:
         assert d_ost.i32(nb) == [0] * nb
-        assert d_out.read() == data, "decoded batch differs from the input"
+        assert d_olen.u32(nb) == [block] * nb
+        for c in range(nchunks):
+            k = min(CHUNK_BLOCKS, nb - c * CHUNK_BLOCKS)
+            want = first_chunk if c == 0 else synth.log_text(k * block, chunk_seed(rank, c))
+            assert d_out.read(k * block, c * CHUNK_BLOCKS * block) == want, f"decoded chunk {c} differs from the input"
+            checked += k
+    checked_all = g.sum(float(checked))
 
     total_u = g.sum(float(nb * block)) * args.steps
     value = total_u / elapsed / GiB
 
-    # ---- roofline for the dominant kernel
+    # ---- rooflines: the dominant kernel, and the decoder (north_star target)
     # side-stream spans overlap the match finder, so they never count as the dominant kernel
     excl = {k: v for k, v in kt.items() if not k.endswith("_side")}
+    alg = {
+        "enc_parse": nb * block,                  # U read once (match finding)
+        "enc_emit": nb * block + comp_bytes,      # U literals read + C framed bytes written
+        "decode": comp_bytes + nb * block,        # C read + U written
+        "xxh32": nb * block,                      # U read (decode-side verify)
+    }
     dom = max(excl, key=lambda k: excl[k][0]) if excl else None
-    roof = None
-    if dom:
-        ms, n = kt[dom]
-        per_launch_s = ms / n / 1e3
-        # algorithmic bytes per launch: each kernel's own reads + writes
-        alg = {
-            "enc_parse": nb * block,                  # U read once (match finding)
-            "enc_emit": nb * block + comp_bytes,      # U literals read + C framed bytes written
-            "decode": comp_bytes + nb * block,        # C read + U written
-            "xxh32": nb * block,                      # U read (decode-side verify; encode side runs on the side stream)
-        }.get(dom, nb * block)
-        achieved = alg / per_launch_s / 1e9
-        traffic, tsrc = pmc_traffic(dom)
-        roof = {
-            "bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(ms / n, 4),
-        }
-        if tsrc:
-            roof["traffic_source"] = tsrc + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same bench command)"
+    prof = nb == 4096 and not args.total_blocks
+    roof = roofline_obj(kt, dom, alg.get(dom, nb * block), prof) if dom else None
+    roof_dec = roofline_obj(kt, "decode", alg["decode"], prof) if "decode" in kt else None
     per_kernel = {k: round(v[0] / args.steps, 4) for k, v in kt.items()}
+    rank_rate = nb * block * args.steps / (t1 - t0) / GiB
+    rates = [rank_rate]
+    if g.dist is not None:
+        import torch
+        t = torch.tensor([rank_rate], dtype=torch.float64)
+        lst = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        g.dist.all_gather(lst, t)
+        rates = [float(x.item()) for x in lst]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(data, block, args.cpu_seconds)
+        cpu = cpu_baseline(first_chunk, block, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -235,19 +355,33 @@ def main():
             "scaling": "strong" if args.total_blocks else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic S3 access-log text (SURVEY.md §8d config 2), seeded, distinct per rank",
+            "data": "synthetic S3 access-log text (SURVEY.md §8d config 2), seeded, every block distinct, distinct per rank",
             "config": {
                 "workload": (f"config5: {args.total_blocks} x 64 KiB log-text blocks split over {world} GPUs" if args.total_blocks
                              else f"config2: {nb} x 64 KiB log-text blocks per GPU") + ", LZ4 frame encode + decode, device-resident",
                 "blocks_per_gpu": nb, "block_bytes": block, "frame": "FLG 0x64 BD 0x40 (lz4_flex Auto), xxh32 content checksum",
                 "compression_ratio": round(comp_bytes / (nb * block), 4), "parallelism": f"shard{world}",
             },
+            "per_gpu_gibps": [round(x, 3) for x in rates],
+            "blocks_checked": int(checked_all),
             "kernel_ms_per_step": per_kernel,
             "roofline": roof,
+            "roofline_decode": roof_dec,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     g.close()
+
+
+def main():
+    args = parse_args()
+    rc = launch_decision(args)
+    if rc is not None:
+        sys.exit(rc)
+    if args.selftest:
+        selftest(args)
+    else:
+        run_rank(args)
 
 
 if __name__ == "__main__":

@@ -64,6 +64,11 @@ size_t or_decompressed_bound(const uint8_t* src, size_t n);
 /* One raw LZ4 block (no frame) with lz4_flex decompress_internal semantics. */
 int or_decode_block(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len);
 
+/* cpu_bench.c: bench.py's cpu_baseline harness — encode (or_lz4flex_compress_frame) + decode
+ * (or_decompress_data) of 'block'-byte blocks on 'threads' threads over contiguous ranges. */
+int or_bench_blocks(const uint8_t* data, size_t nblocks, size_t block, int threads, double seconds,
+                    size_t fixed_per_thread, uint64_t* blocks_done, double* wall, double* enc_s, double* dec_s);
+
 #ifdef __cplusplus
 }
 #endif

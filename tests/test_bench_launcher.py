@@ -1,0 +1,66 @@
+"""bench.py's multi-GPU entry point on CPU (no GPU touched): `--gpus N` without a launcher
+spawns N rank processes itself and reports n_gpus = N; under torch.distributed.run a
+WORLD_SIZE that disagrees with --gpus is refused instead of mislabelling the run; the synthetic
+corpus is distinct per block and deterministic."""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH] + args, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def _line(out):
+    return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_flag_spawns_ranks(n):
+    r = _run(["--gpus", str(n), "--selftest"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == n and d["ranks_reporting"] == n
+    assert d["blocks_total"] == 4096 * n and d["scaling"] == "weak"
+
+
+def test_config5_strong_split():
+    r = _run(["--gpus", "2", "--total-blocks", "1048576", "--selftest"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["blocks_total"] == 1048576 and d["scaling"] == "strong"
+
+
+def test_mismatched_world_size_is_refused():
+    r = _run(["--gpus", "8", "--selftest"], {"WORLD_SIZE": "1", "RANK": "0"})
+    assert r.returncode == 2
+    assert "refusing" in r.stderr
+
+
+def test_single_gpu_default_needs_no_launcher():
+    r = _run(["--selftest"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert _line(r.stdout)["n_gpus"] == 1
+
+
+def test_synthetic_corpus_distinct_and_deterministic():
+    import synth
+
+    d = synth.log_text(256 * 65536, 123)
+    assert d == synth.log_text(256 * 65536, 123, threads=1)
+    assert d != synth.log_text(256 * 65536, 124)
+    assert len({hashlib.sha1(d[i:i + 65536]).digest() for i in range(0, len(d), 65536)}) == 256
+    assert synth.log_text(1000, 5) == synth.log_text(5000, 5)[:1000]  # prefix-stable
+    j = synth.json_records(64 * 65536, 7)
+    assert j.startswith(b'{"id":1,') and len({j[i:i + 65536] for i in range(0, len(j), 65536)}) == 64
+    m, modes = synth.mixed_blocks(6, 65536)
+    assert modes == [0, 1, 0, 1, 0, 1] and m[65536:65540] == b"\xff\xd8\xff\xe0"
