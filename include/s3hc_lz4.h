@@ -198,6 +198,21 @@ void s3hc_handler_record_object(s3hc_handler* h, int compressed);
 /* is_denylisted_extension (:252-308). */
 int s3hc_is_denylisted_extension(const char* path);
 
+/* ---- the cache layer's compression decision (the codec's caller) ------------ */
+/* strip_known_cache_key_suffixes (cache.rs:226-275): the object path of a cache key — a trailing
+ * ":range:<digits>-<digits>" and then ":part:<digits>" are removed, nothing else. Writes the path
+ * NUL-terminated into out (truncated to cap - 1 bytes) and returns its full length. */
+size_t s3hc_strip_known_cache_key_suffixes(const char* cache_key, char* out, size_t cap);
+/* CacheManager::effective_compression (cache.rs:1158-1178): 1 = compress (compress_with_algorithm),
+ * 0 = store-mode. compression_enabled / compression_from_rule are ResolvedSettings'
+ * (bucket_settings.rs:364): the rule-or-global enable flag and whether a rule set it. Order:
+ * disabled -> 0; size < threshold -> 0; set by a rule -> 1; else !denylisted(stripped key). */
+int s3hc_effective_compression(int compression_enabled, int compression_from_rule,
+                               size_t compression_threshold, const char* cache_key, uint64_t size);
+/* The same with the handler's threshold (CompressionHandler::new(threshold, ..), cache.rs:1076-1083). */
+int s3hc_handler_effective_compression(const s3hc_handler* h, int compression_enabled,
+                                       int compression_from_rule, const char* cache_key, uint64_t size);
+
 /* ---- batched incremental writers + cross-request aggregator ---------------- */
 /* IncrementalRangeWriter (disk_cache.rs:262-305) with flush_batch (:1820-1870) routed
  * through an aggregator that encodes the full batches of many writers in one GPU launch

@@ -187,6 +187,41 @@ bool CompressionHandler::decompress_with_algorithm(const uint8_t* data, size_t n
     return decompress_data(data, n, out, err);
 }
 
+static bool all_ascii_digits(const std::string& s, size_t from, size_t to) {
+    for (size_t i = from; i < to; ++i)
+        if (s[i] < '0' || s[i] > '9') return false;
+    return true;
+}
+
+std::string strip_known_cache_key_suffixes(const std::string& key) {  // cache.rs:226-258
+    static const std::string kRange = ":range:", kPart = ":part:";
+    size_t end = key.size();
+    const size_t r = key.rfind(kRange);
+    if (r != std::string::npos) {
+        // is_range_suffix_body (cache.rs:261-271): split at the first '-', both sides non-empty digits
+        const size_t b = r + kRange.size();
+        const size_t dash = key.find('-', b);
+        if (dash != std::string::npos && dash > b && dash + 1 < key.size() && all_ascii_digits(key, b, dash) &&
+            all_ascii_digits(key, dash + 1, key.size()))
+            end = r;
+    }
+    const std::string head = key.substr(0, end);
+    const size_t p = head.rfind(kPart);
+    if (p != std::string::npos) {
+        const size_t b = p + kPart.size();
+        if (b < head.size() && all_ascii_digits(head, b, head.size())) return head.substr(0, p);
+    }
+    return head;
+}
+
+bool effective_compression(const ResolvedCompression& resolved, size_t threshold, const std::string& cache_key,
+                           uint64_t size) {  // cache.rs:1158-1178
+    if (!resolved.compression_enabled) return false;
+    if ((size_t)size < threshold) return false;
+    if (resolved.compression_from_rule) return true;
+    return !CompressionHandler::is_denylisted_extension(strip_known_cache_key_suffixes(cache_key));
+}
+
 }  // namespace s3hc
 
 // ------------------------------------------------------------ C wrappers
@@ -260,4 +295,25 @@ extern "C" void s3hc_handler_record_object(s3hc_handler* h, int compressed) {
 }
 extern "C" int s3hc_is_denylisted_extension(const char* path) {
     return path && CompressionHandler::is_denylisted_extension(path);
+}
+extern "C" size_t s3hc_strip_known_cache_key_suffixes(const char* cache_key, char* out, size_t cap) {
+    if (!cache_key) return 0;
+    const std::string p = s3hc::strip_known_cache_key_suffixes(cache_key);
+    if (out && cap) {
+        const size_t k = p.size() < cap - 1 ? p.size() : cap - 1;
+        memcpy(out, p.data(), k);
+        out[k] = 0;
+    }
+    return p.size();
+}
+extern "C" int s3hc_effective_compression(int compression_enabled, int compression_from_rule,
+                                          size_t compression_threshold, const char* cache_key, uint64_t size) {
+    return s3hc::effective_compression({compression_enabled != 0, compression_from_rule != 0}, compression_threshold,
+                                       cache_key ? cache_key : "", size);
+}
+extern "C" int s3hc_handler_effective_compression(const s3hc_handler* h, int compression_enabled,
+                                                  int compression_from_rule, const char* cache_key, uint64_t size) {
+    if (!h) return 0;
+    return s3hc_effective_compression(compression_enabled, compression_from_rule, h->h.compression_threshold(),
+                                      cache_key, size);
 }

@@ -79,13 +79,30 @@ public:
                                    std::vector<uint8_t>& out, CodecError* err) const;    // :594-604
 
     s3hc_ctx* ctx() const { return ctx_; }
+    size_t compression_threshold() const { return threshold_; }
 
 private:
     s3hc_ctx* ctx_;
-    [[maybe_unused]] size_t threshold_;  // compression.rs:176-183: kept, not read
+    size_t threshold_;  // compression.rs:176-183 (the codec never reads it; effective_compression does)
     bool enabled_;
     CompressionAlgorithm preferred_;
     std::shared_ptr<CompressionStatsAtomic> stats_;
 };
+
+// The compression decision of the cache layer (the caller of this codec): which ranges go through
+// compress_with_algorithm and which through encode_store_mode_frame.
+// cache.rs:226-275: strip the `:range:<digits>-<digits>` suffix (last), then `:part:<digits>`, from
+// the end of a cache key; anything else (a colon inside the object key) is left alone.
+std::string strip_known_cache_key_suffixes(const std::string& cache_key);
+// bucket_settings.rs:364 ResolvedSettings (the two fields the decision reads)
+struct ResolvedCompression {
+    bool compression_enabled;    // resolved: rule override or global config
+    bool compression_from_rule;  // a cache rule set compression_enabled explicitly
+};
+// cache.rs:1158-1178 CacheManager::effective_compression: disabled -> false; size below the
+// threshold -> false; a rule said so -> true (any extension); else the extension denylist on the
+// key with its suffixes stripped.
+bool effective_compression(const ResolvedCompression& resolved, size_t compression_threshold,
+                           const std::string& cache_key, uint64_t size);
 
 }  // namespace s3hc

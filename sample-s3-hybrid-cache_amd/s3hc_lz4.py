@@ -92,6 +92,9 @@ def _load():
         "s3hc_handler_record_batch_bytes": (None, [vp, u64, u64]),
         "s3hc_handler_record_object": (None, [vp, i32]),
         "s3hc_is_denylisted_extension": (i32, [ctypes.c_char_p]),
+        "s3hc_strip_known_cache_key_suffixes": (sz, [ctypes.c_char_p, ctypes.c_char_p, sz]),
+        "s3hc_effective_compression": (i32, [i32, i32, sz, ctypes.c_char_p, u64]),
+        "s3hc_handler_effective_compression": (i32, [vp, i32, i32, ctypes.c_char_p, u64]),
         "s3hc_dev_alloc": (i32, [vp, sz, ctypes.POINTER(vp)]),
         "s3hc_dev_free": (i32, [vp, vp]),
         "s3hc_memcpy": (i32, [vp, vp, vp, sz, i32]),
@@ -148,6 +151,28 @@ def _check(rc: int):
 def is_denylisted_extension(path: str) -> bool:
     """CompressionHandler::is_denylisted_extension (compression.rs:252-255)."""
     return bool(lib.s3hc_is_denylisted_extension(path.encode()))
+
+
+def strip_known_cache_key_suffixes(cache_key: str) -> str:
+    """cache.rs:226-275: the object path of a cache key (":range:a-b" then ":part:n" stripped)."""
+    k = cache_key.encode()
+    n = lib.s3hc_strip_known_cache_key_suffixes(k, None, 0)
+    out = ctypes.create_string_buffer(n + 1)
+    lib.s3hc_strip_known_cache_key_suffixes(k, out, n + 1)
+    return out.raw[:n].decode()
+
+
+@dataclass
+class ResolvedSettings:  # bucket_settings.rs:364 (the fields effective_compression reads)
+    compression_enabled: bool = True
+    compression_from_rule: bool = False
+
+
+def effective_compression(resolved: ResolvedSettings, compression_threshold: int, cache_key: str, size: int) -> bool:
+    """CacheManager::effective_compression (cache.rs:1158-1178)."""
+    return bool(lib.s3hc_effective_compression(1 if resolved.compression_enabled else 0,
+                                               1 if resolved.compression_from_rule else 0,
+                                               compression_threshold, cache_key.encode(), size))
 
 
 def device_count() -> int:
@@ -605,6 +630,12 @@ class CompressionHandler:
 
     def record_batch_bytes(self, before: int, after: int):
         lib.s3hc_handler_record_batch_bytes(self.h, before, after)
+
+    def effective_compression(self, resolved: ResolvedSettings, cache_key: str, size: int) -> bool:
+        """cache.rs:1158-1178 with this handler's threshold (the CacheManager's compression_threshold)."""
+        return bool(lib.s3hc_handler_effective_compression(self.h, 1 if resolved.compression_enabled else 0,
+                                                           1 if resolved.compression_from_rule else 0,
+                                                           cache_key.encode(), size))
 
     def record_object(self, compressed: bool):
         lib.s3hc_handler_record_object(self.h, 1 if compressed else 0)

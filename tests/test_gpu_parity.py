@@ -14,6 +14,7 @@ import pytest
 
 import lz4ref
 import synth
+import s3hc_lz4 as S
 
 pytestmark = pytest.mark.gpu
 
@@ -247,7 +248,11 @@ def test_batch_config2_log_blocks(engine, oracle):
 
 
 def test_batch_config3_mixed(engine, oracle):
-    data, modes = synth.mixed_blocks(128)
+    data, kinds = synth.mixed_blocks(128)
+    # the reference's decision per cache key (cache.rs:1158-1178): JPEG ranges -> store-mode
+    keys = [f"b/o{i}{'.jpg' if k else '.json'}:range:{65536 * i}-{65536 * i + 65535}" for i, k in enumerate(kinds)]
+    modes = [0 if S.effective_compression(S.ResolvedSettings(), 1024, key, 65536) else 1 for key in keys]
+    assert modes == kinds
     _batch_roundtrip(engine, oracle, data, 65536, modes)
 
 

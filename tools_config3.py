@@ -29,8 +29,10 @@ def main():
     a = ap.parse_args()
     nb, block = a.blocks, 65536
     data, _ = synth.mixed_blocks(nb, block)
-    # the decision the reference makes per object key (compression.rs:252-308)
-    modes = [1 if S.is_denylisted_extension(f"bucket/obj-{i}{'.json' if i % 2 == 0 else '.jpg'}") else 0
+    # the decision the reference makes per cache key (cache.rs:1158-1178 effective_compression)
+    modes = [0 if S.effective_compression(S.ResolvedSettings(), 1024,
+                                          f"bucket/obj-{i}{'.json' if i % 2 == 0 else '.jpg'}:range:{i * block}-{i * block + block - 1}",
+                                          block) else 1
              for i in range(nb)]
     eng = S.Engine(0)
     offs = [i * block for i in range(nb)]
