@@ -33,6 +33,7 @@ extern "C" {
 #define S3HC_UNSUPPORTED 4    /* dictionary id, legacy/skippable frame, ... */
 #define S3HC_DEVICE 5         /* HIP runtime error / no device */
 #define S3HC_INVALID_ARG 6
+#define S3HC_NO_MEMORY 7      /* a host or device allocation failed (no exception crosses this ABI) */
 
 /* Frame layout policies for s3hc_compress_frame. */
 #define S3HC_BLK_AUTO_LZ4FLEX 0  /* lz4_flex FrameEncoder BlockSize::Auto: one frame, BD by input size */
@@ -74,9 +75,16 @@ int s3hc_store_mode_frame(s3hc_ctx* ctx, const uint8_t* src, size_t n,
 int s3hc_decompressed_bound(const uint8_t* src, size_t n, size_t* bound);
 
 /* Replaces CompressionHandler::decompress_data (compression.rs:463-502): decode
- * concatenated frames; a frame that yields no bytes ends the loop (Ok(0) => break). */
+ * concatenated frames; a frame that yields no bytes ends the loop (Ok(0) => break).
+ * Device scratch follows the decoded size (frames are decoded in passes of <= 2 GiB of
+ * output slots; a block reserves min(frame block size, 255 x its compressed size)). */
 int s3hc_decompress_frames(s3hc_ctx* ctx, const uint8_t* src, size_t n,
                            uint8_t* dst, size_t cap, size_t* out_len);
+/* The same into a library-allocated buffer of exactly the decoded size (the reference returns
+ * an owned Vec<u8>, grown by read_to_end); release it with s3hc_buffer_free. */
+int s3hc_decompress_frames_alloc(s3hc_ctx* ctx, const uint8_t* src, size_t n,
+                                 uint8_t** out, size_t* out_len);
+void s3hc_buffer_free(uint8_t* p);
 
 /* ---- streaming decoder (stream_range_data, disk_cache.rs:3850-3935) ------- */
 /* Feed compressed bytes in any pieces; read decoded bytes frame by frame.

@@ -95,7 +95,8 @@ def decompressed_bound(data) -> int:
 def decompress_data(data, cap: int | None = None) -> bytes:
     """compression.rs:463-502 decompress_data (concatenated frames)."""
     if cap is None:
-        cap = decompressed_bound(data)
+        # no LZ4 block decodes to more than 255 bytes per compressed byte
+        cap = min(decompressed_bound(data), 255 * len(data) + 64)
     return _frame_call(lib().or_decompress_data, data, cap)
 
 

@@ -2,6 +2,7 @@
 // follow src/compression.rs line by line (cited per method); all codec work is the GPU
 // engine's (s3hc_compress_frame / s3hc_store_mode_frame / s3hc_decompress_frames).
 #include "compression_handler.hpp"
+#include "s3hc_guard.hpp"
 
 #include <algorithm>
 #include <cctype>
@@ -163,18 +164,14 @@ bool CompressionHandler::compress_with_algorithm(const uint8_t* data, size_t n, 
 
 bool CompressionHandler::decompress_data(const uint8_t* data, size_t n, std::vector<uint8_t>& out,
                                          CodecError* err) const {
-    size_t bound = 0;
-    s3hc_decompressed_bound(data, n, &bound);
-    out.resize(bound);
-    size_t len = 0;
-    int rc = s3hc_decompress_frames(ctx_, data, n, out.data(), out.size(), &len);
+    // output grows by the decoded bytes (read_to_end), never by a worst-case bound
+    int rc = decompress_frames_vec(ctx_, data, n, out);
     if (rc) {  // :483-492
         stats_->decompression_failures.fetch_add(1, std::memory_order_relaxed);
         if (err) *err = {rc, std::string("Failed to decompress cached data: ") + s3hc_last_error()};
         out.clear();
         return false;
     }
-    out.resize(len);
     return true;
 }
 
@@ -232,14 +229,30 @@ struct s3hc_handler {
     CompressionHandler h;
 };
 
+template <class F>
+static int guarded(F&& f) {
+    return s3hc::guarded_call(s3hc::set_error, f);  // message via s3hc_last_error()
+}
+template <class F>
+static s3hc_handler* make_handler(F&& f) {
+    try {
+        return new s3hc_handler{f()};
+    } catch (...) {
+        s3hc::set_error(S3HC_NO_MEMORY, "handler allocation failed");
+        return nullptr;
+    }
+}
+
 extern "C" s3hc_handler* s3hc_handler_new(s3hc_ctx* ctx, size_t threshold, int enabled) {
-    return new s3hc_handler{CompressionHandler(ctx, threshold, enabled != 0)};
+    return make_handler([&] { return CompressionHandler(ctx, threshold, enabled != 0); });
 }
 extern "C" s3hc_handler* s3hc_handler_new_with_shared_stats(size_t threshold, int enabled, const s3hc_handler* src) {
     if (!src) return nullptr;
-    return new s3hc_handler{CompressionHandler::with_shared_stats(threshold, enabled != 0, src->h)};
+    return make_handler([&] { return CompressionHandler::with_shared_stats(threshold, enabled != 0, src->h); });
 }
-extern "C" s3hc_handler* s3hc_handler_clone(const s3hc_handler* h) { return h ? new s3hc_handler{h->h} : nullptr; }
+extern "C" s3hc_handler* s3hc_handler_clone(const s3hc_handler* h) {
+    return h ? make_handler([&] { return h->h; }) : nullptr;
+}
 extern "C" void s3hc_handler_free(s3hc_handler* h) { delete h; }
 extern "C" int s3hc_handler_is_compression_enabled(const s3hc_handler* h) { return h && h->h.is_compression_enabled(); }
 
@@ -253,28 +266,34 @@ static int copy_out(const std::vector<uint8_t>& v, uint8_t* dst, size_t cap, siz
 extern "C" int s3hc_handler_compress_with_metadata(s3hc_handler* h, const uint8_t* src, size_t n, const char* path,
                                                    int should_compress, uint8_t* dst, size_t cap, size_t* out_len,
                                                    int* algorithm, int* was_compressed) {
-    if (!h) return S3HC_INVALID_ARG;
-    auto r = h->h.compress_with_metadata(src, n, path ? path : "", should_compress != 0);
-    if (algorithm) *algorithm = (int)r.algorithm;
-    if (was_compressed) *was_compressed = r.was_compressed;
-    return copy_out(r.data, dst, cap, out_len);
+    return guarded([&]() -> int {
+        if (!h) return S3HC_INVALID_ARG;
+        auto r = h->h.compress_with_metadata(src, n, path ? path : "", should_compress != 0);
+        if (algorithm) *algorithm = (int)r.algorithm;
+        if (was_compressed) *was_compressed = r.was_compressed;
+        return copy_out(r.data, dst, cap, out_len);
+    });
 }
 extern "C" int s3hc_handler_compress_with_algorithm(s3hc_handler* h, const uint8_t* src, size_t n, int algorithm,
                                                     uint8_t* dst, size_t cap, size_t* out_len, int* was_compressed) {
-    if (!h) return S3HC_INVALID_ARG;
-    s3hc::CompressionResult r;
-    s3hc::CodecError e{0, ""};
-    if (!h->h.compress_with_algorithm(src, n, (CompressionAlgorithm)algorithm, r, &e)) return e.status;
-    if (was_compressed) *was_compressed = r.was_compressed;
-    return copy_out(r.data, dst, cap, out_len);
+    return guarded([&]() -> int {
+        if (!h) return S3HC_INVALID_ARG;
+        s3hc::CompressionResult r;
+        s3hc::CodecError e{0, ""};
+        if (!h->h.compress_with_algorithm(src, n, (CompressionAlgorithm)algorithm, r, &e)) return e.status;
+        if (was_compressed) *was_compressed = r.was_compressed;
+        return copy_out(r.data, dst, cap, out_len);
+    });
 }
 extern "C" int s3hc_handler_decompress_with_algorithm(s3hc_handler* h, const uint8_t* src, size_t n, int algorithm,
                                                       uint8_t* dst, size_t cap, size_t* out_len) {
-    if (!h) return S3HC_INVALID_ARG;
-    std::vector<uint8_t> out;
-    s3hc::CodecError e{0, ""};
-    if (!h->h.decompress_with_algorithm(src, n, (CompressionAlgorithm)algorithm, out, &e)) return e.status;
-    return copy_out(out, dst, cap, out_len);
+    return guarded([&]() -> int {
+        if (!h) return S3HC_INVALID_ARG;
+        std::vector<uint8_t> out;
+        s3hc::CodecError e{0, ""};
+        if (!h->h.decompress_with_algorithm(src, n, (CompressionAlgorithm)algorithm, out, &e)) return e.status;
+        return copy_out(out, dst, cap, out_len);
+    });
 }
 extern "C" void s3hc_handler_stats(const s3hc_handler* h, uint64_t out[6], float* ratio) {
     if (!h) return;
@@ -294,7 +313,9 @@ extern "C" void s3hc_handler_record_object(s3hc_handler* h, int compressed) {
     if (h) h->h.shared_stats()->record_object(compressed != 0);
 }
 extern "C" int s3hc_is_denylisted_extension(const char* path) {
-    return path && CompressionHandler::is_denylisted_extension(path);
+    return guarded([&]() -> int {
+        return path && CompressionHandler::is_denylisted_extension(path);
+    });
 }
 extern "C" size_t s3hc_strip_known_cache_key_suffixes(const char* cache_key, char* out, size_t cap) {
     if (!cache_key) return 0;
@@ -308,12 +329,16 @@ extern "C" size_t s3hc_strip_known_cache_key_suffixes(const char* cache_key, cha
 }
 extern "C" int s3hc_effective_compression(int compression_enabled, int compression_from_rule,
                                           size_t compression_threshold, const char* cache_key, uint64_t size) {
-    return s3hc::effective_compression({compression_enabled != 0, compression_from_rule != 0}, compression_threshold,
-                                       cache_key ? cache_key : "", size);
+    return guarded([&]() -> int {
+        return s3hc::effective_compression({compression_enabled != 0, compression_from_rule != 0}, compression_threshold,
+                                           cache_key ? cache_key : "", size);
+    });
 }
 extern "C" int s3hc_handler_effective_compression(const s3hc_handler* h, int compression_enabled,
                                                   int compression_from_rule, const char* cache_key, uint64_t size) {
-    if (!h) return 0;
-    return s3hc_effective_compression(compression_enabled, compression_from_rule, h->h.compression_threshold(),
-                                      cache_key, size);
+    return guarded([&]() -> int {
+        if (!h) return 0;
+        return s3hc_effective_compression(compression_enabled, compression_from_rule, h->h.compression_threshold(),
+                                          cache_key, size);
+    });
 }

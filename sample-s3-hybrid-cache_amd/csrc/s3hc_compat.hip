@@ -59,7 +59,8 @@ __device__ __forceinline__ W5 ld5(const uint8_t* p) {
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) { return ld5(p).lo; }
 // hash5 >> HASHTABLE_BIT_SHIFT_4K over the 5 low bytes of the u64 at p (oracle hash5_idx)
 // In 32-bit halves: X = seq << 24 (X_lo = lo << 24, X_hi = lo >> 8 | b4 << 24), P = 207·2^32 +
-// 465362107; bits 48..59 of X·P are bits 16..27 of X_hi·P_lo + X_lo·207 + mulhi(X_lo, P_lo).
+// 465362107. The table index is hash5 >> 4 = bits 52..63 of X·P (the oracle's >> 48 then >> 4),
+// i.e. bits 20..31 of the high word hi = X_hi·P_lo + X_lo·207 + mulhi(X_lo, P_lo) (mod 2^32).
 __device__ __forceinline__ uint32_t hash5w(W5 v) {
     const uint32_t xl = v.lo << 24, xh = (v.lo >> 8) | (v.b4 << 24);
     const uint32_t hi = xh * 465362107u + xl * 207u + __umulhi(xl, 465362107u);

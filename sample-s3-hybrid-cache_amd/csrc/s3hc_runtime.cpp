@@ -23,6 +23,7 @@
 
 #include "s3hc_lz4.h"
 #include "s3hc_plan.hpp"
+#include "s3hc_guard.hpp"
 
 namespace s3hc {
 hipError_t launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*, hipStream_t);
@@ -62,6 +63,11 @@ static int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+template <class F>
+static int guarded(F&& f) {
+    return s3hc::guarded_call(fail, f);
+}
+int s3hc::set_error(int code, const std::string& msg) { return fail(code, msg); }
 #define HIPCHK(expr)                                                                        \
     do {                                                                                    \
         hipError_t e_ = (expr);                                                             \
@@ -389,18 +395,20 @@ static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t
 
 // ------------------------------------------------------------ C ABI: ctx
 extern "C" int s3hc_create(s3hc_ctx** out, int device) {
-    if (!out) return fail(S3HC_INVALID_ARG, "out is NULL");
-    *out = nullptr;
-    int n = 0;
-    hipError_t e = hipGetDeviceCount(&n);
-    if (e != hipSuccess || n == 0) return fail(S3HC_DEVICE, "no HIP device available (the engine has no CPU path)");
-    if (device < 0 || device >= n) return fail(S3HC_INVALID_ARG, "device index out of range");
-    HIPCHK(hipSetDevice(device));
-    std::unique_ptr<s3hc_ctx> c(new s3hc_ctx);
-    c->device = device;
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    *out = c.release();
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!out) return fail(S3HC_INVALID_ARG, "out is NULL");
+        *out = nullptr;
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        if (e != hipSuccess || n == 0) return fail(S3HC_DEVICE, "no HIP device available (the engine has no CPU path)");
+        if (device < 0 || device >= n) return fail(S3HC_INVALID_ARG, "device index out of range");
+        HIPCHK(hipSetDevice(device));
+        std::unique_ptr<s3hc_ctx> c(new s3hc_ctx);
+        c->device = device;
+        HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        *out = c.release();
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_device_count(void) {
     int n = 0;
@@ -415,20 +423,22 @@ extern "C" void s3hc_destroy(s3hc_ctx* ctx) {
 extern "C" void s3hc_set_timing(s3hc_ctx* ctx, int enabled) { if (ctx) ctx->timing = enabled != 0; }
 // Resolve recorded spans into per-name totals (ms) and launch counts; clears the spans.
 extern "C" int s3hc_timing_collect(s3hc_ctx* ctx) {
-    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
-    std::lock_guard<std::mutex> g(ctx->mu);
-    HIPCHK(hipSetDevice(ctx->device));
-    for (auto& t : ctx->pending) {
-        HIPCHK(hipEventSynchronize(t.b));
-        float ms = 0.f;
-        HIPCHK(hipEventElapsedTime(&ms, t.a, t.b));
-        ctx->kernel_ms[t.name] += ms;
-        ctx->kernel_n[t.name] += 1;
-        ctx->event_pool.push_back(t.a);
-        ctx->event_pool.push_back(t.b);
-    }
-    ctx->pending.clear();
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        HIPCHK(hipSetDevice(ctx->device));
+        for (auto& t : ctx->pending) {
+            HIPCHK(hipEventSynchronize(t.b));
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, t.a, t.b));
+            ctx->kernel_ms[t.name] += ms;
+            ctx->kernel_n[t.name] += 1;
+            ctx->event_pool.push_back(t.a);
+            ctx->event_pool.push_back(t.b);
+        }
+        ctx->pending.clear();
+        return S3HC_OK;
+    });
 }
 extern "C" void s3hc_timing_reset(s3hc_ctx* ctx) {
     if (!ctx) return;
@@ -442,9 +452,11 @@ extern "C" float s3hc_last_kernel_ms(const s3hc_ctx* ctx, const char* name) {
     return it == ctx->kernel_ms.end() ? -1.f : it->second;
 }
 extern "C" int s3hc_kernel_count(const s3hc_ctx* ctx, const char* name) {
-    if (!ctx || !name) return 0;
-    auto it = ctx->kernel_n.find(name);
-    return it == ctx->kernel_n.end() ? 0 : it->second;
+    return guarded([&]() -> int {
+        if (!ctx || !name) return 0;
+        auto it = ctx->kernel_n.find(name);
+        return it == ctx->kernel_n.end() ? 0 : it->second;
+    });
 }
 
 extern "C" size_t s3hc_frame_bound(size_t n) {
@@ -455,124 +467,132 @@ extern "C" size_t s3hc_frame_bound(size_t n) {
 // ------------------------------------------------------ C ABI: batch encode
 extern "C" int s3hc_plan_encode(s3hc_ctx* ctx, const uint64_t* src_off, const uint32_t* len, const uint8_t* mode,
                                 uint32_t n, s3hc_plan** out) {
-    if (!ctx || !out || (n && (!src_off || !len))) return fail(S3HC_INVALID_ARG, "bad arguments");
-    std::lock_guard<std::mutex> g(ctx->mu);
-    HIPCHK(hipSetDevice(ctx->device));
-    std::unique_ptr<s3hc_plan> P(new s3hc_plan);
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint8_t m = mode ? mode[i] : 0;
-        if (m > 2) return fail(S3HC_INVALID_ARG, "mode must be 0, 1 or 2");
-        plan_item(P.get(), src_off[i], len[i], m == 1 ? 1 : 0, m == 2 ? S3HC_BLK_64K_PER_FRAME : S3HC_BLK_AUTO_LZ4FLEX);
-    }
-    int rc = plan_upload_encode(P.get(), ctx->stream);
-    if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    *out = P.release();
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx || !out || (n && (!src_off || !len))) return fail(S3HC_INVALID_ARG, "bad arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        HIPCHK(hipSetDevice(ctx->device));
+        std::unique_ptr<s3hc_plan> P(new s3hc_plan);
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint8_t m = mode ? mode[i] : 0;
+            if (m > 2) return fail(S3HC_INVALID_ARG, "mode must be 0, 1 or 2");
+            plan_item(P.get(), src_off[i], len[i], m == 1 ? 1 : 0, m == 2 ? S3HC_BLK_64K_PER_FRAME : S3HC_BLK_AUTO_LZ4FLEX);
+        }
+        int rc = plan_upload_encode(P.get(), ctx->stream);
+        if (rc) return rc;
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        *out = P.release();
+        return S3HC_OK;
+    });
 }
 extern "C" uint64_t s3hc_plan_dst_bound(const s3hc_plan* P) { return P ? P->dst_bound : 0; }
 extern "C" void s3hc_plan_free(s3hc_plan* P) { delete P; }
 
 extern "C" int s3hc_encode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t* d_dst, uint64_t dst_cap,
                                uint64_t* d_item_off, uint32_t* d_item_len, void* stream) {
-    if (!ctx || !P || !P->is_encode || !d_item_off || !d_item_len) return fail(S3HC_INVALID_ARG, "bad arguments");
-    if (dst_cap < P->dst_bound) return fail(S3HC_DST_TOO_SMALL, "dst_cap < s3hc_plan_dst_bound(plan)");
-    std::lock_guard<std::mutex> g(ctx->mu);
-    HIPCHK(hipSetDevice(ctx->device));
-    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
-    return run_encode(ctx, P, d_src, d_dst, d_item_off, d_item_len, st);
+    return guarded([&]() -> int {
+        if (!ctx || !P || !P->is_encode || !d_item_off || !d_item_len) return fail(S3HC_INVALID_ARG, "bad arguments");
+        if (dst_cap < P->dst_bound) return fail(S3HC_DST_TOO_SMALL, "dst_cap < s3hc_plan_dst_bound(plan)");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        HIPCHK(hipSetDevice(ctx->device));
+        hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+        return run_encode(ctx, P, d_src, d_dst, d_item_off, d_item_len, st);
+    });
 }
 
 // ------------------------------------------------------ C ABI: batch decode
 extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const uint32_t* frame_len,
                                 const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t n, s3hc_plan** out) {
-    if (!ctx || !out || (n && (!frame_off || !frame_len || !dst_off || !dst_cap)))
-        return fail(S3HC_INVALID_ARG, "bad arguments");
-    std::lock_guard<std::mutex> g(ctx->mu);
-    HIPCHK(hipSetDevice(ctx->device));
-    std::unique_ptr<s3hc_plan> P(new s3hc_plan);
-    P->is_encode = false;
-    P->nframes = n;
-    uint64_t cap = 0;
-    for (uint32_t i = 0; i < n; ++i) cap += dst_cap[i] / 65536u + 2u;
-    if (cap > 0xFFFFFFF0ull) return fail(S3HC_INVALID_ARG, "batch too large");
-    P->blk_cap = (uint32_t)cap;
-    hipStream_t st = ctx->stream;
-    std::vector<uint64_t> fo(frame_off, frame_off + n), d(dst_off, dst_off + n);
-    std::vector<uint32_t> fl(frame_len, frame_len + n), dc(dst_cap, dst_cap + n);
-    HIPCHK(upload(P->d_frame_off, fo, st));
-    HIPCHK(upload(P->d_frame_len, fl, st));
-    HIPCHK(upload(P->d_dst_off, d, st));
-    HIPCHK(upload(P->d_dst_cap, dc, st));
-    HIPCHK(P->d_nblk.ensure(n * 4 + 16));
-    HIPCHK(P->d_fstatus.ensure(n * 4 + 16));
-    HIPCHK(P->d_blk_base.ensure(n * 8 + 16));
-    HIPCHK(P->d_fwant.ensure(n * 4 + 16));
-    HIPCHK(P->d_got.ensure(n * 4 + 16));
-    HIPCHK(P->d_total.ensure(16));
-    HIPCHK(P->d_dblocks.ensure((size_t)P->blk_cap * sizeof(DecBlock) + 16));
-    HIPCHK(P->d_units.ensure((size_t)P->blk_cap * sizeof(DecUnit) + 16));
-    HIPCHK(P->d_blk_out.ensure((size_t)P->blk_cap * 4 + 16));
-    HIPCHK(P->d_blk_status.ensure((size_t)P->blk_cap * 4 + 16));
-    // large blocks: the device walk finds them; frames with room for more than 64 KiB may hold
-    // some (well-formed frames fill every block but the last, so <= cap / 256 KiB + 1 of them)
-    LbCaps lc;
-    if (n <= kLbFewBlocks / 4) {  // few frames: every compressed block takes the path
-        lc.min_limit = 1;
-        for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t nl = dst_cap[i] / 65536u + 1u;
-            lc.lb += nl;
-            lc.chunks += frame_len[i] / kLbChunk + nl;
+    return guarded([&]() -> int {
+        if (!ctx || !out || (n && (!frame_off || !frame_len || !dst_off || !dst_cap)))
+            return fail(S3HC_INVALID_ARG, "bad arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        HIPCHK(hipSetDevice(ctx->device));
+        std::unique_ptr<s3hc_plan> P(new s3hc_plan);
+        P->is_encode = false;
+        P->nframes = n;
+        uint64_t cap = 0;
+        for (uint32_t i = 0; i < n; ++i) cap += dst_cap[i] / 65536u + 2u;
+        if (cap > 0xFFFFFFF0ull) return fail(S3HC_INVALID_ARG, "batch too large");
+        P->blk_cap = (uint32_t)cap;
+        hipStream_t st = ctx->stream;
+        std::vector<uint64_t> fo(frame_off, frame_off + n), d(dst_off, dst_off + n);
+        std::vector<uint32_t> fl(frame_len, frame_len + n), dc(dst_cap, dst_cap + n);
+        HIPCHK(upload(P->d_frame_off, fo, st));
+        HIPCHK(upload(P->d_frame_len, fl, st));
+        HIPCHK(upload(P->d_dst_off, d, st));
+        HIPCHK(upload(P->d_dst_cap, dc, st));
+        HIPCHK(P->d_nblk.ensure(n * 4 + 16));
+        HIPCHK(P->d_fstatus.ensure(n * 4 + 16));
+        HIPCHK(P->d_blk_base.ensure(n * 8 + 16));
+        HIPCHK(P->d_fwant.ensure(n * 4 + 16));
+        HIPCHK(P->d_got.ensure(n * 4 + 16));
+        HIPCHK(P->d_total.ensure(16));
+        HIPCHK(P->d_dblocks.ensure((size_t)P->blk_cap * sizeof(DecBlock) + 16));
+        HIPCHK(P->d_units.ensure((size_t)P->blk_cap * sizeof(DecUnit) + 16));
+        HIPCHK(P->d_blk_out.ensure((size_t)P->blk_cap * 4 + 16));
+        HIPCHK(P->d_blk_status.ensure((size_t)P->blk_cap * 4 + 16));
+        // large blocks: the device walk finds them; frames with room for more than 64 KiB may hold
+        // some (well-formed frames fill every block but the last, so <= cap / 256 KiB + 1 of them)
+        LbCaps lc;
+        if (n <= kLbFewBlocks / 4) {  // few frames: every compressed block takes the path
+            lc.min_limit = 1;
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t nl = dst_cap[i] / 65536u + 1u;
+                lc.lb += nl;
+                lc.chunks += frame_len[i] / kLbChunk + nl;
+            }
+        } else {
+            for (uint32_t i = 0; i < n; ++i) {
+                if (dst_cap[i] <= 65536u) continue;
+                const uint32_t nl = dst_cap[i] / 262144u + 1u;
+                lc.lb += nl;
+                lc.chunks += frame_len[i] / kLbChunk + nl;
+            }
         }
-    } else {
-        for (uint32_t i = 0; i < n; ++i) {
-            if (dst_cap[i] <= 65536u) continue;
-            const uint32_t nl = dst_cap[i] / 262144u + 1u;
-            lc.lb += nl;
-            lc.chunks += frame_len[i] / kLbChunk + nl;
-        }
-    }
-    HIPCHK(P->lb.prepare(P->blk_cap, lc));
-    HIPCHK(hipStreamSynchronize(st));
-    *out = P.release();
-    return S3HC_OK;
+        HIPCHK(P->lb.prepare(P->blk_cap, lc));
+        HIPCHK(hipStreamSynchronize(st));
+        *out = P.release();
+        return S3HC_OK;
+    });
 }
 
 extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t* d_dst, uint32_t* d_out_len,
                                int32_t* d_status, void* stream) {
-    if (!ctx || !P || P->is_encode || !d_out_len || !d_status) return fail(S3HC_INVALID_ARG, "bad arguments");
-    std::lock_guard<std::mutex> g(ctx->mu);
-    HIPCHK(hipSetDevice(ctx->device));
-    hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
-    const uint32_t n = P->nframes;
-    if (!n) return S3HC_OK;
-    KTimer T(ctx, st);
-    T.begin("dec_plan");
-    HIPCHK(launch_dframe_count(d_src, P->d_frame_off.as<uint64_t>(), P->d_frame_len.as<uint32_t>(),
-                               P->d_dst_cap.as<uint32_t>(), n, P->d_nblk.as<uint32_t>(), d_status, st));
-    HIPCHK(launch_scan(P->d_nblk.as<uint32_t>(), n, P->d_blk_base.as<uint64_t>(), P->d_total.as<uint64_t>(), st));
-    HIPCHK(hipMemsetAsync(P->d_units.p, 0, (size_t)P->blk_cap * sizeof(DecUnit), st));
-    HIPCHK(launch_dframe_fill(d_src, P->d_frame_off.as<uint64_t>(), P->d_frame_len.as<uint32_t>(), n,
-                              P->d_dst_off.as<uint64_t>(), P->d_dst_cap.as<uint32_t>(), P->d_blk_base.as<uint64_t>(),
-                              d_status, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(),
-                              P->d_fwant.as<uint32_t>(), st));
-    T.end();
-    T.begin("decode");
-    HIPCHK(decode_launch(&P->lb, d_src, d_dst, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(), P->blk_cap,
-                         P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st));
-    T.end();
-    T.begin("dec_finish");
-    HIPCHK(launch_dframe_finish(P->d_blk_base.as<uint64_t>(), n, P->d_nblk.as<uint32_t>(), P->d_dblocks.as<DecBlock>(),
-                                P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), d_status, d_out_len, st));
-    T.end();
-    T.begin("xxh32");
-    HIPCHK(launch_xxh32(d_dst, P->d_dst_off.as<uint64_t>(), d_out_len, n, P->d_got.as<uint32_t>(), st));
-    T.end();
-    T.begin("dec_finish");
-    HIPCHK(launch_dframe_verify(d_src, P->d_frame_off.as<uint64_t>(), n, P->d_fwant.as<uint32_t>(),
-                                P->d_got.as<uint32_t>(), d_out_len, d_status, st));
-    T.end();
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx || !P || P->is_encode || !d_out_len || !d_status) return fail(S3HC_INVALID_ARG, "bad arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        HIPCHK(hipSetDevice(ctx->device));
+        hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+        const uint32_t n = P->nframes;
+        if (!n) return S3HC_OK;
+        KTimer T(ctx, st);
+        T.begin("dec_plan");
+        HIPCHK(launch_dframe_count(d_src, P->d_frame_off.as<uint64_t>(), P->d_frame_len.as<uint32_t>(),
+                                   P->d_dst_cap.as<uint32_t>(), n, P->d_nblk.as<uint32_t>(), d_status, st));
+        HIPCHK(launch_scan(P->d_nblk.as<uint32_t>(), n, P->d_blk_base.as<uint64_t>(), P->d_total.as<uint64_t>(), st));
+        HIPCHK(hipMemsetAsync(P->d_units.p, 0, (size_t)P->blk_cap * sizeof(DecUnit), st));
+        HIPCHK(launch_dframe_fill(d_src, P->d_frame_off.as<uint64_t>(), P->d_frame_len.as<uint32_t>(), n,
+                                  P->d_dst_off.as<uint64_t>(), P->d_dst_cap.as<uint32_t>(), P->d_blk_base.as<uint64_t>(),
+                                  d_status, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(),
+                                  P->d_fwant.as<uint32_t>(), st));
+        T.end();
+        T.begin("decode");
+        HIPCHK(decode_launch(&P->lb, d_src, d_dst, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(), P->blk_cap,
+                             P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st));
+        T.end();
+        T.begin("dec_finish");
+        HIPCHK(launch_dframe_finish(P->d_blk_base.as<uint64_t>(), n, P->d_nblk.as<uint32_t>(), P->d_dblocks.as<DecBlock>(),
+                                    P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), d_status, d_out_len, st));
+        T.end();
+        T.begin("xxh32");
+        HIPCHK(launch_xxh32(d_dst, P->d_dst_off.as<uint64_t>(), d_out_len, n, P->d_got.as<uint32_t>(), st));
+        T.end();
+        T.begin("dec_finish");
+        HIPCHK(launch_dframe_verify(d_src, P->d_frame_off.as<uint64_t>(), n, P->d_fwant.as<uint32_t>(),
+                                    P->d_got.as<uint32_t>(), d_out_len, d_status, st));
+        T.end();
+        return S3HC_OK;
+    });
 }
 
 // ------------------------------------------------- C ABI: host-buffer encode
@@ -650,11 +670,13 @@ static int run_compat(s3hc_ctx* ctx, const uint8_t* d_src, const uint64_t* src_o
 extern "C" int s3hc_compat_encode_dev(s3hc_ctx* ctx, const uint8_t* d_src, const uint64_t* src_off, const uint32_t* len,
                                       uint32_t n, uint8_t* d_dst, const uint64_t* dst_off, uint32_t* d_frame_len,
                                       void* stream) {
-    if (!ctx || (n && (!d_src || !src_off || !len || !d_dst || !dst_off || !d_frame_len)))
-        return fail(S3HC_INVALID_ARG, "bad arguments");
-    std::lock_guard<std::mutex> g(ctx->mu);
-    HIPCHK(hipSetDevice(ctx->device));
-    return run_compat(ctx, d_src, src_off, len, n, d_dst, dst_off, d_frame_len, stream ? (hipStream_t)stream : ctx->stream);
+    return guarded([&]() -> int {
+        if (!ctx || (n && (!d_src || !src_off || !len || !d_dst || !dst_off || !d_frame_len)))
+            return fail(S3HC_INVALID_ARG, "bad arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        HIPCHK(hipSetDevice(ctx->device));
+        return run_compat(ctx, d_src, src_off, len, n, d_dst, dst_off, d_frame_len, stream ? (hipStream_t)stream : ctx->stream);
+    });
 }
 
 static int host_compat(s3hc_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap, size_t* out_len) {
@@ -686,20 +708,24 @@ static int host_compat(s3hc_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
 
 extern "C" int s3hc_compress_frame(s3hc_ctx* ctx, const uint8_t* src, size_t n, int policy, uint8_t* dst, size_t cap,
                                    size_t* out_len, int* was_compressed) {
-    if (policy == S3HC_BLK_LZ4FLEX_COMPAT) {
-        int rc = host_compat(ctx, src, n, dst, cap, out_len);
+    return guarded([&]() -> int {
+        if (policy == S3HC_BLK_LZ4FLEX_COMPAT) {
+            int rc = host_compat(ctx, src, n, dst, cap, out_len);
+            if (was_compressed) *was_compressed = rc == S3HC_OK;
+            return rc;
+        }
+        if (policy != S3HC_BLK_AUTO_LZ4FLEX && policy != S3HC_BLK_64K_PER_FRAME) return fail(S3HC_INVALID_ARG, "policy");
+        int rc = host_encode(ctx, src, n, 0, policy, dst, cap, out_len);
         if (was_compressed) *was_compressed = rc == S3HC_OK;
         return rc;
-    }
-    if (policy != S3HC_BLK_AUTO_LZ4FLEX && policy != S3HC_BLK_64K_PER_FRAME) return fail(S3HC_INVALID_ARG, "policy");
-    int rc = host_encode(ctx, src, n, 0, policy, dst, cap, out_len);
-    if (was_compressed) *was_compressed = rc == S3HC_OK;
-    return rc;
+    });
 }
 
 extern "C" int s3hc_store_mode_frame(s3hc_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
                                      size_t* out_len) {
-    return host_encode(ctx, src, n, 1, S3HC_BLK_AUTO_LZ4FLEX, dst, cap, out_len);
+    return guarded([&]() -> int {
+        return host_encode(ctx, src, n, 1, S3HC_BLK_AUTO_LZ4FLEX, dst, cap, out_len);
+    });
 }
 
 // --------------------------------------------- host-buffer frame walker
@@ -792,13 +818,17 @@ static void walk_frames(const uint8_t* src, size_t n, HWalk& W, bool allow_incom
             D.dst_off = F.out_off + slot;
             D.csize = len;
             D.limit = (w & kStoredBit) ? len : F.bmax;
-            D.cap = D.limit;
+            // Output slot: no LZ4 sequence writes more than 255 bytes per compressed byte (a
+            // 255-run extension byte adds at most 255 to a length, every other byte costs at
+            // least one), so a block of `len` bytes decodes to < 255 * len. Tiny blocks in a
+            // BD 4 MiB frame therefore reserve a few hundred bytes, not 4 MiB each.
+            D.cap = (uint32_t)std::min<uint64_t>(D.limit, 255ull * len);
             D.flags = ((w & kStoredBit) ? DB_STORED : 0u) | (linked ? DB_LINKED : 0u);
             D.frame = (uint32_t)W.frames.size();
             fb.push_back(D);
             fhas.push_back((F.flg & 0x10) ? 1 : 0);
             fcs.push_back((F.flg & 0x10) ? rd32h(src + ip + len) : 0);
-            slot += D.limit;
+            slot += D.cap;
             ip += need;
         }
         if (!complete) {
@@ -824,27 +854,33 @@ static void walk_frames(const uint8_t* src, size_t n, HWalk& W, bool allow_incom
 }
 
 extern "C" int s3hc_decompressed_bound(const uint8_t* src, size_t n, size_t* bound) {
-    if ((!src && n) || !bound) return fail(S3HC_INVALID_ARG, "bad arguments");
-    HWalk W;
-    walk_frames(src, n, W, false, true);
-    uint64_t b = 0;
-    for (auto& D : W.blocks) b += D.limit;
-    *bound = b;
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if ((!src && n) || !bound) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HWalk W;
+        walk_frames(src, n, W, false, true);
+        uint64_t b = 0;
+        for (auto& D : W.blocks) b += D.cap;
+        *bound = b;
+        return S3HC_OK;
+    });
 }
 
 // Decode the frames of W (already walked) from a host buffer; append decoded bytes to
 // `out` (host) in frame order. Applies the decompress_data loop rules unless stream_mode.
 // Returns the first error in frame order (or W.tail_status).
 static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bool stream_mode,
-                       std::vector<uint8_t>* vout, uint8_t* dst, size_t cap, size_t* out_len) {
+                       std::vector<uint8_t>* vout, uint8_t* dst, size_t cap, size_t* out_len,
+                       bool upload_in = true, bool* stopped_out = nullptr) {
     hipStream_t st = ctx->stream;
     const size_t nb = W.blocks.size(), nf = W.frames.size();
     std::vector<uint32_t> bo(nb), cs_got(nb);
     std::vector<int32_t> bs(nb);
+    if (stopped_out) *stopped_out = false;
     if (nb) {
-        HIPCHK(ctx->d_in.ensure(n + 64));
-        HIPCHK(hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
+        if (upload_in) {
+            HIPCHK(ctx->d_in.ensure(n + 64));
+            HIPCHK(hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
+        }
         HIPCHK(ctx->d_out.ensure(W.slot_total + 64));
         std::vector<DecUnit> units;
         for (auto& F : W.frames) {
@@ -899,7 +935,7 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
             const uint32_t b = F.blk0 + k;
             if (W.blk_has_cs[b] && cs_got[b] != W.blk_cs_want[b]) { fs = S3HC_CHECKSUM; break; }
             if (bs[b] != S3HC_OK) { fs = bs[b]; break; }
-            if ((F.flg & 0x20) && k + 1 < F.nblk && bo[b] != W.blocks[b].limit) need_compact = true;
+            if ((F.flg & 0x20) && k + 1 < F.nblk && bo[b] != W.blocks[b].cap) need_compact = true;
             tot += bo[b];
         }
         if (fs == S3HC_OK && f + 1 == nf && W.last_incomplete) fs = W.tail_status;  // incomplete frame
@@ -907,6 +943,7 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         fout[f] = tot;
         if (!stream_mode && tot == 0) { use_frames = f + 1; stopped = true; break; }
     }
+    if (stopped_out) *stopped_out = stopped;
     if (err_status == S3HC_OK && !stopped && W.tail_status != S3HC_OK && !W.last_incomplete) {
         // a header-level failure after every walked frame (bad magic, truncated header, ...)
         err_status = W.tail_status;
@@ -946,6 +983,8 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         std::vector<size_t> which;
         for (size_t f = 0; f < use_frames; ++f) {
             if (W.frames[f].flg & 0x04) {
+                // the checksum kernel takes 32-bit range lengths
+                if (fout[f] > 0xFFFFFFFFull) return fail(S3HC_UNSUPPORTED, "a frame that decodes to 4 GiB or more");
                 ro.push_back(fpos[f]);
                 rl.push_back((uint32_t)fout[f]);
                 which.push_back(f);
@@ -992,16 +1031,121 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
     return S3HC_OK;
 }
 
+// Decode a walk in passes of whole frames whose output slots total <= kPassSlot (a frame larger
+// than that is a pass of its own), so device scratch follows the real output, not the whole
+// input's worst case; decoded bytes go to `vout` (grown by what each pass produced) or to
+// dst/cap. Frame order, the first-error rule and the empty-frame stop carry across passes.
+static constexpr uint64_t kPassSlot = 2ull << 30;
+static int decode_walk_passes(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bool stream_mode,
+                              std::vector<uint8_t>* vout, uint8_t* dst, size_t cap, size_t* out_len) {
+    if (W.slot_total <= kPassSlot) return decode_walk(ctx, src, n, W, stream_mode, vout, dst, cap, out_len);
+    const size_t nf = W.frames.size();
+    size_t a = 0;
+    uint64_t done = 0;
+    bool uploaded = false;
+    auto frame_slot = [&](size_t f) {
+        uint64_t s = 0;
+        for (uint32_t k = 0; k < W.frames[f].nblk; ++k) s += W.blocks[W.frames[f].blk0 + k].cap;
+        return s;
+    };
+    while (a < nf) {
+        size_t b = a;
+        uint64_t slot = 0;
+        while (b < nf) {
+            const uint64_t fs = frame_slot(b);
+            if (b > a && slot + fs > kPassSlot) break;
+            slot += fs;
+            ++b;
+        }
+        HWalk P;
+        const uint64_t base = W.frames[a].out_off;
+        const uint32_t blk_base = W.frames[a].blk0;
+        for (size_t f = a; f < b; ++f) {
+            HFrame F = W.frames[f];
+            F.out_off -= base;
+            F.blk0 -= blk_base;
+            P.frames.push_back(F);
+            for (uint32_t k = 0; k < F.nblk; ++k) {
+                DecBlock D = W.blocks[W.frames[f].blk0 + k];
+                D.dst_off -= base;
+                D.frame = (uint32_t)(f - a);
+                P.blocks.push_back(D);
+                P.blk_cs_want.push_back(W.blk_cs_want[W.frames[f].blk0 + k]);
+                P.blk_has_cs.push_back(W.blk_has_cs[W.frames[f].blk0 + k]);
+            }
+        }
+        P.slot_total = slot;
+        if (b == nf) {  // the walk's own tail belongs to its last pass
+            P.tail_status = W.tail_status;
+            P.last_incomplete = W.last_incomplete;
+            P.stopped_empty = W.stopped_empty;
+        }
+        size_t got = 0;
+        bool stopped = false;
+        const int rc = decode_walk(ctx, src, n, P, stream_mode, vout, dst ? dst + done : nullptr,
+                                   dst ? cap - (size_t)done : 0, &got, !uploaded, &stopped);
+        uploaded = true;
+        if (rc) {
+            if (out_len) *out_len = (size_t)done + got;
+            return rc;
+        }
+        done += got;
+        if (stopped) break;  // a frame yielding 0 bytes ended decompress_data's loop
+        a = b;
+    }
+    if (out_len) *out_len = (size_t)done;
+    return S3HC_OK;
+}
+
 extern "C" int s3hc_decompress_frames(s3hc_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst, size_t cap,
                                       size_t* out_len) {
     if (!ctx || (!src && n) || !out_len) return fail(S3HC_INVALID_ARG, "bad arguments");
-    std::lock_guard<std::mutex> g(ctx->mu);
-    HIPCHK(hipSetDevice(ctx->device));
-    *out_len = 0;
-    HWalk W;
-    walk_frames(src, n, W, false, true);
-    return decode_walk(ctx, src, n, W, false, nullptr, dst, cap, out_len);
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        HIPCHK(hipSetDevice(ctx->device));
+        *out_len = 0;
+        HWalk W;
+        walk_frames(src, n, W, false, true);
+        return decode_walk_passes(ctx, src, n, W, false, nullptr, dst, cap, out_len);
+    });
 }
+
+namespace s3hc {
+// decompress_data into a vector sized by the decoded bytes (compression.rs:463-502 read_to_end).
+int decompress_frames_vec(s3hc_ctx* ctx, const uint8_t* src, size_t n, std::vector<uint8_t>& out) {
+    if (!ctx || (!src && n)) return fail(S3HC_INVALID_ARG, "bad arguments");
+    return guarded([&] {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        HIPCHK(hipSetDevice(ctx->device));
+        out.clear();
+        HWalk W;
+        walk_frames(src, n, W, false, true);
+        size_t len = 0;
+        const int rc = decode_walk_passes(ctx, src, n, W, false, &out, nullptr, 0, &len);
+        if (rc) out.clear();
+        return rc;
+    });
+}
+}  // namespace s3hc
+
+extern "C" int s3hc_decompress_frames_alloc(s3hc_ctx* ctx, const uint8_t* src, size_t n, uint8_t** out,
+                                            size_t* out_len) {
+    if (!out || !out_len) return fail(S3HC_INVALID_ARG, "bad arguments");
+    *out = nullptr;
+    *out_len = 0;
+    std::vector<uint8_t> v;
+    const int rc = s3hc::decompress_frames_vec(ctx, src, n, v);
+    if (rc) return rc;
+    return guarded([&] {
+        uint8_t* p = (uint8_t*)malloc(v.size() ? v.size() : 1);
+        if (!p) return fail(S3HC_NO_MEMORY, "host allocation failed");
+        if (!v.empty()) memcpy(p, v.data(), v.size());
+        *out = p;
+        *out_len = v.size();
+        return S3HC_OK;
+    });
+}
+extern "C" void s3hc_buffer_free(uint8_t* p) { free(p); }
 
 // ------------------------------------------------------ streaming decoder
 struct s3hc_stream {
@@ -1015,20 +1159,26 @@ struct s3hc_stream {
 };
 
 extern "C" int s3hc_stream_open(s3hc_ctx* ctx, s3hc_stream** out) {
-    if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
-    *out = new s3hc_stream{ctx};
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
+        *out = new s3hc_stream{ctx};
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_stream_feed(s3hc_stream* s, const uint8_t* src, size_t n) {
-    if (!s || (!src && n)) return fail(S3HC_INVALID_ARG, "bad arguments");
-    if (s->finished) return fail(S3HC_INVALID_ARG, "stream already finished");
-    s->in.insert(s->in.end(), src, src + n);
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!s || (!src && n)) return fail(S3HC_INVALID_ARG, "bad arguments");
+        if (s->finished) return fail(S3HC_INVALID_ARG, "stream already finished");
+        s->in.insert(s->in.end(), src, src + n);
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_stream_finish(s3hc_stream* s) {
-    if (!s) return fail(S3HC_INVALID_ARG, "bad arguments");
-    s->finished = true;
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!s) return fail(S3HC_INVALID_ARG, "bad arguments");
+        s->finished = true;
+        return S3HC_OK;
+    });
 }
 // Decode every complete frame buffered so far (stream_range_data: one FrameDecoder per frame).
 static int stream_pump(s3hc_stream* s) {
@@ -1043,7 +1193,7 @@ static int stream_pump(s3hc_stream* s) {
     if (W.frames.empty() && W.tail_status == S3HC_OK) return S3HC_OK;
     if (s->out_pos == s->out.size()) { s->out.clear(); s->out_pos = 0; }
     size_t before = s->out.size();
-    int rc = decode_walk(s->ctx, s->in.data(), s->in.size(), W, true, &s->out, nullptr, 0, nullptr);
+    int rc = decode_walk_passes(s->ctx, s->in.data(), s->in.size(), W, true, &s->out, nullptr, 0, nullptr);
     if (rc) {
         s->out.resize(before);
         s->error = rc;
@@ -1058,17 +1208,19 @@ static int stream_pump(s3hc_stream* s) {
     return S3HC_OK;
 }
 extern "C" int s3hc_stream_read(s3hc_stream* s, uint8_t* dst, size_t cap, size_t* n) {
-    if (!s || !n || (!dst && cap)) return fail(S3HC_INVALID_ARG, "bad arguments");
-    *n = 0;
-    if (s->out_pos == s->out.size()) {
-        int rc = stream_pump(s);
-        if (rc) return rc;
-    }
-    size_t k = std::min(cap, s->out.size() - s->out_pos);
-    if (k) memcpy(dst, s->out.data() + s->out_pos, k);
-    s->out_pos += k;
-    *n = k;
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!s || !n || (!dst && cap)) return fail(S3HC_INVALID_ARG, "bad arguments");
+        *n = 0;
+        if (s->out_pos == s->out.size()) {
+            int rc = stream_pump(s);
+            if (rc) return rc;
+        }
+        size_t k = std::min(cap, s->out.size() - s->out_pos);
+        if (k) memcpy(dst, s->out.data() + s->out_pos, k);
+        s->out_pos += k;
+        *n = k;
+        return S3HC_OK;
+    });
 }
 extern "C" uint64_t s3hc_stream_total(const s3hc_stream* s) { return s ? s->total : 0; }
 extern "C" void s3hc_stream_close(s3hc_stream* s) { delete s; }
@@ -1077,74 +1229,96 @@ extern "C" void s3hc_stream_close(s3hc_stream* s) { delete s; }
 // Thin helpers so callers (tests, bench) can stage device-resident batches without a
 // second HIP runtime in the process.
 extern "C" int s3hc_dev_alloc(s3hc_ctx* ctx, size_t n, void** out) {
-    if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
-    HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipMalloc(out, n ? n : 16));
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        HIPCHK(hipMalloc(out, n ? n : 16));
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_dev_free(s3hc_ctx* ctx, void* p) {
-    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
-    HIPCHK(hipSetDevice(ctx->device));
-    if (p) HIPCHK(hipFree(p));
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        if (p) HIPCHK(hipFree(p));
+        return S3HC_OK;
+    });
 }
 // kind: 1 host->device, 2 device->host, 3 device->device. Synchronous w.r.t. the host.
 extern "C" int s3hc_memcpy(s3hc_ctx* ctx, void* dst, const void* src, size_t n, int kind) {
-    if (!ctx || kind < 1 || kind > 3) return fail(S3HC_INVALID_ARG, "bad arguments");
-    HIPCHK(hipSetDevice(ctx->device));
-    const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
-    if (n) HIPCHK(hipMemcpyAsync(dst, src, n, k, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx || kind < 1 || kind > 3) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+        if (n) HIPCHK(hipMemcpyAsync(dst, src, n, k, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_memset(s3hc_ctx* ctx, void* dst, int v, size_t n) {
-    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
-    HIPCHK(hipSetDevice(ctx->device));
-    if (n) HIPCHK(hipMemsetAsync(dst, v, n, ctx->stream));
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        if (n) HIPCHK(hipMemsetAsync(dst, v, n, ctx->stream));
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_sync(s3hc_ctx* ctx) {
-    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
-    HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_host_alloc(s3hc_ctx* ctx, size_t n, void** out) {
-    if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
-    HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipHostMalloc(out, n ? n : 16, hipHostMallocDefault));
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        HIPCHK(hipHostMalloc(out, n ? n : 16, hipHostMallocDefault));
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_host_free(s3hc_ctx* ctx, void* p) {
-    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
-    if (p) HIPCHK(hipHostFree(p));
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+        if (p) HIPCHK(hipHostFree(p));
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_queue_create(s3hc_ctx* ctx, void** out) {
-    if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
-    HIPCHK(hipSetDevice(ctx->device));
-    hipStream_t s;
-    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    *out = (void*)s;
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        hipStream_t s;
+        HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        *out = (void*)s;
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_queue_destroy(s3hc_ctx* ctx, void* q) {
-    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
-    if (q) HIPCHK(hipStreamDestroy((hipStream_t)q));
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+        if (q) HIPCHK(hipStreamDestroy((hipStream_t)q));
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_queue_sync(s3hc_ctx* ctx, void* q) {
-    if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
-    HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipStreamSynchronize(q ? (hipStream_t)q : ctx->stream));
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        HIPCHK(hipStreamSynchronize(q ? (hipStream_t)q : ctx->stream));
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_memcpy_async(s3hc_ctx* ctx, void* dst, const void* src, size_t n, int kind, void* q) {
-    if (!ctx || kind < 1 || kind > 3) return fail(S3HC_INVALID_ARG, "bad arguments");
-    HIPCHK(hipSetDevice(ctx->device));
-    const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
-    if (n) HIPCHK(hipMemcpyAsync(dst, src, n, k, q ? (hipStream_t)q : ctx->stream));
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx || kind < 1 || kind > 3) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+        if (n) HIPCHK(hipMemcpyAsync(dst, src, n, k, q ? (hipStream_t)q : ctx->stream));
+        return S3HC_OK;
+    });
 }
 
 // Host copy of a large staging buffer split over a few threads (one thread copies ~6-10 GB/s;
@@ -1518,105 +1692,113 @@ static int reader_complete(s3hc_reader* r) {
 }
 
 extern "C" int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3hc_reader** out) {
-    if (!ctx || !out || depth < 1 || depth > 16 || batch_bytes == 0) return fail(S3HC_INVALID_ARG, "bad arguments");
-    std::lock_guard<std::mutex> g(ctx->mu);
-    HIPCHK(hipSetDevice(ctx->device));
-    std::unique_ptr<s3hc_reader> r(new s3hc_reader);
-    r->ctx = ctx;
-    r->batch_bytes = batch_bytes;
-    r->slots.resize(depth);
-    for (auto& S : r->slots) {
-        HIPCHK(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&S.ev2, hipEventDisableTiming));
-    }
-    *out = r.release();
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx || !out || depth < 1 || depth > 16 || batch_bytes == 0) return fail(S3HC_INVALID_ARG, "bad arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        HIPCHK(hipSetDevice(ctx->device));
+        std::unique_ptr<s3hc_reader> r(new s3hc_reader);
+        r->ctx = ctx;
+        r->batch_bytes = batch_bytes;
+        r->slots.resize(depth);
+        for (auto& S : r->slots) {
+            HIPCHK(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+            HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&S.ev2, hipEventDisableTiming));
+        }
+        *out = r.release();
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_reader_feed(s3hc_reader* r, const uint8_t* src, size_t n) {
-    if (!r || (!src && n)) return fail(S3HC_INVALID_ARG, "bad arguments");
-    if (r->finished) return fail(S3HC_INVALID_ARG, "reader already finished");
-    if (r->error) return S3HC_OK;  // the stream has ended with an error; input is ignored
-    if (r->in_head && r->in_head >= r->in.size() / 2) {  // drop consumed input (amortized)
-        r->in.erase(r->in.begin(), r->in.begin() + r->in_head);
-        r->in_head = 0;
-    }
-    const size_t old = r->in.size();
-    r->in.resize(old + n);
-    par_memcpy(r->in.data() + old, src, n);
-    std::lock_guard<std::mutex> g(r->ctx->mu);
-    HIPCHK(hipSetDevice(r->ctx->device));
-    int rc = reader_advance(r);
-    if (rc) return rc;
-    return reader_pump(r);
+    return guarded([&]() -> int {
+        if (!r || (!src && n)) return fail(S3HC_INVALID_ARG, "bad arguments");
+        if (r->finished) return fail(S3HC_INVALID_ARG, "reader already finished");
+        if (r->error) return S3HC_OK;  // the stream has ended with an error; input is ignored
+        if (r->in_head && r->in_head >= r->in.size() / 2) {  // drop consumed input (amortized)
+            r->in.erase(r->in.begin(), r->in.begin() + r->in_head);
+            r->in_head = 0;
+        }
+        const size_t old = r->in.size();
+        r->in.resize(old + n);
+        par_memcpy(r->in.data() + old, src, n);
+        std::lock_guard<std::mutex> g(r->ctx->mu);
+        HIPCHK(hipSetDevice(r->ctx->device));
+        int rc = reader_advance(r);
+        if (rc) return rc;
+        return reader_pump(r);
+    });
 }
 extern "C" int s3hc_reader_finish(s3hc_reader* r) {
-    if (!r) return fail(S3HC_INVALID_ARG, "bad arguments");
-    r->finished = true;
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!r) return fail(S3HC_INVALID_ARG, "bad arguments");
+        r->finished = true;
+        return S3HC_OK;
+    });
 }
 extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t* n) {
-    if (!r || !n || (!dst && cap)) return fail(S3HC_INVALID_ARG, "bad arguments");
-    *n = 0;
-    if (!cap) return S3HC_OK;
-    // a ready head batch is delivered without the context lock (the copy is the caller's
-    // Bytes::copy_from_slice; concurrent readers must not serialize on it)
-    if (!r->inflight.empty() && r->slots[r->inflight.front()].ready) {
-        RSlot& S = r->slots[r->inflight.front()];
-        if (S.out_pos < S.out_len) {
-            const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
-            if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
-            S.out_pos += k;
-            *n = k;
-            if (S.out_pos < S.out_len) return S3HC_OK;
-        }
-    }
-    std::lock_guard<std::mutex> g(r->ctx->mu);
-    HIPCHK(hipSetDevice(r->ctx->device));
-    for (;;) {
+    return guarded([&]() -> int {
+        if (!r || !n || (!dst && cap)) return fail(S3HC_INVALID_ARG, "bad arguments");
+        *n = 0;
+        if (!cap) return S3HC_OK;
+        // a ready head batch is delivered without the context lock (the copy is the caller's
+        // Bytes::copy_from_slice; concurrent readers must not serialize on it)
         if (!r->inflight.empty() && r->slots[r->inflight.front()].ready) {
             RSlot& S = r->slots[r->inflight.front()];
-            if (*n == 0 && S.out_pos < S.out_len) {
+            if (S.out_pos < S.out_len) {
                 const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
                 if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
                 S.out_pos += k;
                 *n = k;
+                if (S.out_pos < S.out_len) return S3HC_OK;
             }
-            if (S.out_pos == S.out_len) {  // slot free again: queue the next batch
-                S.ready = false;
-                S.state = 0;
-                r->inflight.erase(r->inflight.begin());
-                if (!r->error) {
-                    int rc = reader_pump(r);
-                    if (rc) return rc;
+        }
+        std::lock_guard<std::mutex> g(r->ctx->mu);
+        HIPCHK(hipSetDevice(r->ctx->device));
+        for (;;) {
+            if (!r->inflight.empty() && r->slots[r->inflight.front()].ready) {
+                RSlot& S = r->slots[r->inflight.front()];
+                if (*n == 0 && S.out_pos < S.out_len) {
+                    const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
+                    if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
+                    S.out_pos += k;
+                    *n = k;
                 }
+                if (S.out_pos == S.out_len) {  // slot free again: queue the next batch
+                    S.ready = false;
+                    S.state = 0;
+                    r->inflight.erase(r->inflight.begin());
+                    if (!r->error) {
+                        int rc = reader_pump(r);
+                        if (rc) return rc;
+                    }
+                }
+                if (*n) return S3HC_OK;
+                continue;
             }
-            if (*n) return S3HC_OK;
-            continue;
-        }
-        if (!r->error) {
-            int rc = reader_advance(r);
-            if (rc) return rc;
-            rc = reader_pump(r);
-            if (rc) return rc;
-        }
-        if (r->inflight.empty()) {
-            if (r->error) return fail(r->error, r->error_msg);
-            if (r->finished && r->in_head < r->in.size()) {
-                r->error = S3HC_CORRUPT;
-                r->error_msg = "truncated frame at end of stream";
-                return fail(r->error, r->error_msg);
+            if (!r->error) {
+                int rc = reader_advance(r);
+                if (rc) return rc;
+                rc = reader_pump(r);
+                if (rc) return rc;
             }
-            return S3HC_OK;  // needs more input, or end of stream
+            if (r->inflight.empty()) {
+                if (r->error) return fail(r->error, r->error_msg);
+                if (r->finished && r->in_head < r->in.size()) {
+                    r->error = S3HC_CORRUPT;
+                    r->error_msg = "truncated frame at end of stream";
+                    return fail(r->error, r->error_msg);
+                }
+                return S3HC_OK;  // needs more input, or end of stream
+            }
+            // the oldest batch is still running: wait for it only when the pipeline is full, the
+            // input is finished or it is already done; otherwise ask the caller for more input
+            RSlot& H = r->slots[r->inflight.front()];
+            const bool done = H.state == 1 && hipEventQuery(H.ev2) == hipSuccess;
+            if (!done && r->inflight.size() < r->slots.size() && !r->finished && !r->error) return S3HC_OK;
+            int rc = reader_complete(r);
+            if (rc) return rc;
         }
-        // the oldest batch is still running: wait for it only when the pipeline is full, the
-        // input is finished or it is already done; otherwise ask the caller for more input
-        RSlot& H = r->slots[r->inflight.front()];
-        const bool done = H.state == 1 && hipEventQuery(H.ev2) == hipSuccess;
-        if (!done && r->inflight.size() < r->slots.size() && !r->finished && !r->error) return S3HC_OK;
-        int rc = reader_complete(r);
-        if (rc) return rc;
-    }
+    });
 }
 extern "C" uint64_t s3hc_reader_total(const s3hc_reader* r) { return r ? r->total : 0; }
 extern "C" void s3hc_reader_close(s3hc_reader* r) {

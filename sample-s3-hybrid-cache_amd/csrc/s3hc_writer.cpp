@@ -25,12 +25,14 @@
 // This file uses only the public C ABI (include/s3hc_lz4.h), like disk_cache.rs uses
 // compression.rs: it is caller-side code, not part of the codec.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
 
+#include "s3hc_guard.hpp"
 #include "s3hc_lz4.h"
 
 namespace {
@@ -115,8 +117,8 @@ struct s3hc_writer {
     uint64_t bytes_written = 0;             // every chunk (uncompressed)
     uint64_t compressed_bytes_written = 0;  // delivered frames
     uint32_t queued = 0;                    // batches queued and not yet delivered
-    int error = S3HC_OK;                    // sticky: first failure of a queued batch
-    std::string error_msg;
+    std::atomic<int> error{S3HC_OK};        // sticky: first failure of a queued batch (set under agg->mu)
+    std::string error_msg;                  // guarded by agg->mu
 };
 
 static thread_local std::string g_werr;
@@ -124,6 +126,22 @@ extern "C" const char* s3hc_writer_last_error(void) { return g_werr.c_str(); }
 static int werr(int code, const std::string& m) {
     g_werr = m;
     return code;
+}
+// The writer's sticky error as a status + message (a flush on another thread may set it).
+static int writer_error(s3hc_writer* w) {
+    if (!w->error.load(std::memory_order_acquire)) return S3HC_OK;
+    std::lock_guard<std::mutex> g(w->agg->mu);
+    return werr(w->error.load(std::memory_order_relaxed), w->error_msg);
+}
+template <class F>
+static int guarded(F&& f) {
+    return s3hc::guarded_call(werr, f);
+}
+static void set_writer_error(s3hc_writer* w, int rc, const std::string& msg) {  // caller holds agg->mu
+    if (!w->error.load(std::memory_order_relaxed)) {
+        w->error_msg = msg;
+        w->error.store(rc, std::memory_order_release);
+    }
 }
 
 // Encode every queued batch in one launch and deliver the frames in queue order.
@@ -151,7 +169,7 @@ static int aggregated_flush(s3hc_aggregator* a) {
         const std::string msg = std::string(what) + ": " + s3hc_last_error();
         std::lock_guard<std::mutex> g(a->mu);
         for (auto& b : work) {
-            if (!b.w->error) { b.w->error = rc; b.w->error_msg = msg; }
+            set_writer_error(b.w, rc, msg);
             b.w->queued--;
         }
         return werr(rc, msg);
@@ -215,11 +233,17 @@ static int aggregated_flush(s3hc_aggregator* a) {
         uint32_t* d_clen = (uint32_t*)((uint8_t*)S.d_cout + lens_at);
         if (!rc) rc = s3hc_compat_encode_dev(ctx, (const uint8_t*)S.d_in, offc.data(), lenc.data(), nc,
                                              (uint8_t*)S.d_cout, dof.data(), d_clen, a->queue);
-        if (!rc) rc = s3hc_memcpy_async(ctx, S.h_cout, S.d_cout, lens_at + 4ull * nc, 2, a->queue);
+        // frame lengths first
+        if (!rc) rc = s3hc_memcpy_async(ctx, (uint8_t*)S.h_cout + lens_at, d_clen, 4ull * nc, 2, a->queue);
         if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
         if (rc) return fail_all(rc, "compat encode");
         const uint32_t* cl = (const uint32_t*)((const uint8_t*)S.h_cout + lens_at);
         for (uint32_t j = 0; j < nc; ++j) { frame[ic[j]] = (const uint8_t*)S.h_cout + dof[j]; flen[ic[j]] = cl[j]; }
+        // then only each frame's own bytes (not its whole s3hc_frame_bound slot)
+        for (uint32_t j = 0; j < nc && !rc; ++j)
+            if (cl[j]) rc = s3hc_memcpy_async(ctx, (uint8_t*)S.h_cout + dof[j], (const uint8_t*)S.d_cout + dof[j], cl[j], 2, a->queue);
+        if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
+        if (rc) return fail_all(rc, "compat frame copy");
     }
     {
         std::lock_guard<std::mutex> g(a->mu);
@@ -231,7 +255,7 @@ static int aggregated_flush(s3hc_aggregator* a) {
         s3hc_writer* w = work[i].w;
         const uint8_t* fr = frame[i];
         int src = S3HC_OK;
-        if (!w->error) {
+        if (!w->error.load(std::memory_order_acquire)) {
             if (w->sink && w->sink(w->user, fr, flen[i]) != 0) {
                 src = S3HC_INVALID_ARG;
             } else {
@@ -240,7 +264,7 @@ static int aggregated_flush(s3hc_aggregator* a) {
             }
         }
         std::lock_guard<std::mutex> g(a->mu);
-        if (src && !w->error) { w->error = src; w->error_msg = "frame sink failed (write_all)"; }
+        if (src) set_writer_error(w, src, "frame sink failed (write_all)");
         w->queued--;
     }
     return S3HC_OK;
@@ -266,11 +290,11 @@ static void queue_batch(s3hc_writer* w) {
     s3hc_aggregator* a = w->agg;
     Batch b;
     b.w = w;
-    b.mode = w->compression_enabled ? a->compress_mode : 1;
     b.data.swap(w->batch_buf);
     w->batch_buf.clear();
     w->batch_buf.reserve(a->batch_size);
     std::lock_guard<std::mutex> g(a->mu);
+    b.mode = w->compression_enabled ? a->compress_mode : 1;
     a->pending_bytes += b.data.size();
     w->queued++;
     a->pending.push_back(std::move(b));
@@ -278,38 +302,44 @@ static void queue_batch(s3hc_writer* w) {
 
 extern "C" int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t flush_bytes, uint32_t flush_batches,
                                       s3hc_handler* stats, s3hc_aggregator** out) {
-    if (!ctx || !out) return werr(S3HC_INVALID_ARG, "bad arguments");
-    *out = nullptr;
-    // DiskCacheManager takes any batch size (its tests use 4-8 KiB); the 64 KiB..16 MiB bounds
-    // belong to Config::validate (config.rs:1617-1627), the caller's configuration layer.
-    if (batch_size == 0 || batch_size > 0xFFFFFFFFull / 2) return werr(S3HC_INVALID_ARG, "batch_size out of range");
-    s3hc_aggregator* a = new s3hc_aggregator;
-    a->ctx = ctx;
-    a->batch_size = batch_size;
-    a->flush_bytes = flush_bytes;
-    a->flush_batches = flush_batches;
-    a->stats = stats;
-    int rc = s3hc_queue_create(ctx, &a->queue);
-    if (rc) {
-        delete a;
-        return werr(rc, std::string("queue: ") + s3hc_last_error());
-    }
-    *out = a;
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!ctx || !out) return werr(S3HC_INVALID_ARG, "bad arguments");
+        *out = nullptr;
+        // DiskCacheManager takes any batch size (its tests use 4-8 KiB); the 64 KiB..16 MiB bounds
+        // belong to Config::validate (config.rs:1617-1627), the caller's configuration layer.
+        if (batch_size == 0 || batch_size > 0xFFFFFFFFull / 2) return werr(S3HC_INVALID_ARG, "batch_size out of range");
+        s3hc_aggregator* a = new s3hc_aggregator;
+        a->ctx = ctx;
+        a->batch_size = batch_size;
+        a->flush_bytes = flush_bytes;
+        a->flush_batches = flush_batches;
+        a->stats = stats;
+        int rc = s3hc_queue_create(ctx, &a->queue);
+        if (rc) {
+            delete a;
+            return werr(rc, std::string("queue: ") + s3hc_last_error());
+        }
+        *out = a;
+        return S3HC_OK;
+    });
 }
 
 extern "C" int s3hc_aggregator_set_frame_policy(s3hc_aggregator* a, int policy) {
-    if (!a || (policy != S3HC_BLK_AUTO_LZ4FLEX && policy != S3HC_BLK_64K_PER_FRAME &&
-               policy != S3HC_BLK_LZ4FLEX_COMPAT))
-        return werr(S3HC_INVALID_ARG, "bad arguments");
-    std::lock_guard<std::mutex> g(a->mu);
-    a->compress_mode = policy == S3HC_BLK_64K_PER_FRAME ? 2 : (policy == S3HC_BLK_LZ4FLEX_COMPAT ? kModeCompat : 0);
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!a || (policy != S3HC_BLK_AUTO_LZ4FLEX && policy != S3HC_BLK_64K_PER_FRAME &&
+                   policy != S3HC_BLK_LZ4FLEX_COMPAT))
+            return werr(S3HC_INVALID_ARG, "bad arguments");
+        std::lock_guard<std::mutex> g(a->mu);
+        a->compress_mode = policy == S3HC_BLK_64K_PER_FRAME ? 2 : (policy == S3HC_BLK_LZ4FLEX_COMPAT ? kModeCompat : 0);
+        return S3HC_OK;
+    });
 }
 
 extern "C" int s3hc_aggregator_flush(s3hc_aggregator* a) {
-    if (!a) return werr(S3HC_INVALID_ARG, "bad arguments");
-    return maybe_flush(a, true);
+    return guarded([&]() -> int {
+        if (!a) return werr(S3HC_INVALID_ARG, "bad arguments");
+        return maybe_flush(a, true);
+    });
 }
 
 extern "C" void s3hc_aggregator_counters(const s3hc_aggregator* a, uint64_t* launches, uint64_t* batches) {
@@ -341,33 +371,39 @@ extern "C" void s3hc_aggregator_destroy(s3hc_aggregator* a) {
 
 extern "C" int s3hc_writer_begin(s3hc_aggregator* a, uint64_t start, uint64_t end, int compression_enabled,
                                  s3hc_frame_sink sink, void* user, s3hc_writer** out) {
-    if (!a || !out) return werr(S3HC_INVALID_ARG, "bad arguments");
-    *out = nullptr;
-    if (start > end) return werr(S3HC_INVALID_ARG, "Invalid range: start > end");  // disk_cache.rs:1723-1728
-    s3hc_writer* w = new s3hc_writer;
-    w->agg = a;
-    w->sink = sink;
-    w->user = user;
-    w->start = start;
-    w->end = end;
-    w->compression_enabled = compression_enabled != 0;
-    w->batch_buf.reserve(a->batch_size);
-    *out = w;
-    return S3HC_OK;
+    return guarded([&]() -> int {
+        if (!a || !out) return werr(S3HC_INVALID_ARG, "bad arguments");
+        *out = nullptr;
+        if (start > end) return werr(S3HC_INVALID_ARG, "Invalid range: start > end");  // disk_cache.rs:1723-1728
+        s3hc_writer* w = new s3hc_writer;
+        w->agg = a;
+        w->sink = sink;
+        w->user = user;
+        w->start = start;
+        w->end = end;
+        w->compression_enabled = compression_enabled != 0;
+        w->batch_buf.reserve(a->batch_size);
+        *out = w;
+        return S3HC_OK;
+    });
 }
 
 extern "C" int s3hc_writer_write(s3hc_writer* w, const uint8_t* chunk, size_t n) {
-    if (!w || (!chunk && n)) return werr(S3HC_INVALID_ARG, "bad arguments");
-    if (w->error) return werr(w->error, w->error_msg);
-    if (n == 0) return S3HC_OK;                    // disk_cache.rs:1799-1801
-    w->bytes_written += n;
-    w->batch_buf.insert(w->batch_buf.end(), chunk, chunk + n);
-    if (w->batch_buf.size() >= w->agg->batch_size) {  // >= flushes (disk_cache.rs:1806)
-        queue_batch(w);
-        int rc = maybe_flush(w->agg, false);
-        if (rc && !w->error) return rc;
-    }
-    return w->error ? werr(w->error, w->error_msg) : S3HC_OK;
+    return guarded([&]() -> int {
+        if (!w || (!chunk && n)) return werr(S3HC_INVALID_ARG, "bad arguments");
+        if (int e = writer_error(w)) return e;
+        if (n == 0) return S3HC_OK;                    // disk_cache.rs:1799-1801
+        // one batch is one frame of one plan item (32-bit length): a batch of >= 4 GiB is refused
+        if (w->batch_buf.size() + n > 0xFFFFFFFFull) return werr(S3HC_UNSUPPORTED, "a batch of 4 GiB or more");
+        w->bytes_written += n;
+        w->batch_buf.insert(w->batch_buf.end(), chunk, chunk + n);
+        if (w->batch_buf.size() >= w->agg->batch_size) {  // >= flushes (disk_cache.rs:1806)
+            queue_batch(w);
+            int rc = maybe_flush(w->agg, false);
+            if (rc && !w->error.load(std::memory_order_acquire)) return rc;
+        }
+        return writer_error(w);
+    });
 }
 
 extern "C" size_t s3hc_writer_batch_buf_len(const s3hc_writer* w) { return w ? w->batch_buf.size() : 0; }
@@ -389,46 +425,51 @@ static int drain(s3hc_writer* w) {
 }
 
 extern "C" int s3hc_writer_commit(s3hc_writer* w, double min_commit_ratio, uint64_t spec_out[4]) {
-    if (!w) return werr(S3HC_INVALID_ARG, "bad arguments");
-    // finalize_incremental_range: residual batch first (disk_cache.rs:1981-1986)
-    queue_batch(w);
-    int rc = drain(w);
-    if (!rc && w->error) rc = werr(w->error, w->error_msg);
-    if (rc) {
-        delete w;  // the reference removes the .tmp file; the caller discards what its sink wrote
-        return rc;
-    }
-    uint64_t end = w->end;
-    const uint64_t expected = w->end - w->start + 1;
-    if (w->bytes_written != expected) {
-        // partial-prefix salvage (disk_cache.rs:1988-2023): read path passes a ratio; < 0 = exact only
-        const bool salvage = min_commit_ratio >= 0.0 && w->bytes_written > 0 && w->bytes_written < expected &&
-                             (double)w->bytes_written >= min_commit_ratio * (double)expected;
-        if (!salvage) {
-            char m[160];
-            snprintf(m, sizeof m, "Incremental write size mismatch: expected %llu bytes, got %llu",
-                     (unsigned long long)expected, (unsigned long long)w->bytes_written);
-            delete w;
-            return werr(S3HC_INVALID_ARG, m);
+    return guarded([&]() -> int {
+        if (!w) return werr(S3HC_INVALID_ARG, "bad arguments");
+        // finalize_incremental_range: residual batch first (disk_cache.rs:1981-1986)
+        queue_batch(w);
+        int rc = drain(w);
+        if (!rc) rc = writer_error(w);
+        if (rc) {
+            delete w;  // the reference removes the .tmp file; the caller discards what its sink wrote
+            return rc;
         }
-        end = w->start + w->bytes_written - 1;
-    }
-    if (w->agg->stats) s3hc_handler_record_object(w->agg->stats, w->compression_enabled ? 1 : 0);  // :2053
-    if (spec_out) {  // RangeSpec::new(start, end, path, Lz4, compressed, uncompressed) (disk_cache.rs:2080-2087)
-        spec_out[0] = w->start;
-        spec_out[1] = end;
-        spec_out[2] = w->compressed_bytes_written;
-        spec_out[3] = w->bytes_written;
-    }
-    delete w;
-    return S3HC_OK;
+        uint64_t end = w->end;
+        const uint64_t expected = w->end - w->start + 1;
+        if (w->bytes_written != expected) {
+            // partial-prefix salvage (disk_cache.rs:1988-2023): read path passes a ratio; < 0 = exact only
+            const bool salvage = min_commit_ratio >= 0.0 && w->bytes_written > 0 && w->bytes_written < expected &&
+                                 (double)w->bytes_written >= min_commit_ratio * (double)expected;
+            if (!salvage) {
+                char m[160];
+                snprintf(m, sizeof m, "Incremental write size mismatch: expected %llu bytes, got %llu",
+                         (unsigned long long)expected, (unsigned long long)w->bytes_written);
+                delete w;
+                return werr(S3HC_INVALID_ARG, m);
+            }
+            end = w->start + w->bytes_written - 1;
+        }
+        if (w->agg->stats) s3hc_handler_record_object(w->agg->stats, w->compression_enabled ? 1 : 0);  // :2053
+        if (spec_out) {  // RangeSpec::new(start, end, path, Lz4, compressed, uncompressed) (disk_cache.rs:2080-2087)
+            spec_out[0] = w->start;
+            spec_out[1] = end;
+            spec_out[2] = w->compressed_bytes_written;
+            spec_out[3] = w->bytes_written;
+        }
+        delete w;
+        return S3HC_OK;
+    });
 }
 
 extern "C" void s3hc_writer_abort(s3hc_writer* w) {
     if (!w) return;
     // queued batches still reference w: let them drain (their frames go to the sink, which the
     // caller is discarding together with the .tmp file) before freeing
-    w->error = w->error ? w->error : S3HC_INVALID_ARG;
+    {
+        std::lock_guard<std::mutex> g(w->agg->mu);
+        set_writer_error(w, S3HC_INVALID_ARG, "aborted");
+    }
     (void)drain(w);
     delete w;
 }

@@ -63,6 +63,8 @@ def _load():
         "s3hc_store_mode_frame": (i32, [vp, u8p, sz, u8p, sz, szp]),
         "s3hc_decompressed_bound": (i32, [u8p, sz, szp]),
         "s3hc_decompress_frames": (i32, [vp, u8p, sz, u8p, sz, szp]),
+        "s3hc_decompress_frames_alloc": (i32, [vp, u8p, sz, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), szp]),
+        "s3hc_buffer_free": (None, [ctypes.POINTER(ctypes.c_uint8)]),
         "s3hc_stream_open": (i32, [vp, ctypes.POINTER(vp)]),
         "s3hc_stream_feed": (i32, [vp, u8p, sz]),
         "s3hc_stream_finish": (i32, [vp]),
@@ -221,10 +223,13 @@ class Engine:
 
     def decompress_frames(self, data, cap: int | None = None) -> bytes:
         p, keep = _ptr(data)
-        if cap is None:
-            b = ctypes.c_size_t()
-            _check(lib.s3hc_decompressed_bound(p, len(keep), ctypes.byref(b)))
-            cap = b.value
+        if cap is None:  # library-owned output of exactly the decoded size
+            buf, n = ctypes.POINTER(ctypes.c_uint8)(), ctypes.c_size_t()
+            _check(lib.s3hc_decompress_frames_alloc(self.h, p, len(keep), ctypes.byref(buf), ctypes.byref(n)))
+            try:
+                return ctypes.string_at(buf, n.value)
+            finally:
+                lib.s3hc_buffer_free(buf)
         out = ctypes.create_string_buffer(max(cap, 1))
         n = ctypes.c_size_t()
         _check(lib.s3hc_decompress_frames(self.h, p, len(keep), out, cap, ctypes.byref(n)))
@@ -612,7 +617,7 @@ class CompressionHandler:
     def decompress_with_algorithm(self, data, algorithm: int = ALG_LZ4) -> bytes:
         p, keep = _ptr(data)
         b = ctypes.c_size_t()
-        lib.s3hc_decompressed_bound(p, len(keep), ctypes.byref(b))
+        lib.s3hc_decompressed_bound(p, len(keep), ctypes.byref(b))  # <= 255 x len(data)
         cap = max(b.value, len(keep), 1)
         out = ctypes.create_string_buffer(cap)
         n = ctypes.c_size_t()

@@ -453,3 +453,27 @@ def test_store_mode_corruption_detected(engine, oracle):
     with pytest.raises(S.CodecError) as ei:
         _handler(engine).decompress_data(bytes(g))
     assert ei.value.status == S.S3HC_CHECKSUM
+
+
+def test_tiny_blocks_in_4mib_frame_decode_to_nothing(engine, oracle):
+    """13,000 one-byte blocks in a BD 4 MiB frame decode to b"" (an empty frame ends
+    decompress_data's loop, so the frame after it is ignored) without reserving 4 MiB per block."""
+    import struct
+    f = bytes.fromhex("04224d186470b9") + (struct.pack("<I", 1) + b"\x00") * 13_000 + bytes(4) + \
+        struct.pack("<I", 0x02CC5D05)
+    tail = oracle.lz4flex_compress_frame(b"after the empty frame")
+    for blob in (f, f + tail):
+        assert oracle.decompress_status(blob) == (0, b"")
+        assert engine.decompress_frames(blob) == b""
+    h = S.CompressionHandler(engine, 1024, True)
+    assert h.decompress_data(f + tail) == b""
+    s = engine.stream()  # stream_range_data does not stop at an empty frame
+    s.feed(f + tail)
+    s.finish()
+    got = b""
+    while True:
+        c = s.read(1 << 20)
+        if not c:
+            break
+        got += c
+    assert got == b"after the empty frame"

@@ -65,7 +65,27 @@ def test_decompressed_bound_host_walk(oracle):
         b = ctypes.c_size_t()
         assert S.lib.s3hc_decompressed_bound(f, len(f), ctypes.byref(b)) == 0
         assert b.value >= 2 * len(data)
-        assert b.value == oracle.decompressed_bound(f)
+        assert b.value <= oracle.decompressed_bound(f)  # slots: min(block max, 255 x compressed size)
+
+
+def _tiny_block_frame(nblocks):
+    """BD 0x70 (4 MiB blocks) frame of nblocks 1-byte compressed blocks that decode to nothing
+    (token 0x00: an empty last sequence), EndMark, xxh32("")."""
+    import struct
+    return bytes.fromhex("04224d186470b9") + (struct.pack("<I", 1) + b"\x00") * nblocks + bytes(4) + \
+        struct.pack("<I", 0x02CC5D05)
+
+
+def test_decompressed_bound_tiny_blocks_not_block_max(oracle):
+    """a 4 MiB-BD frame of tiny blocks must not reserve 4 MiB per block."""
+    import s3hc_lz4 as S
+
+    f = _tiny_block_frame(13_000)
+    assert oracle.decompress_data(f) == b""
+    b = ctypes.c_size_t()
+    assert S.lib.s3hc_decompressed_bound(f, len(f), ctypes.byref(b)) == 0
+    assert b.value <= 255 * len(f)
+    assert oracle.decompressed_bound(f) >= 13_000 * (4 << 20)  # what per-block-max sizing would reserve
 
 
 def test_frame_bound():
