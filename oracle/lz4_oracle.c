@@ -137,7 +137,15 @@ int or_store_mode_frame(const uint8_t* src, size_t n, uint8_t* dst, size_t cap, 
 /* Restated from lz4_flex 0.11 block/compress.rs compress_internal as used by
  * frame/compress.rs FrameEncoder::write_block (HashTable4K: 4096 x u32 entries,
  * 5-byte hash on 64-bit targets; table persists across the frame's blocks and
- * stale entries below the stream offset are skipped). */
+ * stale entries below the stream offset are skipped).
+ *
+ * Hash choice (SURVEY.md A.3 erratum): the size-dependent table selection
+ * (input < u16::MAX -> HashTable4KU16 with the 4-byte hash) belongs to the BLOCK API
+ * (compress_into / compress_into_sink_with_dict). The frame encoder owns one HashTable4K
+ * field for its whole life and calls compress_internal directly: its entries are
+ * pos + input_stream_offset, which a u16 table cannot hold past the first 64 KiB of a
+ * stream, so the frame path uses the u32 table for every input size, and that table's
+ * get_hash_at is hash5 on 64-bit targets. Recalled (the crate is absent): unpinned. */
 typedef struct { uint32_t t[4096]; } ht4k_t;
 
 static inline uint32_t hash5_idx(const uint8_t* in, size_t pos) {

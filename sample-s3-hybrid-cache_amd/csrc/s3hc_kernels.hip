@@ -501,6 +501,30 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
                 }
             }
         }
+        // Sources older than the ring (offsets above kRing - S; a third of log-text matches) are
+        // read back from HBM, where this wave flushed them windows ago. All four loads are issued
+        // at once, before the LDS reads, and merged into the ring dword before its store: one
+        // round trip per pass instead of four serialized load + vmcnt(0) waits.
+        uint32_t fv = 0, fmask = 0;
+        bool anyold = false;
+        if (far) {
+            bool old[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                old[j] = ok[j] & !lit[j] & (y[j] < upos - (kRing - S));
+                anyold |= old[j];
+            }
+            if (__ballot(anyold)) {
+                uint32_t fb[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) fb[j] = w.out[old[j] ? y[j] : 0u];  // unit byte 0: always valid
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    fv |= old[j] ? fb[j] << (8 * j) : 0u;
+                    fmask |= old[j] ? 0xFFu << (8 * j) : 0u;
+                }
+            }
+        }
         const uint32_t oldw = ((const uint32_t*)w.ring)[(X & kMask) >> 2];
         uint32_t v[4];
 #pragma unroll
@@ -518,23 +542,11 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
             anypnd |= pnd[j];
             vm |= ok[j] ? 0xFFu << (8 * j) : 0u;
         }
-        const uint32_t val = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
+        const uint32_t val = ((v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24)) & ~fmask) | fv;
         ((uint32_t*)w.ring)[(X & kMask) >> 2] = (val & vm) | (oldw & ~vm);
-        if (far) {
-            // sources older than the ring are read back from HBM (already flushed); kept apart
-            // so the common path never waits on the wave's outstanding flush stores
-            bool old[4], anyold = false;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                old[j] = ok[j] & !lit[j] & (y[j] < upos - (kRing - S));
-                anyold |= old[j];
-            }
-            if (__ballot(anyold)) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (old[j]) w.ring[(X + j) & kMask] = w.out[y[j]];
-            }
-        }
+#ifdef S3HC_PROF
+        const uint64_t tq0 = PROF_NOW();
+#endif
         if (__ballot(anypnd)) {
             // sources inside this pass: follow refs through pending bytes (bytes of earlier
             // passes and bytes with refs == 0xFFFF are final in the ring); refs are pass-local
@@ -567,6 +579,11 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
             for (int j = 0; j < 4; ++j) *(pnd[j] ? w.ring + ((X + j) & kMask) : w.sink + lane) = vv[j];
         }
         wave_sync();
+#ifdef S3HC_PROF
+        __builtin_amdgcn_s_waitcnt(0);
+        PROF_ADD(w.pr, 14, PROF_NOW() - tq0);
+        PROF_ADD(w.pr, 15, __ballot(anyold) ? 1 : 0);
+#endif
     }
     w.upos = upos + S;
     const uint64_t tf = PROF_NOW();
@@ -686,6 +703,9 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
         // chain from q (one readlane per hop) and marks members in four 64-bit masks; members are
         // then compacted into member order (mbcnt ranks through a small LDS slot table).
         const uint32_t nx0 = dec_step(w.cin, q + lane, q, mis, C, fill);
+#ifdef S3HC_PROF
+        uint64_t tsA = PROF_NOW();
+#endif
         const uint32_t nx1 = dec_step(w.cin, q + 64 + lane, q, mis, C, fill);
         const uint32_t nx2 = dec_step(w.cin, q + 128 + lane, q, mis, C, fill);
         const uint32_t nx3 = dec_step(w.cin, q + 192 + lane, q, mis, C, fill);
@@ -695,6 +715,11 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
 #endif
         uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
         uint32_t l = 0, lastl = 0;
+#ifdef S3HC_PROF
+        // steps are consumed by the walk: force them complete before the walk timer starts
+        __builtin_amdgcn_s_waitcnt(0);
+        { const uint64_t tn = PROF_NOW(); PROF_ADD(w.pr, 12, tn - tsA); tsA = tn; }
+#endif
         WALK_PRIO_ON();
         while (l < 64u) { lastl = l; m0 |= 1ull << l; l = rdl(nx0, l); }
         while (l < 128u) { lastl = l; m1 |= 1ull << (l - 64u); l = rdl(nx1, l - 64u); }
@@ -704,6 +729,9 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
         while (l < 320u) { lastl = l; m4 |= 1ull << (l - 256u); l = rdl(nx4, l - 256u); }
 #endif
         WALK_PRIO_OFF();
+#ifdef S3HC_PROF
+        PROF_ADD(w.pr, 13, PROF_NOW() - tsA);
+#endif
         // members are >= 3 bytes apart except the last, so at most kPos / 3 + 1 of them (< kMaxMem)
         const uint32_t c1 = (uint32_t)__builtin_popcountll(m0), c2 = c1 + (uint32_t)__builtin_popcountll(m1);
         const uint32_t c3 = c2 + (uint32_t)__builtin_popcountll(m2);

@@ -13,13 +13,13 @@ import s3hc_lz4 as S  # noqa: E402
 import synth  # noqa: E402
 
 DEC = ["stage", "parse_walk", "window", "seq", "wave_total", "windows", "members", "passes",
-       "pend_windows", "stages", "flush", "bytes"]
+       "pend_windows", "stages", "flush", "bytes", "steps", "walk", "pending", "far_passes"]
 ENC = {16: "stage", 17: "cand", 18: "long_ext", 19: "walk", 20: "flush", 21: "wave_total", 22: "subblocks",
        23: "hops", 24: "long_matches"}
 
 
 def main():
-    nb, block, steps = 4096, 65536, 3
+    nb, block, steps = int(os.environ.get("PROF_BLOCKS", "4096")), 65536, 3
     eng = S.Engine(0)
     L = ctypes.CDLL(S.LIB_PATH)
     f = L.s3hc_diag_prof
