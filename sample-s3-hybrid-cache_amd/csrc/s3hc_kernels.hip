@@ -94,6 +94,7 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
     return x;
 }
 __device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
     x = umax32(x, dpp0<0x111, 0xF>(x));
     x = umax32(x, dpp0<0x112, 0xF>(x));
@@ -284,7 +285,8 @@ struct DecWave {
     uint8_t* marks;      // kMarks bytes: sequence start marks of the current window (zero between windows)
     uint16_t* refs;      // kRefs entries: in-pass match source of each output byte of the current pass
     uint8_t* sink;       // kSink bytes: target of stores from lanes with nothing to store
-    uint2* mtab;         // 128 entries: the window's member sequences (start, ll, off, literal)
+    uint2* mtab;         // the window's member sequences (start, ll, off, literal)
+    uint32_t mmax;       // last valid mtab index
     uint8_t* out;        // unit output base in HBM
 #ifdef S3HC_PROF
     uint64_t pr[16];
@@ -369,6 +371,16 @@ __device__ __forceinline__ uint32_t cin32(const uint8_t* cin, uint32_t i) {
     return __builtin_amdgcn_alignbyte(r[(a + 1) & (dec::kCring / 4 - 1)], r[a & (dec::kCring / 4 - 1)], i & 3u);
 }
 
+// The same read for rings followed by a mirror of their first dword (k_decode_pe): one mask,
+// one ds_read2_b32, one alignbyte.
+template <bool kMir>
+__device__ __forceinline__ uint32_t cin32m(const uint8_t* cin, uint32_t i) {
+    if (!kMir) return cin32(cin, i);
+    const uint32_t a = i & dec::kCmask;
+    const uint32_t* r = (const uint32_t*)(cin + (a & ~3u));
+    return __builtin_amdgcn_alignbyte(r[1], r[0], a & 3u);
+}
+
 // Wave-cooperative LZ4 length-extension scan at pos (bytes of 255 continue the run).
 __device__ __forceinline__ int dec_ext_scan(const uint8_t* in, uint32_t C, uint32_t& pos, uint32_t& acc, int lane) {
     for (;;) {
@@ -415,25 +427,22 @@ __device__ __forceinline__ int dec_seq(DecWave& w, const uint8_t* in, uint32_t l
 // are read at once, the dword is merged and stored, and bytes whose source lies in this pass
 // follow the chain of in-pass sources (refs) to a byte already final. A fixed handful of LDS
 // round trips per 256 bytes, almost no scalar work.
+__device__ __forceinline__ void dec_window_passes(DecWave& w, uint32_t S, bool far);
 __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM0, bool isM1, uint32_t orel0,
                                                 uint32_t orel1, uint32_t sl0, uint32_t sl1, uint32_t ll0,
                                                 uint32_t ll1, uint32_t off0, uint32_t off1, uint32_t lr0,
                                                 uint32_t lr1) {
     using namespace dec;
     const int lane = w.lane;
-    uint8_t* marks = w.marks;
-    uint16_t* refs = w.refs;
     const uint32_t upos = w.upos;
-    const uint32_t a0 = upos & 3u;        // byte u of a pass = window byte u - a0 (ring dwords aligned)
-    const uint32_t xbase = upos - a0;
-    const uint32_t np = (S + a0 + 255u) >> 8;
+    const uint32_t a0 = upos & 3u;
     // member m starts at window byte orel: marks[orel + a0] = m + 1 (marks are zero between
     // windows: each pass clears the dwords it reads). The member table holds
     // (M | E << 16, L | off << 16): M = window byte where the member's match starts (orel + ll),
     // E = M + off (saturated; bytes at or past E copy an overlapping match), L = literal ring
     // index minus orel (window byte t of a literal run is cin[(L + t) & kCmask]).
-    *((isM0 && sl0) ? marks + orel0 + a0 : w.sink + lane) = (uint8_t)(lane + 1);
-    *((isM1 && sl1) ? marks + orel1 + a0 : w.sink + lane) = (uint8_t)(lane + 65);
+    *((isM0 && sl0) ? w.marks + orel0 + a0 : w.sink + lane) = (uint8_t)(lane + 1);
+    *((isM1 && sl1) ? w.marks + orel1 + a0 : w.sink + lane) = (uint8_t)(lane + 65);
     auto entry = [](uint32_t orel, uint32_t ll, uint32_t off, uint32_t lr) -> uint2 {
         const uint32_t M = orel + ll;
         const uint32_t E = M + off < 0xFFFFu ? M + off : 0xFFFFu;
@@ -444,6 +453,20 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
     // a source older than the ring (read back from HBM) needs a match offset above kRing - S
     const bool far = (upos > kRing - S) &&
                      __ballot((isM0 && sl0 > ll0 && off0 > kRing - S) || (isM1 && sl1 > ll1 && off1 > kRing - S));
+    dec_window_passes(w, S, far);
+}
+
+// The byte-parallel passes of one window whose marks and member table (w.mtab, w.mmax
+// entries) are in LDS.
+__device__ __forceinline__ void dec_window_passes(DecWave& w, uint32_t S, bool far) {
+    using namespace dec;
+    const int lane = w.lane;
+    uint8_t* marks = w.marks;
+    uint16_t* refs = w.refs;
+    const uint32_t upos = w.upos;
+    const uint32_t a0 = upos & 3u;        // byte u of a pass = window byte u - a0 (ring dwords aligned)
+    const uint32_t xbase = upos - a0;
+    const uint32_t np = (S + a0 + 255u) >> 8;
     wave_sync();
     uint32_t carry = 0;
     for (uint32_t p = 0; p < np; ++p) {
@@ -464,7 +487,7 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
         o[1] = umax32(ex, c1);
         o[2] = umax32(ex, c2);
         o[3] = umax32(ex, c3);
-        const uint2 fA = w.mtab[(o[0] - 1u) & 127u], fB = w.mtab[(o[3] - 1u) & 127u];
+        const uint2 fA = w.mtab[umin32(o[0] - 1u, w.mmax)], fB = w.mtab[umin32(o[3] - 1u, w.mmax)];
         // ---- sources
         uint32_t y[4], ci[4], mst[4], mf[4];
         bool lit[4], ok[4], wrap[4];
@@ -598,11 +621,12 @@ __device__ __forceinline__ void dec_window_exec(DecWave& w, uint32_t S, bool isM
 struct DecTok {
     uint32_t flags, nxt, lit, ll, off, ml;
 };
+template <bool kMir = false>
 __device__ __forceinline__ DecTok dec_spec(const uint8_t* cin, uint32_t qq, uint32_t mis, uint32_t C, uint32_t fill) {
     using namespace dec;
     DecTok T;
     const uint32_t i = qq + mis;
-    const uint32_t w0 = cin32(cin, i);
+    const uint32_t w0 = cin32m<kMir>(cin, i);
     const uint32_t t = w0 & 0xFFu, L = t >> 4, M = t & 15u;
     const uint32_t e1 = (w0 >> 8) & 0xFFu, e2 = (w0 >> 16) & 0xFFu;
     const uint32_t x1 = L == 15u ? 1u : 0u, x2 = (L == 15u && e1 == 255u) ? 1u : 0u;
@@ -610,7 +634,7 @@ __device__ __forceinline__ DecTok dec_spec(const uint8_t* cin, uint32_t qq, uint
     T.lit = qq + 1u + x1 + x2;
     const uint32_t mp = T.lit + T.ll;
     const uint32_t mi = mp + mis;
-    const uint32_t w1 = cin32(cin, mi);
+    const uint32_t w1 = cin32m<kMir>(cin, mi);
     T.off = w1 & 0xFFFFu;
     const uint32_t f1 = (w1 >> 16) & 0xFFu, f2 = w1 >> 24;
     const uint32_t y1 = M == 15u ? 1u : 0u, y2 = (M == 15u && f1 == 255u) ? 1u : 0u;
@@ -633,15 +657,16 @@ __device__ __forceinline__ DecTok dec_spec(const uint8_t* cin, uint32_t qq, uint
 // ordinary sequence; kPos when the chain leaves the window here (next token at or past q + kPos,
 // last sequence, malformed, long length run, or bytes past the staged input — dec_spec then
 // tells which). Consistent with dec_spec: a step < kPos implies dec_spec flags are clear.
+template <bool kMir = false>
 __device__ __forceinline__ uint32_t dec_step(const uint8_t* cin, uint32_t qq, uint32_t q, uint32_t mis, uint32_t C,
                                              uint32_t fill) {
     using namespace dec;
-    const uint32_t w0 = cin32(cin, qq + mis);
+    const uint32_t w0 = cin32m<kMir>(cin, qq + mis);
     const uint32_t t = w0 & 0xFFu, L = t >> 4, M = t & 15u;
     const uint32_t e1 = (w0 >> 8) & 0xFFu, e2 = (w0 >> 16) & 0xFFu;
     const bool x1 = L == 15u, x2 = x1 && e1 == 255u;
     const uint32_t mp = qq + 1u + L + (x1 ? 1u + e1 : 0u) + (x2 ? 1u + e2 : 0u);
-    const uint32_t w1 = cin32(cin, mp + mis);
+    const uint32_t w1 = cin32m<kMir>(cin, mp + mis);
     const uint32_t f1 = (w1 >> 16) & 0xFFu, f2 = w1 >> 24;
     const bool y1 = M == 15u, y2 = y1 && f1 == 255u;
     const uint32_t nxt = mp + 2u + (y1 ? 1u : 0u) + (y2 ? 1u : 0u);
@@ -897,6 +922,7 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     w.refs = (uint16_t*)(w.marks + dec::kMarks);
     w.sink = (uint8_t*)(w.refs + dec::kRefs);
     w.mtab = (uint2*)(w.sink + dec::kSink);
+    w.mmax = dec::kMaxMem - 1;
     for (uint32_t i = (uint32_t)lane; i < dec::kMarks / 16; i += 64) ((uint4*)w.marks)[i] = make_uint4(0, 0, 0, 0);
     w.out = dst + blk[U.first].dst_off;
     w.upos = 0;
@@ -937,6 +963,607 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     if (lane == 0)
         for (int k = 0; k < 16; ++k) atomicAdd(&g_prof[k], (unsigned long long)w.pr[k]);
 #endif
+}
+
+// ====================================================== decode, parser + executor waves
+// k_decode_pe: the same decoder with the two halves of a window on two waves of one 128-thread
+// workgroup per unit. Wave P walks the token chain (staging, next-token steps, the serial
+// readlane walk, member decode, lz4_flex bound checks) and writes one command per step into a
+// two-slot LDS queue; wave E executes the command P wrote one step earlier (marks, the
+// byte-parallel passes, long sequences, stored blocks, flushes). Both waves meet at one
+// workgroup barrier per step, so a step costs max(parse, execute) instead of their sum, and a
+// 4096-block batch runs 8 waves per SIMD instead of 4 (10 KiB of LDS and <= 64 VGPRs a unit).
+// Statuses and output sizes are written by P (lane 0), the output bytes by E.
+namespace dpe {
+constexpr uint32_t kMaxMem = 88;                          // members of one window: at most kPos / 3 + 1 = 86
+constexpr uint32_t kMaxSeg = 2 * kMaxMem;                 // a literal run and a match per member
+constexpr uint32_t kBitsW = 8 * ((dec::kWin + 3 + 255) / 256);  // one bit per pass byte (5 passes)
+enum : uint32_t { C_NOP = 0, C_WIN = 1, C_STORED = 2, C_END = 3 };
+enum : uint32_t { K_LIT = 0, K_MATCH = 1, K_OVL = 2 };   // segment kinds
+struct Slot {
+    uint32_t cmd;
+    uint32_t S;       // WIN: output bytes of the members
+    uint32_t nseg;    // WIN: segments
+    uint32_t far;     // WIN: a match reads a source older than the output ring
+    uint64_t ptr;     // WIN tail / STORED: compressed block base in HBM
+    uint32_t tail;    // WIN: 0 none, 1 one sequence follows the members, 2 it is the block's last
+    uint32_t tlit;    // tail literal start (block offset) / STORED: size
+    uint32_t tll, toff, tml;
+    uint32_t single;  // STORED: the unit's only block (copied straight to HBM)
+    uint32_t ovl;     // WIN: some match overlaps itself (offset < length)
+    uint32_t pad;
+    uint32_t bits[kBitsW];  // bit u: a segment starts at window byte u - (upos & 3)
+    // segment (d, kind | M << 2 | off << 16): output position X takes its byte from X + d
+    // (K_LIT: input-ring index; K_MATCH / K_OVL: output position); M = window byte where
+    // the segment starts, off = match offset (K_OVL: bytes at or past M + off repeat the period)
+    uint2 seg[kMaxSeg];
+};
+// LDS layout of a unit (10 KiB: 16 units per CU, a 4096-block batch resident at once). The input
+// ring sits at 0 and the output ring at 4096, each followed by a mirror of its first dword, so a
+// segment's source address is one mask (input: s & 2047; output: (s & 4095) | 4096) and a dword
+// read never wraps.
+constexpr uint32_t kMirror = 16;
+constexpr uint32_t kCinOff = 0;
+constexpr uint32_t kSlot = (uint32_t)((sizeof(Slot) + 15) & ~(size_t)15);
+constexpr uint32_t kSlot0Off = kCinOff + dec::kCring + kMirror;
+constexpr uint32_t kLutOff = kSlot0Off + kSlot;       // 16 x uint4: byte masks of a lane's segments
+constexpr uint32_t kSinkOff = kLutOff + 16 * 16;
+constexpr uint32_t kDoneOff = kSinkOff + dec::kSink;
+constexpr uint32_t kRingOff = 4096;
+constexpr uint32_t kSlot1Off = kRingOff + dec::kRing + kMirror;
+constexpr uint32_t kPslotOff = kSlot1Off + kSlot;
+constexpr uint32_t kPslots = 256;  // P: member compaction table (u16 per member, 128 entries)
+constexpr uint32_t kLds = kPslotOff + kPslots;
+static_assert(kDoneOff + 16 <= kRingOff, "slot 0, mask table and flags fit below the output ring");
+static_assert(kLds <= 10240, "16 units per CU (a 4096-block batch resident at once) need <= 10 KiB each");
+}  // namespace dpe
+
+// E: one window from its segment table, 256 output bytes per pass, one aligned ring dword per
+// lane. A lane's 4 bytes belong to at most three segments (matches are >= 4 bytes long, so a
+// middle segment is a literal run): the segment-start bitmask gives each lane its first (A) and
+// last (B) segment (popcount + wave prefix sum) and a 16-entry table the byte masks. Every part's
+// 4 source bytes are one unaligned dword of the input ring (literals) or the output ring
+// (matches): v_perm of two such dwords also covers matches that overlap themselves (their bytes
+// repeat the match's first period, phase (X - M) mod off). Sources older than the output ring
+// come from HBM. A match whose source lies inside the pass reads it after the pass's first store;
+// the pass re-gathers until no value changes (sources precede their bytes, so the fixed point
+// is the decoded output).
+__device__ __forceinline__ uint32_t lds_dw(const uint8_t* smem, uint32_t a) {  // 4 bytes at LDS byte a
+    const uint32_t* r = (const uint32_t*)(smem + (a & ~3u));
+    return __builtin_amdgcn_alignbyte(r[1], r[0], a & 3u);
+}
+__device__ __forceinline__ uint32_t hbm_dw(const uint8_t* p) {  // 4 bytes at p (both dwords readable)
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
+}
+__device__ __forceinline__ void dec_exec_seg(DecWave& w, uint8_t* smem, const dpe::Slot& sl, uint32_t S,
+                                             uint32_t nseg, bool far, bool ovl) {
+    using namespace dec;
+    using namespace dpe;
+    const uint32_t lane = (uint32_t)w.lane;
+    const uint32_t upos = w.upos;
+    const uint32_t a0 = upos & 3u;
+    const uint32_t xbase = upos - a0;
+    const uint32_t np = (S + a0 + 255u) >> 8;
+    const uint32_t lo_ring = upos + S - kRing;  // (far windows only) older positions come from HBM
+    const uint32_t smax = nseg - 1u;
+    const uint4* lut = (const uint4*)(smem + kLutOff);
+    uint32_t* ring32 = (uint32_t*)(smem + kRingOff);
+    auto addr = [](uint32_t s, uint32_t kd) -> uint32_t {
+        return kd == K_LIT ? (s & kCmask) : ((s & kMask) | kRingOff);
+    };
+    uint32_t carry = 0;
+    for (uint32_t p = 0; p < np; ++p) {
+        const uint32_t X = xbase + 256u * p + 4u * lane;  // output position of the lane's byte 0
+        const uint32_t X0 = xbase + 256u * p;             // first output position of the pass
+        const uint32_t nib = (sl.bits[8u * p + (lane >> 3)] >> (4u * (lane & 7u))) & 15u;
+        const uint32_t cnt = (uint32_t)__builtin_popcount(nib);
+        const uint32_t incl = wave_incl_sum(cnt);
+        const uint32_t ex = incl - cnt + carry;  // segments started before the lane's byte 0
+        carry += rdl(incl, 63);
+        const uint32_t oA = ex + (nib & 1u) - 1u, oB = ex + cnt - 1u;  // owners of bytes 0 and 3
+        const uint4 L = lut[nib];  // (A bytes, A + C bytes, 3 segments, 8 x first byte of B)
+        const uint2 eA = sl.seg[umin32(oA, smax)], eB = sl.seg[umin32(oB, smax)];
+        const uint32_t kdA = eA.y & 3u, kdB = eB.y & 3u;
+        const uint32_t sA = X + eA.x, sB = X + eB.x;
+        uint32_t aA = addr(sA, kdA), aB = addr(sB, kdB);
+        uint32_t a2A = aA, a2B = aB, selA = 0x03020100u, selB = 0x03020100u;
+        const bool lok = (X + 4u > upos) & (X < upos + S);  // some byte of the lane is in the window
+        // ---- sources older than the ring: HBM, where this wave flushed them windows ago (B's
+        // first byte is byte L.w / 8, whose source sB + that may be position 0 while sB is not)
+        const uint32_t kB = L.w >> 3;
+        const bool farA = far & lok & (oA <= smax) & (kdA != K_LIT) & (sA < lo_ring);
+        const bool farB = far & lok & (kdB != K_LIT) & (sB + kB < lo_ring);
+        uint32_t fvA = 0, fvB = 0;
+        if (__ballot(farA | farB)) {
+            fvA = hbm_dw(w.out + (farA ? sA : 0u));
+            fvB = hbm_dw(w.out + (farB ? sB + kB : 0u)) << L.w;
+        }
+        // ---- the middle literal run of a three-segment lane: fixed, read once
+        uint32_t craw = 0;
+        if (__ballot(L.z)) {
+            const uint2 eC = sl.seg[umin32(oA + 1u, smax)];
+            craw = lds_dw(smem, (X + eC.x) & kCmask);
+        }
+        // ---- matches overlapping themselves: byte j repeats the first period [M - off, M)
+        const bool ovA = ovl & (kdA == K_OVL), ovB = ovl & (kdB == K_OVL);
+        const bool anyov = ovl && __ballot(ovA | ovB);
+        if (anyov) {
+            auto period = [&](uint2 e, uint32_t& a1, uint32_t& a2, uint32_t& sel) {
+                const uint32_t Ma = upos + ((e.y >> 2) & 0x3FFFu), off = e.y >> 16;
+                // r0 = (X - Ma) mod off; ee < 2^24, ee * rcp(off) is exact or one short
+                const uint32_t ee = X - Ma + 4u * off;
+                const uint32_t qt = (uint32_t)((float)ee * __builtin_amdgcn_rcpf((float)off));
+                uint32_t r0 = ee - __umul24(qt, off);
+                r0 = r0 >= off ? r0 - off : r0;
+                if (off >= 4u) {
+                    const uint32_t s1 = Ma - off + r0;  // bytes j < off - r0 from s1 + j, the rest from s1 + j - off
+                    a1 = addr(s1, K_MATCH);
+                    a2 = addr(s1 - off, K_MATCH);
+                    const uint32_t sp = off - r0 < 4u ? off - r0 : 4u;
+                    const uint32_t hm = sp >= 4u ? 0u : 0xFFFFFFFFu << (8u * sp);  // bytes from s1 - off
+                    sel = (0x07060504u & hm) | (0x03020100u & ~hm);
+                } else {
+                    a1 = a2 = addr(Ma - off, K_MATCH);
+                    const uint32_t r1 = r0 + 1u >= off ? r0 + 1u - off : r0 + 1u;
+                    const uint32_t r2 = r1 + 1u >= off ? r1 + 1u - off : r1 + 1u;
+                    const uint32_t r3 = r2 + 1u >= off ? r2 + 1u - off : r2 + 1u;
+                    sel = r0 | (r1 << 8) | (r2 << 16) | (r3 << 24);
+                }
+            };
+            if (ovA) period(eA, aA, a2A, selA);
+            if (ovB) period(eB, aB, a2B, selB);
+        }
+        auto gather = [&]() -> uint32_t {
+            uint32_t vA = lds_dw(smem, aA), vB = lds_dw(smem, aB);
+            if (anyov) {
+                vA = __builtin_amdgcn_perm(lds_dw(smem, a2A), vA, selA);
+                vB = __builtin_amdgcn_perm(lds_dw(smem, a2B), vB, selB);
+            }
+            vA = farA ? fvA : vA;
+            vB = farB ? fvB : vB;
+            const uint32_t t = (vA & L.x) | (craw & ~L.x);  // A bytes, then C
+            return (t & L.y) | (vB & ~L.y);                  // then B
+        };
+        // bytes outside the window (first and last pass) keep the ring's older content
+        const bool edge = (p == 0u) | (p + 1u == np);
+        uint32_t vm = 0xFFFFFFFFu;
+        if (edge) {
+            vm = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) vm |= (X + j - upos < S) ? 0xFFu << (8u * j) : 0u;
+        }
+        const uint32_t ri = (X & kMask) >> 2;
+        const uint32_t mi = ri == 0u ? kRing / 4u : (kSinkOff - kRingOff) / 4u + (lane & 15u);  // mirror
+        auto store = [&](uint32_t v) {
+            if (edge) v = (v & vm) | (ring32[ri] & ~vm);
+            ring32[ri] = v;
+            ring32[mi] = v;
+        };
+        uint32_t val = gather();
+        store(val);
+        // ---- matches reading this pass: re-gather until the pass is a fixed point
+        const uint32_t MA = upos + ((eA.y >> 2) & 0x3FFFu), MB = upos + ((eB.y >> 2) & 0x3FFFu);
+        const bool pA = (kdA != K_LIT) & !farA & (kdA == K_OVL ? MA > X0 : sA + 4u > X0);
+        const bool pB = (kdB != K_LIT) & !farB & (kdB == K_OVL ? MB > X0 : sB + 4u > X0);
+        const bool pnd = lok & (pA | pB);
+        if (__ballot(pnd)) {
+            for (;;) {
+                wave_sync();
+                const uint32_t nv = gather();
+                const bool ch = pnd & (nv != val);
+                if (!__ballot(ch)) break;
+                val = ch ? nv : val;
+                if (ch) store(val);
+            }
+        }
+        wave_sync();
+    }
+    w.upos = upos + S;
+    dec_maybe_flush(w);
+}
+
+#ifndef S3HC_PE_WAVES_PER_EU
+#define S3HC_PE_WAVES_PER_EU 8
+#endif
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAVES_PER_EU, 8))) void k_decode_pe(
+    const uint8_t* __restrict__ src, uint8_t* dst, const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+    uint32_t nunits, uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
+    const uint8_t* __restrict__ unit_lb) {
+    using namespace dec;
+    using dpe::Slot;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[dpe::kLds];
+    const uint32_t u = blockIdx.x;
+    if (u >= nunits) return;
+    if (unit_lb && unit_lb[u]) return;  // decoded by the large-block path (s3hc_lb.hip)
+    const DecUnit U = units[u];
+    if (U.n == 0) return;
+    const int lane = lane_id();
+    const bool isP = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == 0;
+    uint8_t* ring = smem + dpe::kRingOff;
+    uint8_t* cin = smem + dpe::kCinOff;
+    uint8_t* sink = smem + dpe::kSinkOff;
+    Slot* slot0 = (Slot*)(smem + dpe::kSlot0Off);
+    Slot* slot1 = (Slot*)(smem + dpe::kSlot1Off);
+    uint16_t* pslots = (uint16_t*)(smem + dpe::kPslotOff);
+    volatile uint32_t* done = (volatile uint32_t*)(smem + dpe::kDoneOff);
+
+    // ---- E state
+    DecWave w;
+    w.ring = ring;
+    w.cin = cin;
+    w.marks = nullptr;
+    w.refs = nullptr;
+    w.sink = sink;
+    w.mtab = nullptr;
+    w.mmax = 0;
+    w.out = dst + blk[U.first].dst_off;
+    w.upos = 0;
+    w.flushed = 0;
+    w.lane = lane;
+    // ---- P state (wave-uniform except pf)
+    uint32_t b = 0;          // next block of the unit
+    int status = S3HC_OK;
+    uint32_t upos = 0;       // unit bytes produced by everything emitted so far
+    uint32_t bstart = 0;     // upos at the start of the current block
+    bool inblk = false;      // inside a compressed block
+    bool ended = false;
+    uint32_t prev_lo = 0xFFFFFFFFu;  // input-ring start of the window E executes this step (none)
+    const uint8_t* in = nullptr;
+    const uint32_t* aw = nullptr;
+    uint32_t C = 0, limit = 0, cap = 0, hist = 0, mis = 0, kmax = 0, fill_end = 0, fill = 0, q = 0, pf = 0;
+    if (!isP) {
+        if (lane == 0) *done = 0u;
+        if (lane < 16) {  // byte masks of a lane's segments by its 4 start bits (bit j: a segment starts at byte j)
+            const uint32_t hb = (uint32_t)lane & 14u;
+            const uint32_t kB = hb ? 31u - (uint32_t)__builtin_clz(hb) : 0u;  // first byte of the last segment
+            const bool three = (hb & (hb - 1u)) != 0u;
+            const uint32_t kA = three ? (uint32_t)__builtin_ctz(hb) : kB;     // first byte after the first segment
+            const uint32_t mlo = kB ? 0xFFFFFFFFu >> (32u - 8u * kB) : 0u;
+            const uint32_t mA = kA ? 0xFFFFFFFFu >> (32u - 8u * kA) : 0u;
+            ((uint4*)(smem + dpe::kLutOff))[lane] = make_uint4(mA, mlo, three ? 1u : 0u, 8u * kB);
+        }
+    }
+    for (uint32_t it = 0;; ++it) {
+        if (isP) {
+            Slot& sl = (it & 1u) ? *slot1 : *slot0;
+            uint32_t cmd = dpe::C_NOP;
+            uint32_t emit_lo = 0xFFFFFFFFu;
+            // block bookkeeping: P knows every block's size and status before E has run it
+            auto finish_block = [&](int st) {
+                if (lane == 0) {
+                    blk_out[U.first + b] = st == S3HC_OK ? upos - bstart : 0u;
+                    blk_status[U.first + b] = st;
+                }
+                status = st;
+                inblk = false;
+                ++b;
+            };
+            while (!ended && cmd == dpe::C_NOP) {
+                if (!inblk) {
+                    if (b == U.n) {
+                        cmd = dpe::C_END;
+                        ended = true;
+                        break;
+                    }
+                    const DecBlock B = blk[U.first + b];
+                    bstart = upos;
+                    if (status != S3HC_OK) {
+                        finish_block(status);
+                        continue;
+                    }
+                    in = src + B.src_off;
+                    if (B.flags & DB_STORED) {
+                        if (B.csize > B.limit) { finish_block(S3HC_CORRUPT); continue; }
+                        if (B.csize > B.cap) { finish_block(S3HC_DST_TOO_SMALL); continue; }
+                        cmd = dpe::C_STORED;
+                        if (lane == 0) {
+                            sl.ptr = (uint64_t)(uintptr_t)in;
+                            sl.tlit = B.csize;
+                            sl.single = U.n == 1 ? 1u : 0u;
+                        }
+                        upos += B.csize;
+                        finish_block(S3HC_OK);
+                        break;
+                    }
+                    if (B.csize == 0) { finish_block(S3HC_CORRUPT); continue; }
+                    if (prev_lo != 0xFFFFFFFFu) break;  // E still reads the input ring: restage next step
+                    C = B.csize;
+                    limit = B.limit;
+                    cap = B.cap;
+                    hist = (B.flags & DB_LINKED) ? upos : 0u;
+                    mis = (uint32_t)((uintptr_t)in & 3);
+                    aw = (const uint32_t*)((uintptr_t)in - mis);
+                    kmax = (mis + C - 1) >> 2;
+                    fill_end = (mis + C + kChunk - 1) & ~(kChunk - 1);
+                    {
+                        uint32_t d[kInit];
+#pragma unroll
+                        for (uint32_t c = 0; c < kInit; ++c) {
+                            const uint32_t k = 64u * c + (uint32_t)lane;
+                            d[c] = aw[k < kmax ? k : kmax];
+                        }
+                        const uint32_t kp = 64u * kInit + (uint32_t)lane;
+                        pf = aw[kp < kmax ? kp : kmax];
+#pragma unroll
+                        for (uint32_t c = 0; c < kInit; ++c) ((uint32_t*)cin)[64u * c + (uint32_t)lane] = d[c];
+                        if (lane == 0) ((uint32_t*)cin)[kCring / 4] = d[0];  // mirror of the ring's first dword
+                        fill = kInit * kChunk;
+                    }
+                    q = 0;
+                    inblk = true;
+                }
+                // ---- one window at q
+                if (q >= C) { finish_block(S3HC_CORRUPT); continue; }
+                {
+                    const uint32_t want = q + mis + kAhead < fill_end ? q + mis + kAhead : fill_end;
+                    // the window E executes this step reads input-ring bytes from prev_lo on
+                    const uint32_t guard = prev_lo == 0xFFFFFFFFu ? 0xFFFFFFFFu : prev_lo + kCring - kChunk;
+                    while (fill < want && fill <= guard) {
+                        const uint32_t ci = ((fill >> 2) + lane) & (kCring / 4 - 1);
+                        ((uint32_t*)cin)[ci] = pf;
+                        if (ci == 0) ((uint32_t*)cin)[kCring / 4] = pf;  // mirror
+                        fill += kChunk;
+                        const uint32_t kn = (fill >> 2) + (uint32_t)lane;
+                        pf = aw[kn < kmax ? kn : kmax];
+                    }
+                    wave_sync();
+                }
+                const uint32_t nx0 = dec_step<true>(cin, q + lane, q, mis, C, fill);
+                const uint32_t nx1 = dec_step<true>(cin, q + 64 + lane, q, mis, C, fill);
+                const uint32_t nx2 = dec_step<true>(cin, q + 128 + lane, q, mis, C, fill);
+                const uint32_t nx3 = dec_step<true>(cin, q + 192 + lane, q, mis, C, fill);
+                uint64_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+                uint32_t l = 0, lastl = 0;
+                WALK_PRIO_ON();
+                while (l < 64u) { lastl = l; m0 |= 1ull << l; l = rdl(nx0, l); }
+                while (l < 128u) { lastl = l; m1 |= 1ull << (l - 64u); l = rdl(nx1, l - 64u); }
+                while (l < 192u) { lastl = l; m2 |= 1ull << (l - 128u); l = rdl(nx2, l - 128u); }
+                while (l < 256u) { lastl = l; m3 |= 1ull << (l - 192u); l = rdl(nx3, l - 192u); }
+                WALK_PRIO_OFF();
+                const uint32_t c1 = (uint32_t)__builtin_popcountll(m0), c2 = c1 + (uint32_t)__builtin_popcountll(m1);
+                const uint32_t c3 = c2 + (uint32_t)__builtin_popcountll(m2);
+                uint32_t n = c3 + (uint32_t)__builtin_popcountll(m3);
+                {
+                    auto put = [&](uint64_t m, uint32_t base, uint32_t k) {
+                        const uint32_t rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                        *(((m >> lane) & 1ull) ? pslots + rank : (uint16_t*)sink + (lane & 31)) = (uint16_t)(64u * k + (uint32_t)lane);
+                    };
+                    put(m0, 0, 0);
+                    if (m1) put(m1, c1, 1);
+                    if (m2) put(m2, c2, 2);
+                    if (m3) put(m3, c3, 3);
+                    wave_sync();
+                }
+                const uint32_t rp0 = pslots[lane];
+                const uint32_t rp1 = n > 64u ? pslots[64 + lane] : 0u;
+                const DecTok t0 = dec_spec<true>(cin, q + rp0, mis, C, fill);
+                DecTok t1 = {0u, 0u, 0u, 0u, 0u, 0u};
+                if (n > 64u) t1 = dec_spec<true>(cin, q + rp1, mis, C, fill);
+                auto rd2 = [&](uint32_t v0, uint32_t v1, uint32_t m) -> uint32_t { return m < 64 ? rdl(v0, m) : rdl(v1, m - 64); };
+                int stop = 0;  // 0 window exhausted, 1 last sequence, 2 error, 3 slow path at cur, 4 long sequence
+                uint32_t cur, cm = 0;
+                {
+                    const uint32_t fl = rd2(t0.flags, t1.flags, n - 1u);
+                    if (fl & (F_LONG | F_MORE | F_ERR)) {
+                        --n;
+                        stop = (fl & (F_LONG | F_MORE)) ? 3 : 2;
+                        cur = q + lastl;
+                    } else if (fl & F_LAST) {
+                        stop = 1;
+                        cur = C;
+                    } else {
+                        cur = rd2(t0.nxt, t1.nxt, n - 1u);
+                    }
+                }
+                uint32_t S = 0;
+                if (n) {
+                    bool isM0 = (uint32_t)lane < n, isM1 = (uint32_t)lane + 64u < n;
+                    const uint32_t sl0 = isM0 ? t0.ll + ((t0.flags & F_LAST) ? 0u : t0.ml) : 0u;
+                    const uint32_t sl1 = isM1 ? t1.ll + ((t1.flags & F_LAST) ? 0u : t1.ml) : 0u;
+                    const uint32_t orel0 = wave_excl_scan(sl0, lane);
+                    const uint32_t tot0 = rdl(orel0 + sl0, 63);
+                    uint32_t orel1 = tot0;
+                    S = tot0;
+                    if (n > 64u) {
+                        orel1 = tot0 + wave_excl_scan(sl1, lane);
+                        S = rdl(orel1 + sl1, 63);
+                    }
+                    const uint64_t cut0 = __ballot(isM0 && orel0 + sl0 > kWin);
+                    const uint64_t cut1 = __ballot(isM1 && orel1 + sl1 > kWin);
+                    if (cut0 | cut1) {
+                        const uint32_t c = cut0 ? (uint32_t)__builtin_ctzll(cut0) : 64u + (uint32_t)__builtin_ctzll(cut1);
+                        n = c;
+                        isM0 = (uint32_t)lane < n;
+                        isM1 = (uint32_t)lane + 64u < n;
+                        S = rd2(orel0, orel1, c);
+                        stop = n ? 0 : 4;
+                        cm = c;
+                        cur = q + rd2(rp0, rp1, c);
+                    }
+                    if (n) {
+                        const uint32_t base = upos - bstart;
+                        auto check = [&](const DecTok& T, uint32_t orel) -> int {
+                            const uint32_t produced = base + orel;
+                            const bool lastm = (T.flags & F_LAST) != 0;
+                            const uint32_t have = produced + T.ll;
+                            int st = S3HC_OK;
+                            st = (!lastm && T.ml > cap - have) ? S3HC_DST_TOO_SMALL : st;
+                            st = (!lastm && T.ml > limit - have) ? S3HC_CORRUPT : st;
+                            st = (!lastm && (T.off == 0 || T.off > have + hist)) ? S3HC_CORRUPT : st;
+                            st = (T.ll > cap - produced) ? S3HC_DST_TOO_SMALL : st;
+                            st = (T.ll > limit - produced) ? S3HC_CORRUPT : st;
+                            return st;
+                        };
+                        const int st0 = check(t0, orel0);
+                        const int st1 = n > 64u ? check(t1, orel1) : S3HC_OK;
+                        const uint64_t bad0 = __ballot(isM0 && st0 != S3HC_OK);
+                        const uint64_t bad1 = n > 64u ? __ballot(isM1 && st1 != S3HC_OK) : 0ull;
+                        if (bad0 | bad1) {
+                            finish_block(bad0 ? (int)rdl((uint32_t)st0, (uint32_t)__builtin_ctzll(bad0))
+                                              : (int)rdl((uint32_t)st1, (uint32_t)__builtin_ctzll(bad1)));
+                            continue;
+                        }
+                        // segments in stream order: member m's literal run (if any), then its match
+                        const uint32_t a0 = upos & 3u;
+                        const bool ln0 = isM0 && t0.ll != 0u, hm0 = isM0 && !(t0.flags & F_LAST);
+                        const bool two = n > 64u;
+                        const bool ln1 = two && isM1 && t1.ll != 0u, hm1 = two && isM1 && !(t1.flags & F_LAST);
+                        const uint64_t bL0 = __ballot(ln0), bM0 = __ballot(hm0);
+                        const uint64_t bL1 = two ? __ballot(ln1) : 0ull, bM1 = two ? __ballot(hm1) : 0ull;
+                        auto below = [&](uint64_t m) -> uint32_t {
+                            return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                        };
+                        const uint32_t n0 = (uint32_t)__builtin_popcountll(bL0) + (uint32_t)__builtin_popcountll(bM0);
+                        const uint32_t r0 = below(bL0) + below(bM0);
+                        const uint32_t r1 = two ? n0 + below(bL1) + below(bM1) : 0u;
+                        const uint32_t nseg = n0 + (uint32_t)__builtin_popcountll(bL1) + (uint32_t)__builtin_popcountll(bM1);
+                        if (lane < (int)dpe::kBitsW) sl.bits[lane] = 0u;
+                        wave_sync();
+                        auto put_seg = [&](const DecTok& T, uint32_t orel, uint32_t r, bool ln, bool hm) {
+                            const uint32_t lr = (T.lit + mis) & kCmask;
+                            if (ln) {
+                                sl.seg[r] = make_uint2(lr - orel - upos, dpe::K_LIT | (orel << 2));
+                                const uint32_t u = orel + a0;
+                                atomicOr(&sl.bits[u >> 5], 1u << (u & 31u));
+                            }
+                            if (hm) {
+                                const uint32_t M = orel + T.ll;
+                                const uint32_t kd = T.off < T.ml ? dpe::K_OVL : dpe::K_MATCH;
+                                sl.seg[r + (ln ? 1u : 0u)] = make_uint2(0u - T.off, kd | (M << 2) | (T.off << 16));
+                                const uint32_t u = M + a0;
+                                atomicOr(&sl.bits[u >> 5], 1u << (u & 31u));
+                            }
+                        };
+                        put_seg(t0, orel0, r0, ln0, hm0);
+                        if (n > 64u) put_seg(t1, orel1, r1, ln1, hm1);
+                        const bool ovl = __ballot((hm0 && t0.off < t0.ml) || (two && hm1 && t1.off < t1.ml)) != 0;
+                        const uint32_t wu = upos;  // E's output position at this window
+                        const bool far = (wu > kRing - S) &&
+                                         __ballot((hm0 && t0.off > kRing - S) || (two && hm1 && t1.off > kRing - S));
+                        if (lane == 0) {
+                            sl.far = far ? 1u : 0u;
+                            sl.ovl = ovl ? 1u : 0u;
+                            sl.nseg = nseg;
+                        }
+                        upos += S;
+                    }
+                }
+                // the window's trailing single sequence (too long for a window, or past the staged input)
+                uint32_t tail = 0, tlit = 0, tll = 0, toff = 0, tml = 0;
+                bool blk_done = stop == 1;
+                if (stop == 2) { finish_block(S3HC_CORRUPT); continue; }
+                if (stop == 4) {
+                    const uint32_t c = cm;
+                    const uint32_t f = rd2(t0.flags, t1.flags, c);
+                    tlit = rd2(t0.lit, t1.lit, c);
+                    tll = rd2(t0.ll, t1.ll, c);
+                    toff = rd2(t0.off, t1.off, c);
+                    tml = rd2(t0.ml, t1.ml, c);
+                    tail = (f & F_LAST) ? 2u : 1u;
+                    if (!(f & F_LAST)) cur = rd2(t0.nxt, t1.nxt, c);
+                } else if (stop == 3) {
+                    uint32_t pos = cur;
+                    const uint32_t t = in[pos];
+                    pos++;
+                    uint32_t sll = t >> 4;
+                    if (sll == 15 && dec_ext_scan(in, C, pos, sll, lane)) { finish_block(S3HC_CORRUPT); continue; }
+                    if (sll > C - pos) { finish_block(S3HC_CORRUPT); continue; }
+                    tlit = pos;
+                    tll = sll;
+                    pos += sll;
+                    if (pos == C) {
+                        tail = 2;
+                    } else {
+                        if (C - pos < 2) { finish_block(S3HC_CORRUPT); continue; }
+                        toff = (uint32_t)in[pos] | ((uint32_t)in[pos + 1] << 8);
+                        pos += 2;
+                        uint32_t sml = (t & 15) + 4;
+                        if ((t & 15) == 15 && dec_ext_scan(in, C, pos, sml, lane)) { finish_block(S3HC_CORRUPT); continue; }
+                        tml = sml;
+                        tail = 1;
+                        cur = pos;
+                    }
+                }
+                if (tail) {
+                    // dec_seq's checks, in stream order
+                    const uint32_t produced = upos - bstart;
+                    int st = S3HC_OK;
+                    if (tll > limit - produced) st = S3HC_CORRUPT;
+                    else if (tll > cap - produced) st = S3HC_DST_TOO_SMALL;
+                    else if (tail == 1) {
+                        const uint32_t have = produced + tll;
+                        if (toff == 0 || toff > have + hist) st = S3HC_CORRUPT;
+                        else if (tml > limit - have) st = S3HC_CORRUPT;
+                        else if (tml > cap - have) st = S3HC_DST_TOO_SMALL;
+                    }
+                    if (st != S3HC_OK) { finish_block(st); continue; }
+                    upos += tll + (tail == 1 ? tml : 0u);
+                    blk_done = tail == 2;
+                }
+                if (n == 0 && tail == 0) {
+                    // nothing to execute (a window whose only token is the block's empty last sequence)
+                    if (blk_done) finish_block(S3HC_OK);
+                    else q = cur;
+                    continue;
+                }
+                cmd = dpe::C_WIN;
+                emit_lo = n ? q + mis : 0xFFFFFFFFu;
+                if (lane == 0) {
+                    sl.S = n ? S : 0u;
+                    if (!n) sl.nseg = 0u;
+                    sl.ptr = (uint64_t)(uintptr_t)in;
+                    sl.tail = tail;
+                    sl.tlit = tlit;
+                    sl.tll = tll;
+                    sl.toff = toff;
+                    sl.tml = tml;
+                }
+                if (blk_done) finish_block(S3HC_OK);
+                else q = cur;
+            }
+            if (lane == 0) sl.cmd = cmd;
+            prev_lo = emit_lo;
+        } else if (it > 0) {
+            const Slot& sl = ((it - 1u) & 1u) ? *slot1 : *slot0;
+            // the header is wave-uniform: scalar copies keep E's loops and branches scalar
+            auto rfl = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+            const uint32_t cmd = rfl(sl.cmd);
+            const uint8_t* sptr = (const uint8_t*)(uintptr_t)(((uint64_t)rfl((uint32_t)(sl.ptr >> 32)) << 32) |
+                                                              rfl((uint32_t)sl.ptr));
+            if (cmd == dpe::C_WIN) {
+                const uint32_t S = rfl(sl.S);
+#ifndef S3HC_DIAG_NOEXEC  // diagnostic builds: P alone (instruction counts of the parse half)
+                if (S) dec_exec_seg(w, smem, sl, S, rfl(sl.nseg), rfl(sl.far) != 0u, rfl(sl.ovl) != 0u);
+#else
+                w.upos += S;
+#endif
+                const uint32_t tail = rfl(sl.tail);
+                if (tail) {
+                    dec_literals(w, sptr, rfl(sl.tlit), rfl(sl.tll), 0xFFFFFFFFu, false);
+                    if (tail == 1) dec_match(w, rfl(sl.toff), rfl(sl.tml));
+                    wave_sync();
+                    if (lane == 0) ((uint32_t*)ring)[kRing / 4] = ((const uint32_t*)ring)[0];  // mirror
+                }
+            } else if (cmd == dpe::C_STORED) {
+                const uint32_t cs = rfl(sl.tlit);
+                if (rfl(sl.single)) {
+                    wave_copy_global(w.out, sptr, cs, lane);
+                    w.upos = w.flushed = cs;
+                } else {
+                    dec_literals(w, sptr, 0, cs, 0xFFFFFFFFu, false);
+                    wave_sync();
+                    if (lane == 0) ((uint32_t*)ring)[kRing / 4] = ((const uint32_t*)ring)[0];  // mirror
+                }
+            } else if (cmd == dpe::C_END) {
+                dec_final_flush(w);
+                if (lane == 0) *done = 1u;
+            }
+        }
+        __syncthreads();
+        if (*done) break;
+    }
 }
 
 // ================================================================== encode
@@ -1743,8 +2370,14 @@ hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock*
                                uint32_t nunits, uint32_t* blk_out, int32_t* blk_status, const uint8_t* unit_lb,
                                hipStream_t st) {
     if (!nunits) return hipSuccess;
-    hipLaunchKernelGGL(k_decode_units, dim3(cdiv(nunits, dec::kWaves)), dim3(64 * dec::kWaves), 0, st, src, dst, blk,
-                       units, nunits, blk_out, blk_status, unit_lb);
+    // S3HC_DEC_ONEWAVE=1 (comparisons): one wave per unit doing both halves (k_decode_units)
+    static const bool onewave = getenv("S3HC_DEC_ONEWAVE") != nullptr;
+    if (onewave)
+        hipLaunchKernelGGL(k_decode_units, dim3(cdiv(nunits, dec::kWaves)), dim3(64 * dec::kWaves), 0, st, src, dst,
+                           blk, units, nunits, blk_out, blk_status, unit_lb);
+    else
+        hipLaunchKernelGGL(k_decode_pe, dim3(nunits), dim3(128), 0, st, src, dst, blk, units, nunits, blk_out,
+                           blk_status, unit_lb);
     return hipGetLastError();
 }
 hipError_t launch_enc_parse(const uint8_t* src, const EncBlock* blocks, const uint2* groups, uint32_t ngroups,
