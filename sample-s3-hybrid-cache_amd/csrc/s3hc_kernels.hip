@@ -975,194 +975,27 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
 // 4096-block batch runs 8 waves per SIMD instead of 4 (10 KiB of LDS and <= 64 VGPRs a unit).
 // Statuses and output sizes are written by P (lane 0), the output bytes by E.
 namespace dpe {
-constexpr uint32_t kMaxMem = 88;                          // members of one window: at most kPos / 3 + 1 = 86
-constexpr uint32_t kMaxSeg = 2 * kMaxMem;                 // a literal run and a match per member
-constexpr uint32_t kBitsW = 8 * ((dec::kWin + 3 + 255) / 256);  // one bit per pass byte (5 passes)
+constexpr uint32_t kMaxMem = 88;  // members of one window: at most kPos / 3 + 1 = 86
 enum : uint32_t { C_NOP = 0, C_WIN = 1, C_STORED = 2, C_END = 3 };
-enum : uint32_t { K_LIT = 0, K_MATCH = 1, K_OVL = 2 };   // segment kinds
 struct Slot {
     uint32_t cmd;
     uint32_t S;       // WIN: output bytes of the members
-    uint32_t nseg;    // WIN: segments
-    uint32_t far;     // WIN: a match reads a source older than the output ring
+    uint32_t n;       // WIN: members
+    uint32_t far;     // WIN: a member reads a source older than the output ring
     uint64_t ptr;     // WIN tail / STORED: compressed block base in HBM
     uint32_t tail;    // WIN: 0 none, 1 one sequence follows the members, 2 it is the block's last
     uint32_t tlit;    // tail literal start (block offset) / STORED: size
     uint32_t tll, toff, tml;
     uint32_t single;  // STORED: the unit's only block (copied straight to HBM)
-    uint32_t ovl;     // WIN: some match overlaps itself (offset < length)
-    uint32_t pad;
-    uint32_t bits[kBitsW];  // bit u: a segment starts at window byte u - (upos & 3)
-    // segment (d, kind | M << 2 | off << 16): output position X takes its byte from X + d
-    // (K_LIT: input-ring index; K_MATCH / K_OVL: output position); M = window byte where
-    // the segment starts, off = match offset (K_OVL: bytes at or past M + off repeat the period)
-    uint2 seg[kMaxSeg];
+    uint2 mtab[kMaxMem];
+    uint16_t orel[kMaxMem];  // member's first window byte; 0xFFFF = produces nothing
 };
-// LDS layout of a unit (10 KiB: 16 units per CU, a 4096-block batch resident at once). The input
-// ring sits at 0 and the output ring at 4096, each followed by a mirror of its first dword, so a
-// segment's source address is one mask (input: s & 2047; output: (s & 4095) | 4096) and a dword
-// read never wraps.
-constexpr uint32_t kMirror = 16;
-constexpr uint32_t kCinOff = 0;
 constexpr uint32_t kSlot = (uint32_t)((sizeof(Slot) + 15) & ~(size_t)15);
-constexpr uint32_t kSlot0Off = kCinOff + dec::kCring + kMirror;
-constexpr uint32_t kLutOff = kSlot0Off + kSlot;       // 16 x uint4: byte masks of a lane's segments
-constexpr uint32_t kSinkOff = kLutOff + 16 * 16;
-constexpr uint32_t kDoneOff = kSinkOff + dec::kSink;
-constexpr uint32_t kRingOff = 4096;
-constexpr uint32_t kSlot1Off = kRingOff + dec::kRing + kMirror;
-constexpr uint32_t kPslotOff = kSlot1Off + kSlot;
 constexpr uint32_t kPslots = 256;  // P: member compaction table (u16 per member, 128 entries)
-constexpr uint32_t kLds = kPslotOff + kPslots;
-static_assert(kDoneOff + 16 <= kRingOff, "slot 0, mask table and flags fit below the output ring");
+constexpr uint32_t kMirror = 16;  // the input ring is followed by a copy of its first dword
+constexpr uint32_t kLds = dec::kRing + dec::kCring + kMirror + dec::kMarks + 2 * dec::kRefs + dec::kSink + 2 * kSlot + kPslots + 16;
 static_assert(kLds <= 10240, "16 units per CU (a 4096-block batch resident at once) need <= 10 KiB each");
 }  // namespace dpe
-
-// E: one window from its segment table, 256 output bytes per pass, one aligned ring dword per
-// lane. A lane's 4 bytes belong to at most three segments (matches are >= 4 bytes long, so a
-// middle segment is a literal run): the segment-start bitmask gives each lane its first (A) and
-// last (B) segment (popcount + wave prefix sum) and a 16-entry table the byte masks. Every part's
-// 4 source bytes are one unaligned dword of the input ring (literals) or the output ring
-// (matches): v_perm of two such dwords also covers matches that overlap themselves (their bytes
-// repeat the match's first period, phase (X - M) mod off). Sources older than the output ring
-// come from HBM. A match whose source lies inside the pass reads it after the pass's first store;
-// the pass re-gathers until no value changes (sources precede their bytes, so the fixed point
-// is the decoded output).
-__device__ __forceinline__ uint32_t lds_dw(const uint8_t* smem, uint32_t a) {  // 4 bytes at LDS byte a
-    const uint32_t* r = (const uint32_t*)(smem + (a & ~3u));
-    return __builtin_amdgcn_alignbyte(r[1], r[0], a & 3u);
-}
-__device__ __forceinline__ uint32_t hbm_dw(const uint8_t* p) {  // 4 bytes at p (both dwords readable)
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
-    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
-}
-__device__ __forceinline__ void dec_exec_seg(DecWave& w, uint8_t* smem, const dpe::Slot& sl, uint32_t S,
-                                             uint32_t nseg, bool far, bool ovl) {
-    using namespace dec;
-    using namespace dpe;
-    const uint32_t lane = (uint32_t)w.lane;
-    const uint32_t upos = w.upos;
-    const uint32_t a0 = upos & 3u;
-    const uint32_t xbase = upos - a0;
-    const uint32_t np = (S + a0 + 255u) >> 8;
-    const uint32_t lo_ring = upos + S - kRing;  // (far windows only) older positions come from HBM
-    const uint32_t smax = nseg - 1u;
-    const uint4* lut = (const uint4*)(smem + kLutOff);
-    uint32_t* ring32 = (uint32_t*)(smem + kRingOff);
-    auto addr = [](uint32_t s, uint32_t kd) -> uint32_t {
-        return kd == K_LIT ? (s & kCmask) : ((s & kMask) | kRingOff);
-    };
-    uint32_t carry = 0;
-    for (uint32_t p = 0; p < np; ++p) {
-        const uint32_t X = xbase + 256u * p + 4u * lane;  // output position of the lane's byte 0
-        const uint32_t X0 = xbase + 256u * p;             // first output position of the pass
-        const uint32_t nib = (sl.bits[8u * p + (lane >> 3)] >> (4u * (lane & 7u))) & 15u;
-        const uint32_t cnt = (uint32_t)__builtin_popcount(nib);
-        const uint32_t incl = wave_incl_sum(cnt);
-        const uint32_t ex = incl - cnt + carry;  // segments started before the lane's byte 0
-        carry += rdl(incl, 63);
-        const uint32_t oA = ex + (nib & 1u) - 1u, oB = ex + cnt - 1u;  // owners of bytes 0 and 3
-        const uint4 L = lut[nib];  // (A bytes, A + C bytes, 3 segments, 8 x first byte of B)
-        const uint2 eA = sl.seg[umin32(oA, smax)], eB = sl.seg[umin32(oB, smax)];
-        const uint32_t kdA = eA.y & 3u, kdB = eB.y & 3u;
-        const uint32_t sA = X + eA.x, sB = X + eB.x;
-        uint32_t aA = addr(sA, kdA), aB = addr(sB, kdB);
-        uint32_t a2A = aA, a2B = aB, selA = 0x03020100u, selB = 0x03020100u;
-        const bool lok = (X + 4u > upos) & (X < upos + S);  // some byte of the lane is in the window
-        // ---- sources older than the ring: HBM, where this wave flushed them windows ago (B's
-        // first byte is byte L.w / 8, whose source sB + that may be position 0 while sB is not)
-        const uint32_t kB = L.w >> 3;
-        const bool farA = far & lok & (oA <= smax) & (kdA != K_LIT) & (sA < lo_ring);
-        const bool farB = far & lok & (kdB != K_LIT) & (sB + kB < lo_ring);
-        uint32_t fvA = 0, fvB = 0;
-        if (__ballot(farA | farB)) {
-            fvA = hbm_dw(w.out + (farA ? sA : 0u));
-            fvB = hbm_dw(w.out + (farB ? sB + kB : 0u)) << L.w;
-        }
-        // ---- the middle literal run of a three-segment lane: fixed, read once
-        uint32_t craw = 0;
-        if (__ballot(L.z)) {
-            const uint2 eC = sl.seg[umin32(oA + 1u, smax)];
-            craw = lds_dw(smem, (X + eC.x) & kCmask);
-        }
-        // ---- matches overlapping themselves: byte j repeats the first period [M - off, M)
-        const bool ovA = ovl & (kdA == K_OVL), ovB = ovl & (kdB == K_OVL);
-        const bool anyov = ovl && __ballot(ovA | ovB);
-        if (anyov) {
-            auto period = [&](uint2 e, uint32_t& a1, uint32_t& a2, uint32_t& sel) {
-                const uint32_t Ma = upos + ((e.y >> 2) & 0x3FFFu), off = e.y >> 16;
-                // r0 = (X - Ma) mod off; ee < 2^24, ee * rcp(off) is exact or one short
-                const uint32_t ee = X - Ma + 4u * off;
-                const uint32_t qt = (uint32_t)((float)ee * __builtin_amdgcn_rcpf((float)off));
-                uint32_t r0 = ee - __umul24(qt, off);
-                r0 = r0 >= off ? r0 - off : r0;
-                if (off >= 4u) {
-                    const uint32_t s1 = Ma - off + r0;  // bytes j < off - r0 from s1 + j, the rest from s1 + j - off
-                    a1 = addr(s1, K_MATCH);
-                    a2 = addr(s1 - off, K_MATCH);
-                    const uint32_t sp = off - r0 < 4u ? off - r0 : 4u;
-                    const uint32_t hm = sp >= 4u ? 0u : 0xFFFFFFFFu << (8u * sp);  // bytes from s1 - off
-                    sel = (0x07060504u & hm) | (0x03020100u & ~hm);
-                } else {
-                    a1 = a2 = addr(Ma - off, K_MATCH);
-                    const uint32_t r1 = r0 + 1u >= off ? r0 + 1u - off : r0 + 1u;
-                    const uint32_t r2 = r1 + 1u >= off ? r1 + 1u - off : r1 + 1u;
-                    const uint32_t r3 = r2 + 1u >= off ? r2 + 1u - off : r2 + 1u;
-                    sel = r0 | (r1 << 8) | (r2 << 16) | (r3 << 24);
-                }
-            };
-            if (ovA) period(eA, aA, a2A, selA);
-            if (ovB) period(eB, aB, a2B, selB);
-        }
-        auto gather = [&]() -> uint32_t {
-            uint32_t vA = lds_dw(smem, aA), vB = lds_dw(smem, aB);
-            if (anyov) {
-                vA = __builtin_amdgcn_perm(lds_dw(smem, a2A), vA, selA);
-                vB = __builtin_amdgcn_perm(lds_dw(smem, a2B), vB, selB);
-            }
-            vA = farA ? fvA : vA;
-            vB = farB ? fvB : vB;
-            const uint32_t t = (vA & L.x) | (craw & ~L.x);  // A bytes, then C
-            return (t & L.y) | (vB & ~L.y);                  // then B
-        };
-        // bytes outside the window (first and last pass) keep the ring's older content
-        const bool edge = (p == 0u) | (p + 1u == np);
-        uint32_t vm = 0xFFFFFFFFu;
-        if (edge) {
-            vm = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) vm |= (X + j - upos < S) ? 0xFFu << (8u * j) : 0u;
-        }
-        const uint32_t ri = (X & kMask) >> 2;
-        const uint32_t mi = ri == 0u ? kRing / 4u : (kSinkOff - kRingOff) / 4u + (lane & 15u);  // mirror
-        auto store = [&](uint32_t v) {
-            if (edge) v = (v & vm) | (ring32[ri] & ~vm);
-            ring32[ri] = v;
-            ring32[mi] = v;
-        };
-        uint32_t val = gather();
-        store(val);
-        // ---- matches reading this pass: re-gather until the pass is a fixed point
-        const uint32_t MA = upos + ((eA.y >> 2) & 0x3FFFu), MB = upos + ((eB.y >> 2) & 0x3FFFu);
-        const bool pA = (kdA != K_LIT) & !farA & (kdA == K_OVL ? MA > X0 : sA + 4u > X0);
-        const bool pB = (kdB != K_LIT) & !farB & (kdB == K_OVL ? MB > X0 : sB + 4u > X0);
-        const bool pnd = lok & (pA | pB);
-        if (__ballot(pnd)) {
-            for (;;) {
-                wave_sync();
-                const uint32_t nv = gather();
-                const bool ch = pnd & (nv != val);
-                if (!__ballot(ch)) break;
-                val = ch ? nv : val;
-                if (ch) store(val);
-            }
-        }
-        wave_sync();
-    }
-    w.upos = upos + S;
-    dec_maybe_flush(w);
-}
 
 #ifndef S3HC_PE_WAVES_PER_EU
 #define S3HC_PE_WAVES_PER_EU 8
@@ -1181,23 +1014,24 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAV
     if (U.n == 0) return;
     const int lane = lane_id();
     const bool isP = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) == 0;
-    uint8_t* ring = smem + dpe::kRingOff;
-    uint8_t* cin = smem + dpe::kCinOff;
-    uint8_t* sink = smem + dpe::kSinkOff;
-    Slot* slot0 = (Slot*)(smem + dpe::kSlot0Off);
-    Slot* slot1 = (Slot*)(smem + dpe::kSlot1Off);
-    uint16_t* pslots = (uint16_t*)(smem + dpe::kPslotOff);
-    volatile uint32_t* done = (volatile uint32_t*)(smem + dpe::kDoneOff);
+    uint8_t* ring = smem;
+    uint8_t* cin = ring + kRing;
+    uint8_t* marks = cin + kCring + dpe::kMirror;
+    uint16_t* refs = (uint16_t*)(marks + kMarks);
+    uint8_t* sink = (uint8_t*)(refs + kRefs);
+    Slot* slots = (Slot*)(sink + kSink);
+    uint16_t* pslots = (uint16_t*)((uint8_t*)slots + 2 * dpe::kSlot);
+    volatile uint32_t* done = (volatile uint32_t*)((uint8_t*)pslots + dpe::kPslots);
 
     // ---- E state
     DecWave w;
     w.ring = ring;
     w.cin = cin;
-    w.marks = nullptr;
-    w.refs = nullptr;
+    w.marks = marks;
+    w.refs = refs;
     w.sink = sink;
-    w.mtab = nullptr;
-    w.mmax = 0;
+    w.mtab = slots[0].mtab;
+    w.mmax = dpe::kMaxMem - 1;
     w.out = dst + blk[U.first].dst_off;
     w.upos = 0;
     w.flushed = 0;
@@ -1214,20 +1048,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAV
     const uint32_t* aw = nullptr;
     uint32_t C = 0, limit = 0, cap = 0, hist = 0, mis = 0, kmax = 0, fill_end = 0, fill = 0, q = 0, pf = 0;
     if (!isP) {
+        for (uint32_t i = (uint32_t)lane; i < kMarks / 16; i += 64) ((uint4*)marks)[i] = make_uint4(0, 0, 0, 0);
         if (lane == 0) *done = 0u;
-        if (lane < 16) {  // byte masks of a lane's segments by its 4 start bits (bit j: a segment starts at byte j)
-            const uint32_t hb = (uint32_t)lane & 14u;
-            const uint32_t kB = hb ? 31u - (uint32_t)__builtin_clz(hb) : 0u;  // first byte of the last segment
-            const bool three = (hb & (hb - 1u)) != 0u;
-            const uint32_t kA = three ? (uint32_t)__builtin_ctz(hb) : kB;     // first byte after the first segment
-            const uint32_t mlo = kB ? 0xFFFFFFFFu >> (32u - 8u * kB) : 0u;
-            const uint32_t mA = kA ? 0xFFFFFFFFu >> (32u - 8u * kA) : 0u;
-            ((uint4*)(smem + dpe::kLutOff))[lane] = make_uint4(mA, mlo, three ? 1u : 0u, 8u * kB);
-        }
     }
     for (uint32_t it = 0;; ++it) {
         if (isP) {
-            Slot& sl = (it & 1u) ? *slot1 : *slot0;
+            Slot& sl = slots[it & 1u];
             uint32_t cmd = dpe::C_NOP;
             uint32_t emit_lo = 0xFFFFFFFFu;
             // block bookkeeping: P knows every block's size and status before E has run it
@@ -1405,48 +1231,25 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAV
                                               : (int)rdl((uint32_t)st1, (uint32_t)__builtin_ctzll(bad1)));
                             continue;
                         }
-                        // segments in stream order: member m's literal run (if any), then its match
-                        const uint32_t a0 = upos & 3u;
-                        const bool ln0 = isM0 && t0.ll != 0u, hm0 = isM0 && !(t0.flags & F_LAST);
-                        const bool two = n > 64u;
-                        const bool ln1 = two && isM1 && t1.ll != 0u, hm1 = two && isM1 && !(t1.flags & F_LAST);
-                        const uint64_t bL0 = __ballot(ln0), bM0 = __ballot(hm0);
-                        const uint64_t bL1 = two ? __ballot(ln1) : 0ull, bM1 = two ? __ballot(hm1) : 0ull;
-                        auto below = [&](uint64_t m) -> uint32_t {
-                            return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                        // member table: (M | E << 16, L | off << 16) as dec_window_exec builds it
+                        auto entry = [](uint32_t orel, uint32_t ll, uint32_t off, uint32_t lr) -> uint2 {
+                            const uint32_t M = orel + ll;
+                            const uint32_t E = M + off < 0xFFFFu ? M + off : 0xFFFFu;
+                            return make_uint2(M | (E << 16), ((lr - orel) & 0xFFFFu) | (off << 16));
                         };
-                        const uint32_t n0 = (uint32_t)__builtin_popcountll(bL0) + (uint32_t)__builtin_popcountll(bM0);
-                        const uint32_t r0 = below(bL0) + below(bM0);
-                        const uint32_t r1 = two ? n0 + below(bL1) + below(bM1) : 0u;
-                        const uint32_t nseg = n0 + (uint32_t)__builtin_popcountll(bL1) + (uint32_t)__builtin_popcountll(bM1);
-                        if (lane < (int)dpe::kBitsW) sl.bits[lane] = 0u;
-                        wave_sync();
-                        auto put_seg = [&](const DecTok& T, uint32_t orel, uint32_t r, bool ln, bool hm) {
-                            const uint32_t lr = (T.lit + mis) & kCmask;
-                            if (ln) {
-                                sl.seg[r] = make_uint2(lr - orel - upos, dpe::K_LIT | (orel << 2));
-                                const uint32_t u = orel + a0;
-                                atomicOr(&sl.bits[u >> 5], 1u << (u & 31u));
-                            }
-                            if (hm) {
-                                const uint32_t M = orel + T.ll;
-                                const uint32_t kd = T.off < T.ml ? dpe::K_OVL : dpe::K_MATCH;
-                                sl.seg[r + (ln ? 1u : 0u)] = make_uint2(0u - T.off, kd | (M << 2) | (T.off << 16));
-                                const uint32_t u = M + a0;
-                                atomicOr(&sl.bits[u >> 5], 1u << (u & 31u));
-                            }
-                        };
-                        put_seg(t0, orel0, r0, ln0, hm0);
-                        if (n > 64u) put_seg(t1, orel1, r1, ln1, hm1);
-                        const bool ovl = __ballot((hm0 && t0.off < t0.ml) || (two && hm1 && t1.off < t1.ml)) != 0;
+                        if (isM0) {
+                            sl.mtab[lane] = entry(orel0, t0.ll, t0.off, (t0.lit + mis) & kCmask);
+                            sl.orel[lane] = sl0 ? (uint16_t)orel0 : (uint16_t)0xFFFFu;
+                        }
+                        if (isM1) {
+                            sl.mtab[64 + lane] = entry(orel1, t1.ll, t1.off, (t1.lit + mis) & kCmask);
+                            sl.orel[64 + lane] = sl1 ? (uint16_t)orel1 : (uint16_t)0xFFFFu;
+                        }
                         const uint32_t wu = upos;  // E's output position at this window
                         const bool far = (wu > kRing - S) &&
-                                         __ballot((hm0 && t0.off > kRing - S) || (two && hm1 && t1.off > kRing - S));
-                        if (lane == 0) {
-                            sl.far = far ? 1u : 0u;
-                            sl.ovl = ovl ? 1u : 0u;
-                            sl.nseg = nseg;
-                        }
+                                         __ballot((isM0 && sl0 > t0.ll && t0.off > kRing - S) ||
+                                                  (isM1 && sl1 > t1.ll && t1.off > kRing - S));
+                        if (lane == 0) sl.far = far ? 1u : 0u;
                         upos += S;
                     }
                 }
@@ -1511,8 +1314,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAV
                 cmd = dpe::C_WIN;
                 emit_lo = n ? q + mis : 0xFFFFFFFFu;
                 if (lane == 0) {
-                    sl.S = n ? S : 0u;
-                    if (!n) sl.nseg = 0u;
+                    sl.S = S;
+                    sl.n = n;
                     sl.ptr = (uint64_t)(uintptr_t)in;
                     sl.tail = tail;
                     sl.tlit = tlit;
@@ -1526,25 +1329,32 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAV
             if (lane == 0) sl.cmd = cmd;
             prev_lo = emit_lo;
         } else if (it > 0) {
-            const Slot& sl = ((it - 1u) & 1u) ? *slot1 : *slot0;
+            const Slot& sl = slots[(it - 1u) & 1u];
             // the header is wave-uniform: scalar copies keep E's loops and branches scalar
             auto rfl = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
             const uint32_t cmd = rfl(sl.cmd);
             const uint8_t* sptr = (const uint8_t*)(uintptr_t)(((uint64_t)rfl((uint32_t)(sl.ptr >> 32)) << 32) |
                                                               rfl((uint32_t)sl.ptr));
             if (cmd == dpe::C_WIN) {
-                const uint32_t S = rfl(sl.S);
+                const uint32_t n = rfl(sl.n);
+                if (n) {
+                    const uint32_t a0 = w.upos & 3u;
+                    const uint32_t r0 = (uint32_t)lane < n ? sl.orel[lane] : 0xFFFFu;
+                    const uint32_t r1 = (uint32_t)lane + 64u < n ? sl.orel[64 + lane] : 0xFFFFu;
+                    *(r0 != 0xFFFFu ? marks + r0 + a0 : sink + lane) = (uint8_t)(lane + 1);
+                    *(r1 != 0xFFFFu ? marks + r1 + a0 : sink + lane) = (uint8_t)(lane + 65);
+                    w.mtab = const_cast<uint2*>(sl.mtab);
+                    wave_sync();
 #ifndef S3HC_DIAG_NOEXEC  // diagnostic builds: P alone (instruction counts of the parse half)
-                if (S) dec_exec_seg(w, smem, sl, S, rfl(sl.nseg), rfl(sl.far) != 0u, rfl(sl.ovl) != 0u);
+                    dec_window_passes(w, rfl(sl.S), rfl(sl.far) != 0u);
 #else
-                w.upos += S;
+                    w.upos += rfl(sl.S);
 #endif
+                }
                 const uint32_t tail = rfl(sl.tail);
                 if (tail) {
                     dec_literals(w, sptr, rfl(sl.tlit), rfl(sl.tll), 0xFFFFFFFFu, false);
                     if (tail == 1) dec_match(w, rfl(sl.toff), rfl(sl.tml));
-                    wave_sync();
-                    if (lane == 0) ((uint32_t*)ring)[kRing / 4] = ((const uint32_t*)ring)[0];  // mirror
                 }
             } else if (cmd == dpe::C_STORED) {
                 const uint32_t cs = rfl(sl.tlit);
@@ -1553,8 +1363,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAV
                     w.upos = w.flushed = cs;
                 } else {
                     dec_literals(w, sptr, 0, cs, 0xFFFFFFFFu, false);
-                    wave_sync();
-                    if (lane == 0) ((uint32_t*)ring)[kRing / 4] = ((const uint32_t*)ring)[0];  // mirror
                 }
             } else if (cmd == dpe::C_END) {
                 dec_final_flush(w);
