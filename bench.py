@@ -194,7 +194,9 @@ def cpu_baseline(data_chunk: bytes, block: int, seconds: float):
 
 
 # ------------------------------------------------------------------ the GPU bench (one rank)
-KERNEL_SYMBOL = {"enc_parse": "k_enc_parse", "enc_emit": "k_enc_emit", "decode": "k_decode_units",
+# decode: the parser + executor kernel (k_decode_pe); S3HC_DEC_ONEWAVE=1 selects the one-wave kernel
+KERNEL_SYMBOL = {"enc_parse": "k_enc_parse", "enc_emit": "k_enc_emit",
+                 "decode": "k_decode_units" if os.environ.get("S3HC_DEC_ONEWAVE") else "k_decode_pe",
                  "xxh32": "k_xxh32_ranges"}
 
 
