@@ -203,6 +203,10 @@ void s3hc_handler_stats(const s3hc_handler* h, uint64_t out[6], float* ratio);
 /* record_batch_bytes / record_object (:105-120) for streaming writers. */
 void s3hc_handler_record_batch_bytes(s3hc_handler* h, uint64_t before, uint64_t after);
 void s3hc_handler_record_object(s3hc_handler* h, int compressed);
+/* Tests only (no reference counterpart): make this handler's LZ4 frame encoder (bit 0),
+ * store-mode encoder (bit 1) or decoder (bit 2) fail with S3HC_DEVICE, to exercise the
+ * fallback branches of compress_with_metadata (:420-457) and the decode error path (:483-492). */
+void s3hc_handler_debug_set_faults(s3hc_handler* h, int mask);
 /* is_denylisted_extension (:252-308). */
 int s3hc_is_denylisted_extension(const char* path);
 

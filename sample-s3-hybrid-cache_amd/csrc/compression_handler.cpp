@@ -77,7 +77,8 @@ bool CompressionHandler::encode_store_mode_frame(const uint8_t* data, size_t n, 
                                                  CodecError* err) const {
     out.resize(s3hc_frame_bound(n) + 4 * (n / (4u << 20) + 1));
     size_t len = 0;
-    int rc = s3hc_store_mode_frame(ctx_, data, n, out.data(), out.size(), &len);
+    int rc = (faults_ & 2) ? s3hc::set_error(S3HC_DEVICE, "injected store-mode encoder fault")
+                           : s3hc_store_mode_frame(ctx_, data, n, out.data(), out.size(), &len);
     if (rc) {
         if (err) *err = {rc, std::string("Store-mode frame encoding failed: ") + s3hc_last_error()};
         out.clear();
@@ -146,7 +147,9 @@ bool CompressionHandler::compress_with_algorithm(const uint8_t* data, size_t n, 
     out.data.resize(s3hc_frame_bound(n));
     size_t len = 0;
     int wc = 0;
-    int rc = s3hc_compress_frame(ctx_, data, n, S3HC_BLK_AUTO_LZ4FLEX, out.data.data(), out.data.size(), &len, &wc);
+    int rc = (faults_ & 1) ? s3hc::set_error(S3HC_DEVICE, "injected LZ4 encoder fault")
+                           : s3hc_compress_frame(ctx_, data, n, S3HC_BLK_AUTO_LZ4FLEX, out.data.data(), out.data.size(),
+                                                 &len, &wc);
     if (rc) {
         if (err) *err = {rc, std::string("Failed to write data to LZ4 frame encoder: ") + s3hc_last_error()};
         return false;
@@ -165,7 +168,8 @@ bool CompressionHandler::compress_with_algorithm(const uint8_t* data, size_t n, 
 bool CompressionHandler::decompress_data(const uint8_t* data, size_t n, std::vector<uint8_t>& out,
                                          CodecError* err) const {
     // output grows by the decoded bytes (read_to_end), never by a worst-case bound
-    int rc = decompress_frames_vec(ctx_, data, n, out);
+    int rc = (faults_ & 4) ? s3hc::set_error(S3HC_DEVICE, "injected decoder fault")
+                           : decompress_frames_vec(ctx_, data, n, out);
     if (rc) {  // :483-492
         stats_->decompression_failures.fetch_add(1, std::memory_order_relaxed);
         if (err) *err = {rc, std::string("Failed to decompress cached data: ") + s3hc_last_error()};
@@ -311,6 +315,9 @@ extern "C" void s3hc_handler_record_batch_bytes(s3hc_handler* h, uint64_t before
 }
 extern "C" void s3hc_handler_record_object(s3hc_handler* h, int compressed) {
     if (h) h->h.shared_stats()->record_object(compressed != 0);
+}
+extern "C" void s3hc_handler_debug_set_faults(s3hc_handler* h, int mask) {
+    if (h) h->h.set_debug_faults(mask);
 }
 extern "C" int s3hc_is_denylisted_extension(const char* path) {
     return guarded([&]() -> int {

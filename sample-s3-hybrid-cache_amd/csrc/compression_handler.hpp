@@ -80,6 +80,9 @@ public:
 
     s3hc_ctx* ctx() const { return ctx_; }
     size_t compression_threshold() const { return threshold_; }
+    // Fault injection for tests of the error-fallback branches (:420-457): bit 0 makes the LZ4
+    // frame encoder fail, bit 1 the store-mode encoder, bit 2 the decoder; 0 in production.
+    void set_debug_faults(int mask) { faults_ = mask; }
 
 private:
     s3hc_ctx* ctx_;
@@ -87,6 +90,7 @@ private:
     bool enabled_;
     CompressionAlgorithm preferred_;
     std::shared_ptr<CompressionStatsAtomic> stats_;
+    int faults_ = 0;
 };
 
 // The compression decision of the cache layer (the caller of this codec): which ranges go through

@@ -93,6 +93,7 @@ def _load():
         "s3hc_handler_stats": (None, [vp, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_float)]),
         "s3hc_handler_record_batch_bytes": (None, [vp, u64, u64]),
         "s3hc_handler_record_object": (None, [vp, i32]),
+        "s3hc_handler_debug_set_faults": (None, [vp, i32]),
         "s3hc_is_denylisted_extension": (i32, [ctypes.c_char_p]),
         "s3hc_strip_known_cache_key_suffixes": (sz, [ctypes.c_char_p, ctypes.c_char_p, sz]),
         "s3hc_effective_compression": (i32, [i32, i32, sz, ctypes.c_char_p, u64]),
@@ -644,6 +645,12 @@ class CompressionHandler:
 
     def record_object(self, compressed: bool):
         lib.s3hc_handler_record_object(self.h, 1 if compressed else 0)
+
+    # tests only: make the LZ4 encoder / store-mode encoder / decoder of this handler fail
+    FAULT_LZ4, FAULT_STORE, FAULT_DECODE = 1, 2, 4
+
+    def debug_set_faults(self, mask: int):
+        lib.s3hc_handler_debug_set_faults(self.h, mask)
 
 
 # ---------------------------------------------------------------------------------------------

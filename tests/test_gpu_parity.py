@@ -477,3 +477,60 @@ def test_tiny_blocks_in_4mib_frame_decode_to_nothing(engine, oracle):
             break
         got += c
     assert got == b"after the empty frame"
+
+
+# ---- compress_with_metadata's error-fallback branches (compression.rs:384-457), reached through
+# the handler's test-only fault hook (s3hc_handler_debug_set_faults)
+def test_metadata_lz4_failure_falls_back_to_store_mode(engine, oracle):
+    h = _handler(engine)
+    data = b"log line 42 status=200 bytes=1234\n" * 50
+    h.debug_set_faults(h.FAULT_LZ4)
+    r = h.compress_with_metadata(data, "file.txt", True)
+    # :420-447: compression_failures += 1, a store-mode frame tagged Lz4, was_compressed false
+    assert r.algorithm == S.ALG_LZ4 and not r.was_compressed
+    assert r.data == oracle.store_mode_frame(data)
+    assert r.original_size == len(data) and r.compressed_size == len(r.data)
+    s = h.get_stats()
+    assert s.compression_failures == 1 and s.total_objects_uncompressed == 0 and s.total_objects_compressed == 0
+    h.debug_set_faults(0)
+    assert h.decompress_data(r.data) == data
+
+
+def test_metadata_both_encoders_failing_returns_raw_tagged_lz4(engine):
+    h = _handler(engine)
+    data = b"abcdefghij" * 30
+    h.debug_set_faults(h.FAULT_LZ4 | h.FAULT_STORE)
+    r = h.compress_with_metadata(data, "file.txt", True)
+    # :448-457 (last resort): raw bytes, still tagged Lz4, uncompressed counter += 1
+    assert r.data == data and r.algorithm == S.ALG_LZ4 and not r.was_compressed
+    assert r.compressed_size == r.original_size == len(data)
+    s = h.get_stats()
+    assert s.compression_failures == 1 and s.total_objects_uncompressed == 1
+
+
+def test_metadata_store_mode_failure_returns_raw_tagged_none(engine):
+    h = _handler(engine)
+    data = b"\xff\xd8\xff\xe0fake jpeg bytes"
+    h.debug_set_faults(h.FAULT_STORE)
+    r = h.compress_with_metadata(data, "image.jpg", False)
+    # :399-416: raw bytes tagged None, compression_failures and total_objects_uncompressed += 1
+    assert r.data == data and r.algorithm == S.ALG_NONE and not r.was_compressed
+    assert r.compressed_size == len(data)
+    s = h.get_stats()
+    assert s.compression_failures == 1 and s.total_objects_uncompressed == 1
+
+
+def test_decompress_with_algorithm_none_and_decoder_fault(engine):
+    h = _handler(engine)
+    raw = b"legacy uncompressed cache entry"
+    # :594-604: None -> the bytes as stored (to_vec), no decoder involved, no counter touched
+    assert h.decompress_with_algorithm(raw, S.ALG_NONE) == raw
+    assert h.get_stats().decompression_failures == 0
+    frame = h.compress_with_algorithm(raw).data
+    h.debug_set_faults(h.FAULT_DECODE)
+    with pytest.raises(S.CodecError):
+        h.decompress_with_algorithm(frame, S.ALG_LZ4)
+    assert h.get_stats().decompression_failures == 1
+    assert h.decompress_with_algorithm(raw, S.ALG_NONE) == raw  # the None arm never decodes
+    h.debug_set_faults(0)
+    assert h.decompress_with_algorithm(frame, S.ALG_LZ4) == raw
