@@ -1400,6 +1400,27 @@ constexpr uint32_t kEmpty = 0xFFFFu;
 // LZ4 length-extension bytes for a length field of n: (n - 15) / 255 + 1 for n >= 15, else 0
 // (branch-free form: (n + 240) / 255).
 __device__ __forceinline__ uint32_t ext_bytes(uint32_t n) { return (n + 240u) / 255u; }
+// v_ffbl_b32 / v_ffbh_u32 with the hardware's answer for 0 (all ones), so a chain of
+// first-mismatch tests is a min over saturating adds instead of compare + select per dword.
+__device__ __forceinline__ uint32_t ffbl_hw(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ uint32_t ffbh_hw(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+// Bytes equal after the first 4 of a match: first differing byte of the kNQ dword pairs
+// (d[j] = XOR of dword j + 1), 4 + 4j + byte; kFwd + a lot when all are equal.
+template <int N>
+__device__ __forceinline__ uint32_t fwd_len(const uint32_t (&d)[N]) {
+    uint32_t m = ffbl_hw(d[0]);
+#pragma unroll
+    for (int j = 1; j < N; ++j) m = umin32(m, __builtin_elementwise_add_sat(ffbl_hw(d[j]), 32u * (uint32_t)j));
+    return (m >> 3) + 4u;
+}
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
 __device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t l) {
     return (uint64_t)rdl((uint32_t)v, l) | ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32);
@@ -1607,17 +1628,12 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
 #pragma unroll
             for (int j = 0; j < kNQ; ++j) Q[j + 1] = __builtin_amdgcn_alignbyte(O[j + 1], O[j], sh);
             const uint32_t maxf = end_lim - P;  // >= 4 for P <= smax
-            uint32_t lt = kFwd + 1u;
+            uint32_t dtt[kNQ];
 #pragma unroll
-            for (int j = kNQ - 1; j >= 0; --j) {
-                const uint32_t dt = Q[j + 1] ^ __builtin_amdgcn_alignbyte(T[j + 3], T[j + 2], ts);
-                lt = dt ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dt) >> 3) : lt;
-            }
-            lt = lt > kFwd ? kFwd : lt;
-            lt = lt > maxf ? maxf : lt;
+            for (int j = 0; j < kNQ; ++j) dtt[j] = Q[j + 1] ^ __builtin_amdgcn_alignbyte(T[j + 3], T[j + 2], ts);
+            uint32_t lt = umin32(umin32(fwd_len(dtt), kFwd), maxf);
             const uint32_t bt = vm4 ^ __builtin_amdgcn_alignbyte(T[1], T[0], ts);
-            uint32_t nbt = bt ? (uint32_t)__builtin_clz(bt) >> 3 : 4u;
-            nbt = nbt > ct ? ct : nbt;                      // ct < i
+            const uint32_t nbt = umin32(umin32(ffbh_hw(bt) >> 3, 4u), ct);  // ct < i
             const bool gt = valid & tin & (__builtin_amdgcn_alignbyte(T[2], T[1], ts) == v);
             uint32_t len = lt, nb = nbt, dist = i - ct;
             bool gf = false;
@@ -1631,17 +1647,12 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
                 const uint32_t df = (e1 & (i >= 1)) ? 1u : ((e2 & (i >= 2)) ? 2u : ((e3 & (i >= 3)) ? 3u : ((e4 & (i >= 4)) ? 4u : 0u)));
                 gf = want_short & (df != 0);
                 const uint32_t fs = (4u - df) & 3u;
-                uint32_t lf = kFwd + 1u;
+                uint32_t dff[kNQ];
 #pragma unroll
-                for (int j = kNQ - 1; j >= 0; --j) {
-                    const uint32_t dfw = Q[j + 1] ^ __builtin_amdgcn_alignbyte(Q[j + 1], Q[j], fs);
-                    lf = dfw ? 4u + 4u * j + ((uint32_t)__builtin_ctz(dfw) >> 3) : lf;
-                }
-                lf = lf > kFwd ? kFwd : lf;
-                lf = lf > maxf ? maxf : lf;
+                for (int j = 0; j < kNQ; ++j) dff[j] = Q[j + 1] ^ __builtin_amdgcn_alignbyte(Q[j + 1], Q[j], fs);
+                const uint32_t lf = umin32(umin32(fwd_len(dff), kFwd), maxf);
                 const uint32_t bf = vm4 ^ __builtin_amdgcn_alignbyte(vm4, vm8[q], fs);
-                uint32_t nbf = bf ? (uint32_t)__builtin_clz(bf) >> 3 : 4u;
-                nbf = nbf > i - df ? i - df : nbf;
+                const uint32_t nbf = umin32(umin32(ffbh_hw(bf) >> 3, 4u), i - df);
                 const bool ut = gt & (!gf | (lt >= lf));
                 len = ut ? lt : lf;
                 nb = ut ? nbt : nbf;
