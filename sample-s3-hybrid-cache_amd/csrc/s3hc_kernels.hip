@@ -2190,7 +2190,7 @@ hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock*
                                hipStream_t st) {
     if (!nunits) return hipSuccess;
     // S3HC_DEC_ONEWAVE=1 (comparisons): one wave per unit doing both halves (k_decode_units)
-    static const bool onewave = getenv("S3HC_DEC_ONEWAVE") != nullptr;
+    const bool onewave = getenv("S3HC_DEC_ONEWAVE") != nullptr;  // read per launch (tests toggle it)
     if (onewave)
         hipLaunchKernelGGL(k_decode_units, dim3(cdiv(nunits, dec::kWaves)), dim3(64 * dec::kWaves), 0, st, src, dst,
                            blk, units, nunits, blk_out, blk_status, unit_lb);
