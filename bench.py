@@ -197,7 +197,7 @@ def cpu_baseline(data_chunk: bytes, block: int, seconds: float):
 # decode: the parser + executor kernel (k_decode_pe); S3HC_DEC_ONEWAVE=1 selects the one-wave kernel
 KERNEL_SYMBOL = {"enc_parse": "k_enc_parse", "enc_emit": "k_enc_emit",
                  "decode": "k_decode_units" if os.environ.get("S3HC_DEC_ONEWAVE") else "k_decode_pe",
-                 "xxh32": "k_xxh32_ranges"}
+                 "dec_close": "k_dframe_close"}
 
 
 def pmc_traffic(kernel):
@@ -325,7 +325,7 @@ def run_rank(args):
         "enc_parse": nb * block,                  # U read once (match finding)
         "enc_emit": nb * block + comp_bytes,      # U literals read + C framed bytes written
         "decode": comp_bytes + nb * block,        # C read + U written
-        "xxh32": nb * block,                      # U read (decode-side verify)
+        "dec_close": nb * block,                  # U read (content xxh32 of every frame)
     }
     dom = max(excl, key=lambda k: excl[k][0]) if excl else None
     prof = nb == 4096 and not args.total_blocks

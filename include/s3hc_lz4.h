@@ -99,11 +99,16 @@ void s3hc_stream_close(s3hc_stream* s);
 
 /* ---- pipelined range reader (stream_range_data for throughput, config 4) --- */
 /* Complete frames are grouped into device batches of about batch_bytes compressed bytes that
- * run on `depth` HIP queues (pinned H2D, device frame walk + decode + checksum verify, D2H), so
- * batches overlap; decoded bytes come back in stream order. Same semantics as s3hc_stream; the
- * first failing frame ends the stream after the bytes of every earlier frame. */
+ * run on `depth` HIP queues (pinned H2D of input + host-walked frame tables, decode, one
+ * frame-close launch = lengths + content xxh32 + EndMark checks, D2H), so batches overlap;
+ * decoded bytes come back in stream order. Same semantics as s3hc_stream; the first failing
+ * frame ends the stream after the bytes of every earlier frame.
+ * s3hc_reader_set_batch_max (optional, default = batch_bytes): while earlier batches are still
+ * in flight, a new batch may take buffered frames up to max_bytes (the first batch after an idle
+ * pipeline stays at batch_bytes, so time to first byte is unchanged). */
 typedef struct s3hc_reader s3hc_reader;
 int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3hc_reader** out);
+int s3hc_reader_set_batch_max(s3hc_reader* r, size_t max_bytes);
 int s3hc_reader_feed(s3hc_reader* r, const uint8_t* src, size_t n);
 int s3hc_reader_finish(s3hc_reader* r);
 int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t* n);

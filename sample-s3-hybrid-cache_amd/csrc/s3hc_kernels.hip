@@ -168,17 +168,11 @@ __device__ __forceinline__ uint32_t xround(uint32_t acc, uint32_t in) {
     return acc * XP1;
 }
 
-// out[r] = xxh32(base + off[r], len[r], seed 0). Lanes 4r..4r+3 run the 4 accumulator chains
-// (gid = global thread index of the calling grid's xxh32 threads).
+// xxh32 of [p, p + L) by the 4 lanes 4k..4k+3 of a wave (a = lane & 3 picks the accumulator);
+// every lane calls (shuffles), the result is valid in lane a == 0 of an active group.
 template <uint32_t kIF, bool kPipe>  // loads per batch (VGPRs: the match finder's copy uses fewer)
-__device__ __forceinline__ void xxh32_ranges_dev(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
-                                                 const uint32_t* __restrict__ len, uint32_t n,
-                                                 uint32_t* __restrict__ out, uint32_t gid) {
-    const uint32_t r = gid >> 2, a = gid & 3;
+__device__ __forceinline__ uint32_t xxh32_lanes(const uint8_t* __restrict__ p, uint32_t L, bool act, uint32_t a) {
     const int lane = lane_id();
-    const bool act = r < n;
-    const uint32_t L = act ? len[r] : 0u;
-    const uint8_t* p = base + (act ? off[r] : 0);
     const uint32_t ns = L >> 4;
     uint32_t acc = a == 0 ? XP1 + XP2 : (a == 1 ? XP2 : (a == 2 ? 0u : 0u - XP1));
     const uint8_t* q = p + 4 * a;
@@ -224,7 +218,7 @@ __device__ __forceinline__ void xxh32_ranges_dev(const uint8_t* __restrict__ bas
     }
     const int qb = lane & ~3;
     uint32_t v1 = __shfl(acc, qb), v2 = __shfl(acc, qb + 1), v3 = __shfl(acc, qb + 2), v4 = __shfl(acc, qb + 3);
-    if (!act || a != 0) return;
+    if (!act || a != 0) return 0u;
     uint32_t h = L >= 16 ? rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18) : XP5;
     h += L;
     uint32_t t = ns * 16;
@@ -243,7 +237,20 @@ __device__ __forceinline__ void xxh32_ranges_dev(const uint8_t* __restrict__ bas
     h ^= h >> 13;
     h *= XP3;
     h ^= h >> 16;
-    out[r] = h;
+    return h;
+}
+
+// out[r] = xxh32(base + off[r], len[r], seed 0). Lanes 4r..4r+3 run the 4 accumulator chains
+// (gid = global thread index of the calling grid's xxh32 threads).
+template <uint32_t kIF, bool kPipe>
+__device__ __forceinline__ void xxh32_ranges_dev(const uint8_t* __restrict__ base, const uint64_t* __restrict__ off,
+                                                 const uint32_t* __restrict__ len, uint32_t n,
+                                                 uint32_t* __restrict__ out, uint32_t gid) {
+    const uint32_t r = gid >> 2, a = gid & 3;
+    const bool act = r < n;
+    const uint32_t L = act ? len[r] : 0u;
+    const uint32_t h = xxh32_lanes<kIF, kPipe>(base + (act ? off[r] : 0), L, act, a);
+    if (act && a == 0) out[r] = h;
 }
 __global__ __launch_bounds__(64) void k_xxh32_ranges(const uint8_t* __restrict__ base,
                                                       const uint64_t* __restrict__ off,
@@ -2167,8 +2174,52 @@ __global__ void k_dframe_verify(const uint8_t* __restrict__ src, const uint64_t*
     if (fstatus[f] != S3HC_OK) return;
     const uint8_t* fp = src + frame_off[f];
     const uint32_t flg = fp[4];
-    if ((flg & 0x08) && rd32(fp + 6) != out_len[f]) { fstatus[f] = S3HC_CORRUPT; return; }
+    if ((flg & 0x08) && (rd32(fp + 6) | ((uint64_t)rd32(fp + 10) << 32)) != out_len[f]) {
+        fstatus[f] = S3HC_CORRUPT;
+        return;
+    }
     if ((flg & 0x04) && got_hash[f] != fwant[f]) fstatus[f] = S3HC_CHECKSUM;
+}
+
+// k_dframe_finish + k_xxh32_ranges + k_dframe_verify in one launch (same rules, same results):
+// lanes 4f..4f+3 own frame f; each sums the frame's block results (frames hold few blocks), the
+// four hash the frame's output, lane 4f checks the EndMark. fstat_in: statuses set before the
+// decode (nullptr: none).
+__global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__ src, const uint64_t* __restrict__ frame_off,
+                                                     const uint64_t* __restrict__ blk_base, const uint32_t* __restrict__ nblk,
+                                                     const DecBlock* __restrict__ blocks, const uint32_t* __restrict__ blk_out,
+                                                     const int32_t* __restrict__ blk_status, const uint8_t* __restrict__ out,
+                                                     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ fwant,
+                                                     uint32_t n, const int32_t* fstat_in, int32_t* fstatus,
+                                                     uint32_t* __restrict__ out_len) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, f = gid >> 2, a = gid & 3;
+    const bool act = f < n;
+    int st = S3HC_OK;
+    uint64_t tot = 0;
+    if (act) {
+        st = fstat_in ? fstat_in[f] : S3HC_OK;
+        if (st == S3HC_OK) {
+            const uint32_t b0 = (uint32_t)blk_base[f], nb = nblk[f];
+            for (uint32_t k = 0; k < nb; ++k) {
+                const int bs = blk_status[b0 + k];
+                if (bs != S3HC_OK) { st = bs; break; }
+                const DecBlock D = blocks[b0 + k];
+                if (!(D.flags & DB_LINKED) && k + 1 < nb && blk_out[b0 + k] != D.limit) { st = S3HC_UNSUPPORTED; break; }
+                tot += blk_out[b0 + k];
+            }
+        }
+    }
+    const uint32_t L = st == S3HC_OK ? (uint32_t)tot : 0u;
+    const uint32_t h = xxh32_lanes<32, true>(out + (act ? out_off[f] : 0), L, act, a);
+    if (!act || a != 0) return;
+    out_len[f] = L;
+    if (st == S3HC_OK) {
+        const uint8_t* fp = src + frame_off[f];
+        const uint32_t flg = fp[4];
+        if ((flg & 0x08) && (rd32(fp + 6) | ((uint64_t)rd32(fp + 10) << 32)) != L) st = S3HC_CORRUPT;
+        else if ((flg & 0x04) && h != fwant[f]) st = S3HC_CHECKSUM;
+    }
+    fstatus[f] = st;
 }
 
 }  // namespace s3hc
@@ -2258,6 +2309,16 @@ hipError_t launch_dframe_finish(const uint64_t* blk_base, uint32_t n, const uint
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_dframe_finish, dim3(cdiv(n, 256)), dim3(256), 0, st, blk_base, n, nblk, blocks, blk_out,
                        blk_status, fstatus, out_len);
+    return hipGetLastError();
+}
+hipError_t launch_dframe_close(const uint8_t* src, const uint64_t* frame_off, const uint64_t* blk_base,
+                               const uint32_t* nblk, const DecBlock* blocks, const uint32_t* blk_out,
+                               const int32_t* blk_status, const uint8_t* out, const uint64_t* out_off,
+                               const uint32_t* fwant, uint32_t n, const int32_t* fstat_in, int32_t* fstatus,
+                               uint32_t* out_len, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_dframe_close, dim3(cdiv((uint64_t)n * 4, 64)), dim3(64), 0, st, src, frame_off, blk_base, nblk,
+                       blocks, blk_out, blk_status, out, out_off, fwant, n, fstat_in, fstatus, out_len);
     return hipGetLastError();
 }
 hipError_t launch_dframe_verify(const uint8_t* src, const uint64_t* frame_off, uint32_t n, const uint32_t* fwant,

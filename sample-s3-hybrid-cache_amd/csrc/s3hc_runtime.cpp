@@ -53,6 +53,9 @@ hipError_t launch_dframe_finish(const uint64_t*, uint32_t, const uint32_t*, cons
                                 const int32_t*, int32_t*, uint32_t*, hipStream_t);
 hipError_t launch_dframe_verify(const uint8_t*, const uint64_t*, uint32_t, const uint32_t*, const uint32_t*,
                                 const uint32_t*, int32_t*, hipStream_t);
+hipError_t launch_dframe_close(const uint8_t*, const uint64_t*, const uint64_t*, const uint32_t*, const DecBlock*,
+                               const uint32_t*, const int32_t*, const uint8_t*, const uint64_t*, const uint32_t*,
+                               uint32_t, const int32_t*, int32_t*, uint32_t*, hipStream_t);
 }  // namespace s3hc
 
 using namespace s3hc;
@@ -127,6 +130,211 @@ template <class T> static hipError_t upload(DevBuf& b, const std::vector<T>& v, 
     if (e != hipSuccess || v.empty()) return e;
     return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st);
 }
+
+// ------------------------------------------------------------ pinned host memory
+struct PinnedBuf {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
+        const size_t want = std::max<size_t>(n, 1 << 16);
+        hipError_t e = hipHostMalloc((void**)&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+};
+
+// Host copy of a large staging buffer split over a few threads (one thread copies ~6-10 GB/s;
+// the reader's feed/stage/deliver copies are otherwise the bottleneck of the pipeline).
+// Host copies of the range reader and the batch paths: split over a small persistent pool of
+// copy threads (no thread start-up per call). The calling thread copies too and helps with
+// queued pieces while it waits, so concurrent callers never block each other.
+namespace {
+class CopyPool {
+  public:
+    struct State {
+        std::atomic<int> left{0};
+    };
+    struct Job {
+        uint8_t* d;
+        const uint8_t* s;
+        size_t n;
+        State* st;
+    };
+    explicit CopyPool(unsigned nt) {
+        for (unsigned i = 0; i < nt; ++i) th_.emplace_back([this] { run(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    unsigned threads() const { return (unsigned)th_.size(); }
+    void copy(uint8_t* d, const uint8_t* s, size_t n, size_t parts) {
+        const size_t per = ((n + parts - 1) / parts + 63) & ~(size_t)63;
+        State st;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (size_t o = per; o < n; o += per) {
+                q_.push_back(Job{d + o, s + o, std::min(per, n - o), &st});
+                st.left.fetch_add(1, std::memory_order_relaxed);
+            }
+        }
+        cv_.notify_all();
+        memcpy(d, s, std::min(per, n));
+        while (st.left.load(std::memory_order_acquire) > 0) {
+            Job j{};
+            bool have = false;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (!q_.empty()) {
+                    j = q_.back();
+                    q_.pop_back();
+                    have = true;
+                }
+            }
+            if (have) do_job(j);
+            else std::this_thread::yield();
+        }
+    }
+
+  private:
+    static void do_job(const Job& j) {
+        memcpy(j.d, j.s, j.n);
+        j.st->left.fetch_sub(1, std::memory_order_release);
+    }
+    void run() {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                j = q_.back();
+                q_.pop_back();
+            }
+            do_job(j);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<Job> q_;
+    bool stop_ = false;
+};
+CopyPool& copy_pool() {
+    static CopyPool p(std::max(1u, std::min(7u, std::thread::hardware_concurrency() / 2)));
+    return p;
+}
+}  // namespace
+
+static void par_memcpy(void* dst, const void* src, size_t n) {
+    constexpr size_t kPiece = 128u << 10;
+    CopyPool& P = copy_pool();
+    const size_t parts = std::min<size_t>(P.threads() + 1, n / kPiece);
+    if (parts < 2) {
+        memcpy(dst, src, n);
+        return;
+    }
+    P.copy((uint8_t*)dst, (const uint8_t*)src, n, parts);
+}
+
+// Host <-> device copies of the host-buffer calls. A hipMemcpyAsync on pageable memory costs
+// ~0.13 ms per call on this platform whatever its size (measured: 16 x 64 KiB D2H = 2.2 ms of a
+// 2.6 ms 1 MiB decompress), so pageable caller buffers go through two pinned chunks: the DMA of
+// one chunk overlaps the (multi-threaded) host copy of the other. Pinned caller buffers are
+// copied directly.
+static bool host_pinned(const void* p) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error: clear it
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+// outputs up to this size come back in the readback round trip (no second synchronisation)
+static constexpr uint64_t kSpecBytes = 8u << 20;
+struct HostStage {
+    static constexpr size_t kChunk = 8u << 20;
+    PinnedBuf buf[2];
+    PinnedBuf small;  // per-block / per-frame results read back in one copy
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    ~HostStage() {
+        for (auto e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+    hipError_t init(size_t n) {
+        hipError_t e = hipSuccess;
+        for (int b = 0; b < 2; ++b) {
+            if (!ev[b] && (e = hipEventCreateWithFlags(&ev[b], hipEventDisableTiming)) != hipSuccess) return e;
+            if ((e = buf[b].ensure(std::min(n, kChunk))) != hipSuccess) return e;
+        }
+        return e;
+    }
+    // host src -> device dst (stream ordered; returns once src may be reused)
+    hipError_t h2d(void* dst, const void* src, size_t n, hipStream_t st) {
+        if (!n) return hipSuccess;
+        if (host_pinned(src)) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
+        hipError_t e = init(n);
+        if (e != hipSuccess) return e;
+        int b = 0;
+        for (size_t o = 0; o < n; o += kChunk, b ^= 1) {
+            const size_t k = std::min(kChunk, n - o);
+            if ((e = hipEventSynchronize(ev[b])) != hipSuccess) return e;  // chunk b's last DMA is done
+            par_memcpy(buf[b].p, (const uint8_t*)src + o, k);
+            if ((e = hipMemcpyAsync((uint8_t*)dst + o, buf[b].p, k, hipMemcpyHostToDevice, st)) != hipSuccess) return e;
+            if ((e = hipEventRecord(ev[b], st)) != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    // device runs (in order) -> contiguous host dst; returns when dst holds every byte
+    hipError_t d2h(uint8_t* dst, const std::vector<std::pair<const uint8_t*, uint64_t>>& runs, hipStream_t st) {
+        uint64_t n = 0;
+        for (auto& r : runs) n += r.second;
+        if (!n) return hipSuccess;
+        hipError_t e;
+        if (host_pinned(dst)) {
+            uint64_t o = 0;
+            for (auto& r : runs) {
+                if (r.second && (e = hipMemcpyAsync(dst + o, r.first, r.second, hipMemcpyDeviceToHost, st)) != hipSuccess)
+                    return e;
+                o += r.second;
+            }
+            return hipStreamSynchronize(st);
+        }
+        if ((e = init(n)) != hipSuccess) return e;
+        size_t ri = 0, rpos = 0;  // next run byte to stage
+        int b = 0, pend = -1;
+        uint64_t pend_off = 0, pend_len = 0;
+        for (uint64_t o = 0; o < n; o += kChunk, b ^= 1) {
+            const uint64_t k = std::min<uint64_t>(kChunk, n - o);
+            for (uint64_t f = 0; f < k;) {  // the chunk's pieces of the runs
+                while (runs[ri].second == rpos) { ++ri; rpos = 0; }
+                const uint64_t take = std::min<uint64_t>(k - f, runs[ri].second - rpos);
+                if ((e = hipMemcpyAsync(buf[b].p + f, runs[ri].first + rpos, take, hipMemcpyDeviceToHost, st)) != hipSuccess)
+                    return e;
+                f += take;
+                rpos += take;
+            }
+            if ((e = hipEventRecord(ev[b], st)) != hipSuccess) return e;
+            if (pend >= 0) {
+                if ((e = hipEventSynchronize(ev[pend])) != hipSuccess) return e;
+                par_memcpy(dst + pend_off, buf[pend].p, pend_len);
+            }
+            pend = b;
+            pend_off = o;
+            pend_len = k;
+        }
+        if ((e = hipEventSynchronize(ev[pend])) != hipSuccess) return e;
+        par_memcpy(dst + pend_off, buf[pend].p, pend_len);
+        return hipSuccess;
+    }
+};
 
 // ------------------------------------------------- large-block decode scratch
 // Caps of the large-block path (s3hc_lb.hip) for one decode launch. They only size scratch:
@@ -229,6 +437,8 @@ struct s3hc_ctx {
     s3hc_plan* host_plan = nullptr;
     DevBuf d_blocks, d_units, d_blk_out, d_blk_status, d_rng_off, d_rng_len, d_hash;
     DevBuf d_c_soff, d_c_len, d_c_doff, d_c_hash, d_c_flen;  // compat encoder descriptors
+    DevBuf d_ftab, d_fstat, d_flen, d_fhash;                  // per-frame tables of decode_walk
+    HostStage hs;
     LbScratch lb;
     ~s3hc_ctx();
 };
@@ -580,16 +790,12 @@ extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src
         HIPCHK(decode_launch(&P->lb, d_src, d_dst, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(), P->blk_cap,
                              P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st));
         T.end();
-        T.begin("dec_finish");
-        HIPCHK(launch_dframe_finish(P->d_blk_base.as<uint64_t>(), n, P->d_nblk.as<uint32_t>(), P->d_dblocks.as<DecBlock>(),
-                                    P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), d_status, d_out_len, st));
-        T.end();
-        T.begin("xxh32");
-        HIPCHK(launch_xxh32(d_dst, P->d_dst_off.as<uint64_t>(), d_out_len, n, P->d_got.as<uint32_t>(), st));
-        T.end();
-        T.begin("dec_finish");
-        HIPCHK(launch_dframe_verify(d_src, P->d_frame_off.as<uint64_t>(), n, P->d_fwant.as<uint32_t>(),
-                                    P->d_got.as<uint32_t>(), d_out_len, d_status, st));
+        // frame results, content xxh32 and EndMark checks (one launch)
+        T.begin("dec_close");
+        HIPCHK(launch_dframe_close(d_src, P->d_frame_off.as<uint64_t>(), P->d_blk_base.as<uint64_t>(),
+                                   P->d_nblk.as<uint32_t>(), P->d_dblocks.as<DecBlock>(), P->d_blk_out.as<uint32_t>(),
+                                   P->d_blk_status.as<int32_t>(), d_dst, P->d_dst_off.as<uint64_t>(),
+                                   P->d_fwant.as<uint32_t>(), n, d_status, d_status, d_out_len, st));
         T.end();
         return S3HC_OK;
     });
@@ -622,16 +828,26 @@ static int host_encode(s3hc_ctx* ctx, const uint8_t* src, size_t n, int mode, in
     const size_t ni = P->item_blk0.size();
     HIPCHK(d_io.ensure(ni * 8));
     HIPCHK(d_il.ensure(ni * 4));
-    if (n) HIPCHK(hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
+    HostStage& hs = ctx->hs;
+    HIPCHK(hs.h2d(ctx->d_in.p, src, n, st));
     rc = run_encode(ctx, P, ctx->d_in.as<uint8_t>(), ctx->d_out.as<uint8_t>(), d_io.as<uint64_t>(),
                     d_il.as<uint32_t>(), st);
     if (rc) return rc;
+    HIPCHK(hs.small.ensure(16));
+    HIPCHK(hipMemcpyAsync(hs.small.p, P->d_total.p, 8, hipMemcpyDeviceToHost, st));
+    // small outputs come back in the same round trip (bound-sized copy into pinned staging)
+    const bool spec = P->dst_bound <= kSpecBytes && !host_pinned(dst);
+    if (spec) {
+        HIPCHK(hs.init(P->dst_bound));
+        HIPCHK(hs.buf[0].ensure(P->dst_bound + 16));
+        HIPCHK(hipMemcpyAsync(hs.buf[0].p, ctx->d_out.p, P->dst_bound, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
     uint64_t total = 0;
-    HIPCHK(hipMemcpyAsync(&total, P->d_total.p, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    memcpy(&total, hs.small.p, 8);
     if (total > cap) return fail(S3HC_DST_TOO_SMALL, "dst capacity below encoded size");
-    HIPCHK(hipMemcpyAsync(dst, ctx->d_out.p, total, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    if (spec) par_memcpy(dst, hs.buf[0].p, total);
+    else HIPCHK(hs.d2h(dst, {{ctx->d_out.as<uint8_t>(), total}}, st));
     *out_len = total;
     return S3HC_OK;
 }
@@ -690,18 +906,19 @@ static int host_compat(s3hc_ctx* ctx, const uint8_t* src, size_t n, uint8_t* dst
     HIPCHK(ctx->d_in.ensure(n + 64));
     HIPCHK(ctx->d_out.ensure(bound + 64));
     HIPCHK(ctx->d_c_flen.ensure(16));
-    if (n) HIPCHK(hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
+    HIPCHK(ctx->hs.h2d(ctx->d_in.p, src, n, st));
     const uint64_t so = 0, dof = 0;
     const uint32_t ln = (uint32_t)n;
     int rc = run_compat(ctx, ctx->d_in.as<uint8_t>(), &so, &ln, 1, ctx->d_out.as<uint8_t>(), &dof,
                         ctx->d_c_flen.as<uint32_t>(), st);
     if (rc) return rc;
+    HIPCHK(ctx->hs.small.ensure(16));
+    HIPCHK(hipMemcpyAsync(ctx->hs.small.p, ctx->d_c_flen.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
     uint32_t flen = 0;
-    HIPCHK(hipMemcpyAsync(&flen, ctx->d_c_flen.p, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    memcpy(&flen, ctx->hs.small.p, 4);
     if (flen > bound) return fail(S3HC_DEVICE, "compat frame longer than its bound");
-    HIPCHK(hipMemcpyAsync(dst, ctx->d_out.p, flen, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(ctx->hs.d2h(dst, {{ctx->d_out.as<uint8_t>(), flen}}, st));
     *out_len = flen;
     return S3HC_OK;
 }
@@ -868,18 +1085,29 @@ extern "C" int s3hc_decompressed_bound(const uint8_t* src, size_t n, size_t* bou
 // Decode the frames of W (already walked) from a host buffer; append decoded bytes to
 // `out` (host) in frame order. Applies the decompress_data loop rules unless stream_mode.
 // Returns the first error in frame order (or W.tail_status).
+//
+// One submission and one readback in the common case: decode, block checksums, each frame's
+// output length and content xxh32 over its device slots (k_dframe_finish + k_xxh32_ranges),
+// and — for outputs up to kSpecBytes — the decoded slots themselves into pinned staging; then
+// one synchronisation, the host resolves frames in order and copies the delivered bytes out.
+// Frames whose output is not contiguous on the device (a short non-final independent block)
+// take the second round trip below (device compaction, checksum, copy).
 static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bool stream_mode,
                        std::vector<uint8_t>* vout, uint8_t* dst, size_t cap, size_t* out_len,
                        bool upload_in = true, bool* stopped_out = nullptr) {
     hipStream_t st = ctx->stream;
+    HostStage& hs = ctx->hs;
     const size_t nb = W.blocks.size(), nf = W.frames.size();
-    std::vector<uint32_t> bo(nb), cs_got(nb);
-    std::vector<int32_t> bs(nb);
+    // readback layout (u32 words): bo[nb] bs[nb] cs_got[nb] flen[nf] fhash[nf]
+    const uint32_t* bo = nullptr;
+    const int32_t* bs = nullptr;
+    const uint32_t *cs_got = nullptr, *flen = nullptr, *fhash = nullptr;
+    bool spec = false;  // the decoded slots [0, slot_total) are in hs.buf[0]
     if (stopped_out) *stopped_out = false;
     if (nb) {
         if (upload_in) {
             HIPCHK(ctx->d_in.ensure(n + 64));
-            HIPCHK(hipMemcpyAsync(ctx->d_in.p, src, n, hipMemcpyHostToDevice, st));
+            HIPCHK(hs.h2d(ctx->d_in.p, src, n, st));
         }
         HIPCHK(ctx->d_out.ensure(W.slot_total + 64));
         std::vector<DecUnit> units;
@@ -912,11 +1140,48 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
             HIPCHK(ctx->d_hash.ensure(nb * 4));
             HIPCHK(launch_xxh32(ctx->d_in.as<uint8_t>(), ctx->d_rng_off.as<uint64_t>(), ctx->d_rng_len.as<uint32_t>(),
                                 (uint32_t)nb, ctx->d_hash.as<uint32_t>(), st));
-            HIPCHK(hipMemcpyAsync(cs_got.data(), ctx->d_hash.p, nb * 4, hipMemcpyDeviceToHost, st));
         }
-        HIPCHK(hipMemcpyAsync(bo.data(), ctx->d_blk_out.p, nb * 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(bs.data(), ctx->d_blk_status.p, nb * 4, hipMemcpyDeviceToHost, st));
+        // per-frame output length (blocks in order, contiguous slots) and content checksum
+        {
+            std::vector<uint64_t> ft(2 * nf + (nf + 1) / 2);
+            uint32_t* fnb = (uint32_t*)(ft.data() + 2 * nf);
+            for (size_t f = 0; f < nf; ++f) {
+                ft[f] = W.frames[f].blk0;
+                ft[nf + f] = W.frames[f].out_off;
+                fnb[f] = W.frames[f].nblk;
+            }
+            HIPCHK(upload(ctx->d_ftab, ft, st));
+            HIPCHK(ctx->d_fstat.ensure(nf * 4));
+            HIPCHK(ctx->d_flen.ensure(nf * 4));
+            HIPCHK(ctx->d_fhash.ensure(nf * 4));
+            HIPCHK(hipMemsetAsync(ctx->d_fstat.p, 0, nf * 4, st));
+            const uint64_t* d_ft = ctx->d_ftab.as<uint64_t>();
+            HIPCHK(launch_dframe_finish(d_ft, (uint32_t)nf, (const uint32_t*)(d_ft + 2 * nf), ctx->d_blocks.as<DecBlock>(),
+                                        ctx->d_blk_out.as<uint32_t>(), ctx->d_blk_status.as<int32_t>(),
+                                        ctx->d_fstat.as<int32_t>(), ctx->d_flen.as<uint32_t>(), st));
+            HIPCHK(launch_xxh32(ctx->d_out.as<uint8_t>(), d_ft + nf, ctx->d_flen.as<uint32_t>(), (uint32_t)nf,
+                                ctx->d_fhash.as<uint32_t>(), st));
+        }
+        HIPCHK(hs.small.ensure((3 * nb + 2 * nf) * 4 + 16));
+        uint32_t* rb = (uint32_t*)hs.small.p;
+        HIPCHK(hipMemcpyAsync(rb, ctx->d_blk_out.p, nb * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(rb + nb, ctx->d_blk_status.p, nb * 4, hipMemcpyDeviceToHost, st));
+        if (any_cs) HIPCHK(hipMemcpyAsync(rb + 2 * nb, ctx->d_hash.p, nb * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(rb + 3 * nb, ctx->d_flen.p, nf * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(rb + 3 * nb + nf, ctx->d_fhash.p, nf * 4, hipMemcpyDeviceToHost, st));
+        // small outputs: their slots come back in the same round trip (pageable destinations)
+        spec = W.slot_total <= kSpecBytes && (vout || !host_pinned(dst));
+        if (spec) {
+            HIPCHK(hs.init(W.slot_total));
+            HIPCHK(hs.buf[0].ensure(W.slot_total + 16));
+            HIPCHK(hipMemcpyAsync(hs.buf[0].p, ctx->d_out.p, W.slot_total, hipMemcpyDeviceToHost, st));
+        }
         HIPCHK(hipStreamSynchronize(st));
+        bo = rb;
+        bs = (const int32_t*)(rb + nb);
+        cs_got = rb + 2 * nb;
+        flen = rb + 3 * nb;
+        fhash = rb + 3 * nb + nf;
     }
     // Resolve frames in order (FrameDecoder reads frames sequentially): the first failure in
     // stream order wins — a block's checksum/decode error, then at its EndMark the frame's
@@ -956,6 +1221,7 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
     const uint8_t* dev_out = ctx->d_out.as<uint8_t>();
     std::vector<uint64_t> fpos(use_frames);
     if (need_compact) {
+        spec = false;
         HIPCHK(compact.ensure(total + 64));
         uint64_t o = 0;
         for (size_t f = 0; f < use_frames; ++f) {
@@ -976,38 +1242,40 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
     } else {
         for (size_t f = 0; f < use_frames; ++f) fpos[f] = W.frames[f].out_off;
     }
-    // EndMark checks of every delivered frame, in order: content size, content checksum (GPU xxh32)
+    // EndMark checks of every delivered frame, in order: content size, content checksum (GPU
+    // xxh32: the one already read back when the device hashed exactly the frame's bytes)
     {
         std::vector<uint64_t> ro;
         std::vector<uint32_t> rl;
         std::vector<size_t> which;
         for (size_t f = 0; f < use_frames; ++f) {
-            if (W.frames[f].flg & 0x04) {
-                // the checksum kernel takes 32-bit range lengths
-                if (fout[f] > 0xFFFFFFFFull) return fail(S3HC_UNSUPPORTED, "a frame that decodes to 4 GiB or more");
-                ro.push_back(fpos[f]);
-                rl.push_back((uint32_t)fout[f]);
-                which.push_back(f);
-            }
+            if (!(W.frames[f].flg & 0x04)) continue;
+            if (flen && !need_compact && flen[f] == fout[f]) continue;  // fhash[f] is the frame's checksum
+            // the checksum kernel takes 32-bit range lengths
+            if (fout[f] > 0xFFFFFFFFull) return fail(S3HC_UNSUPPORTED, "a frame that decodes to 4 GiB or more");
+            ro.push_back(fpos[f]);
+            rl.push_back((uint32_t)fout[f]);
+            which.push_back(f);
         }
-        std::vector<uint32_t> got(ro.size());
+        std::vector<uint32_t> got(nf, 0);
         if (!ro.empty()) {
             HIPCHK(upload(ctx->d_rng_off, ro, st));
             HIPCHK(upload(ctx->d_rng_len, rl, st));
             HIPCHK(ctx->d_hash.ensure(ro.size() * 4));
             HIPCHK(launch_xxh32(dev_out, ctx->d_rng_off.as<uint64_t>(), ctx->d_rng_len.as<uint32_t>(),
                                 (uint32_t)ro.size(), ctx->d_hash.as<uint32_t>(), st));
-            HIPCHK(hipMemcpyAsync(got.data(), ctx->d_hash.p, ro.size() * 4, hipMemcpyDeviceToHost, st));
+            std::vector<uint32_t> g(ro.size());
+            HIPCHK(hipMemcpyAsync(g.data(), ctx->d_hash.p, ro.size() * 4, hipMemcpyDeviceToHost, st));
             HIPCHK(hipStreamSynchronize(st));
+            for (size_t i = 0; i < which.size(); ++i) got[which[i]] = g[i];
         }
-        size_t wi = 0;
+        std::vector<bool> redo(nf, false);
+        for (size_t f : which) redo[f] = true;
         for (size_t f = 0; f < use_frames; ++f) {
             const HFrame& F = W.frames[f];
             if ((F.flg & 0x08) && fout[f] != F.content_size) return fail(S3HC_CORRUPT, "content size mismatch");
-            if (F.flg & 0x04) {
-                if (got[wi] != F.want) return fail(S3HC_CHECKSUM, "content checksum mismatch");
-                wi++;
-            }
+            if ((F.flg & 0x04) && (redo[f] ? got[f] : fhash[f]) != F.want)
+                return fail(S3HC_CHECKSUM, "content checksum mismatch");
         }
     }
     if (err_status != S3HC_OK) return fail(err_status, "frame decode failed");
@@ -1021,12 +1289,24 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         *out_len = total;
         return fail(S3HC_DST_TOO_SMALL, "dst capacity below decoded size");
     }
-    uint64_t o = 0;
+    // runs of adjacent frames' bytes (one copy each)
+    std::vector<std::pair<const uint8_t*, uint64_t>> runs;
+    std::vector<std::pair<uint64_t, uint64_t>> spans;  // (device offset, bytes)
     for (size_t f = 0; f < use_frames; ++f) {
-        if (fout[f]) HIPCHK(hipMemcpyAsync(hdst + o, dev_out + fpos[f], fout[f], hipMemcpyDeviceToHost, st));
-        o += fout[f];
+        if (!fout[f]) continue;
+        if (!spans.empty() && spans.back().first + spans.back().second == fpos[f]) spans.back().second += fout[f];
+        else spans.push_back({fpos[f], fout[f]});
     }
-    HIPCHK(hipStreamSynchronize(st));
+    if (spec) {
+        uint64_t o = 0;
+        for (auto& sp : spans) {
+            par_memcpy(hdst + o, hs.buf[0].p + sp.first, sp.second);
+            o += sp.second;
+        }
+    } else {
+        for (auto& sp : spans) runs.push_back({dev_out + sp.first, sp.second});
+        HIPCHK(hs.d2h(hdst, runs, st));
+    }
     if (out_len) *out_len = total;
     return S3HC_OK;
 }
@@ -1321,104 +1601,6 @@ extern "C" int s3hc_memcpy_async(s3hc_ctx* ctx, void* dst, const void* src, size
     });
 }
 
-// Host copy of a large staging buffer split over a few threads (one thread copies ~6-10 GB/s;
-// the reader's feed/stage/deliver copies are otherwise the bottleneck of the pipeline).
-// Host copies of the range reader and the batch paths: split over a small persistent pool of
-// copy threads (no thread start-up per call). The calling thread copies too and helps with
-// queued pieces while it waits, so concurrent callers never block each other.
-namespace {
-class CopyPool {
-  public:
-    struct State {
-        std::atomic<int> left{0};
-    };
-    struct Job {
-        uint8_t* d;
-        const uint8_t* s;
-        size_t n;
-        State* st;
-    };
-    explicit CopyPool(unsigned nt) {
-        for (unsigned i = 0; i < nt; ++i) th_.emplace_back([this] { run(); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-    unsigned threads() const { return (unsigned)th_.size(); }
-    void copy(uint8_t* d, const uint8_t* s, size_t n, size_t parts) {
-        const size_t per = ((n + parts - 1) / parts + 63) & ~(size_t)63;
-        State st;
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            for (size_t o = per; o < n; o += per) {
-                q_.push_back(Job{d + o, s + o, std::min(per, n - o), &st});
-                st.left.fetch_add(1, std::memory_order_relaxed);
-            }
-        }
-        cv_.notify_all();
-        memcpy(d, s, std::min(per, n));
-        while (st.left.load(std::memory_order_acquire) > 0) {
-            Job j{};
-            bool have = false;
-            {
-                std::lock_guard<std::mutex> g(mu_);
-                if (!q_.empty()) {
-                    j = q_.back();
-                    q_.pop_back();
-                    have = true;
-                }
-            }
-            if (have) do_job(j);
-            else std::this_thread::yield();
-        }
-    }
-
-  private:
-    static void do_job(const Job& j) {
-        memcpy(j.d, j.s, j.n);
-        j.st->left.fetch_sub(1, std::memory_order_release);
-    }
-    void run() {
-        for (;;) {
-            Job j;
-            {
-                std::unique_lock<std::mutex> g(mu_);
-                cv_.wait(g, [this] { return stop_ || !q_.empty(); });
-                if (stop_ && q_.empty()) return;
-                j = q_.back();
-                q_.pop_back();
-            }
-            do_job(j);
-        }
-    }
-    std::vector<std::thread> th_;
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::vector<Job> q_;
-    bool stop_ = false;
-};
-CopyPool& copy_pool() {
-    static CopyPool p(std::max(1u, std::min(7u, std::thread::hardware_concurrency() / 2)));
-    return p;
-}
-}  // namespace
-
-static void par_memcpy(void* dst, const void* src, size_t n) {
-    constexpr size_t kPiece = 128u << 10;
-    CopyPool& P = copy_pool();
-    const size_t parts = std::min<size_t>(P.threads() + 1, n / kPiece);
-    if (parts < 2) {
-        memcpy(dst, src, n);
-        return;
-    }
-    P.copy((uint8_t*)dst, (const uint8_t*)src, n, parts);
-}
-
 // ------------------------------------------- pipelined range reader (config 4)
 // stream_range_data (disk_cache.rs:3850-3935) for throughput. Complete frames are grouped into
 // device batches of about batch_bytes compressed bytes; each batch runs on one of `depth` HIP
@@ -1429,25 +1611,11 @@ static void par_memcpy(void* dst, const void* src, size_t n) {
 // bytes that never form a complete frame are CORRUPT at finish. The caller keeps the reference's
 // final size check (disk_cache.rs:3929-3934) against s3hc_reader_total.
 namespace {
-struct PinnedBuf {
-    uint8_t* p = nullptr;
-    size_t cap = 0;
-    ~PinnedBuf() { if (p) (void)hipHostFree(p); }
-    hipError_t ensure(size_t n) {
-        if (n <= cap) return hipSuccess;
-        if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
-        const size_t want = std::max<size_t>(n, 1 << 16);
-        hipError_t e = hipHostMalloc((void**)&p, want, hipHostMallocDefault);
-        if (e == hipSuccess) cap = want;
-        return e;
-    }
-};
 struct RSlot {
     hipStream_t st = nullptr;
     hipEvent_t ev = nullptr;
     PinnedBuf h_in, h_meta, h_res, h_out;
-    DevBuf d_in, d_out, d_meta, d_res, d_nblk, d_blk_base, d_fwant, d_got, d_total, d_dblocks, d_units, d_blk_out,
-        d_blk_status;
+    DevBuf d_in, d_out, d_meta, d_res, d_blk_out, d_blk_status;
     LbScratch lb;
     uint32_t n = 0;
     std::vector<uint64_t> dst_off;
@@ -1463,6 +1631,7 @@ struct RSlot {
 struct s3hc_reader {
     s3hc_ctx* ctx;
     size_t batch_bytes;
+    size_t batch_max;           // batch limit while earlier batches are in flight (>= batch_bytes)
     std::vector<RSlot> slots;
     std::vector<int> inflight;  // slot indices in stream order (head may be ready / being read)
     std::vector<uint8_t> in;    // buffered input; undecoded bytes start at in_head (a frame boundary)
@@ -1473,98 +1642,90 @@ struct s3hc_reader {
     uint64_t total = 0;
 };
 
-// Queue frames [0, nf) of W (all complete) as one batch on slot s.
+// Queue frames [0, nf) of W (all complete) as one batch on slot s. The host walk already knows
+// every frame and block, so its tables go up with the input (one copy) and the device runs the
+// block decode and one frame-close launch (lengths, content xxh32, EndMark checks).
 static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     const HFrame& F0 = W.frames[0];
-    const size_t end = nf < W.frames.size() ? W.frames[nf].pos : W.end;
+    const bool all = nf >= W.frames.size();
+    const size_t end = all ? W.end : W.frames[nf].pos;
     const size_t nin = end - F0.pos;
     const uint32_t n = (uint32_t)nf;
+    const uint32_t nbk = (all ? (uint32_t)W.blocks.size() : W.frames[nf].blk0) - F0.blk0;
+    const uint64_t slot = (all ? W.slot_total : W.frames[nf].out_off) - F0.out_off;
     S.n = n;
     S.dst_off.resize(n);
-    std::vector<uint64_t> fo(n);
-    std::vector<uint32_t> fl(n), dc(n);
-    uint64_t slot = 0, blk_cap = 0;
+    std::vector<DecUnit> units;
     for (uint32_t f = 0; f < n; ++f) {
         const HFrame& F = W.frames[f];
-        const size_t fe = f + 1 < W.frames.size() ? W.frames[f + 1].pos : W.end;
-        fo[f] = F.pos - F0.pos;
-        fl[f] = (uint32_t)(fe - F.pos);
-        const uint64_t cap = (uint64_t)std::max<uint32_t>(F.nblk, 1u) * F.bmax;  // device slot layout k * bmax
-        if (cap > 0xFFFFFFFFull) return fail(S3HC_UNSUPPORTED, "frame too large for one batch");
-        dc[f] = (uint32_t)cap;
-        S.dst_off[f] = slot;
-        slot += cap;
-        blk_cap += cap / 65536u + 2u;
+        const uint64_t fend = f + 1 < W.frames.size() ? W.frames[f + 1].out_off : W.slot_total;
+        if (fend - F.out_off > 0xFFFFFFFFull) return fail(S3HC_UNSUPPORTED, "frame too large for one batch");
+        S.dst_off[f] = F.out_off - F0.out_off;
+        if (!F.nblk) continue;
+        if (!(F.flg & 0x20)) units.push_back(DecUnit{F.blk0 - F0.blk0, F.nblk});
+        else for (uint32_t k = 0; k < F.nblk; ++k) units.push_back(DecUnit{F.blk0 - F0.blk0 + k, 1});
     }
+    const uint32_t nu = (uint32_t)units.size();
+    // meta: frame_off u64[n] | blk_base u64[n] | out_off u64[n] | nblk u32[n] | want u32[n] |
+    //       blocks DecBlock[nbk] | units DecUnit[nu]   (sections 16-byte aligned)
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t o_fo = 0, o_bb = al(8ull * n), o_oo = o_bb + al(8ull * n), o_nb = o_oo + al(8ull * n),
+                 o_w = o_nb + al(4ull * n), o_blk = o_w + al(4ull * n), o_u = o_blk + al(sizeof(DecBlock) * nbk),
+                 nmeta = o_u + al(sizeof(DecUnit) * nu);
+    HIPCHK(S.h_meta.ensure(nmeta));
+    uint8_t* m = S.h_meta.p;
+    for (uint32_t f = 0; f < n; ++f) {
+        const HFrame& F = W.frames[f];
+        ((uint64_t*)(m + o_fo))[f] = F.pos - F0.pos;
+        ((uint64_t*)(m + o_bb))[f] = F.blk0 - F0.blk0;
+        ((uint64_t*)(m + o_oo))[f] = S.dst_off[f];
+        ((uint32_t*)(m + o_nb))[f] = F.nblk;
+        ((uint32_t*)(m + o_w))[f] = F.want;
+    }
+    DecBlock* mb = (DecBlock*)(m + o_blk);
+    for (uint32_t k = 0; k < nbk; ++k) {
+        DecBlock D = W.blocks[F0.blk0 + k];
+        D.src_off -= F0.pos;
+        D.dst_off -= F0.out_off;
+        D.frame -= (uint32_t)(&F0 - W.frames.data());
+        mb[k] = D;
+    }
+    if (nu) memcpy(m + o_u, units.data(), sizeof(DecUnit) * nu);
     hipStream_t st = S.st;
     HIPCHK(S.h_in.ensure(nin));
     par_memcpy(S.h_in.p, r->in.data() + r->in_head + F0.pos, nin);
-    HIPCHK(S.h_meta.ensure(24ull * n));
-    uint8_t* m = S.h_meta.p;
-    memcpy(m, fo.data(), 8ull * n);
-    memcpy(m + 8ull * n, S.dst_off.data(), 8ull * n);
-    memcpy(m + 16ull * n, fl.data(), 4ull * n);
-    memcpy(m + 20ull * n, dc.data(), 4ull * n);
     HIPCHK(S.d_in.ensure(nin + 64));
     HIPCHK(S.d_out.ensure(slot + 64));
-    HIPCHK(S.d_meta.ensure(24ull * n + 64));
+    HIPCHK(S.d_meta.ensure(nmeta + 64));
     HIPCHK(S.d_res.ensure(8ull * n + 64));
-    HIPCHK(S.d_nblk.ensure(4ull * n + 16));
-    HIPCHK(S.d_blk_base.ensure(8ull * n + 16));
-    HIPCHK(S.d_fwant.ensure(4ull * n + 16));
-    HIPCHK(S.d_got.ensure(4ull * n + 16));
-    HIPCHK(S.d_total.ensure(16));
-    HIPCHK(S.d_dblocks.ensure(blk_cap * sizeof(DecBlock) + 16));
-    HIPCHK(S.d_units.ensure(blk_cap * sizeof(DecUnit) + 16));
-    HIPCHK(S.d_blk_out.ensure(blk_cap * 4 + 16));
-    HIPCHK(S.d_blk_status.ensure(blk_cap * 4 + 16));
+    HIPCHK(S.d_blk_out.ensure(4ull * nbk + 16));
+    HIPCHK(S.d_blk_status.ensure(4ull * nbk + 16));
     {
         // large blocks of the batch (the host walk knows every block)
         LbCaps lc;
-        uint32_t nb = 0;
-        for (uint32_t f = 0; f < n; ++f) nb += W.frames[f].nblk;
-        if (nb <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
-        for (uint32_t f = 0; f < n; ++f) {
-            const HFrame& F = W.frames[f];
-            for (uint32_t k = 0; k < F.nblk; ++k) {
-                const DecBlock& D = W.blocks[F.blk0 + k];
-                if (lb_candidate(D, (F.flg & 0x20) != 0, lc.min_limit)) lc.add_block(D.csize);
-            }
-        }
-        HIPCHK(S.lb.prepare((uint32_t)blk_cap, lc));
+        if (nbk <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
+        for (auto& U : units)
+            if (lb_candidate(mb[U.first], U.n == 1, lc.min_limit)) lc.add_block(mb[U.first].csize);
+        HIPCHK(S.lb.prepare(nu, lc));
     }
     HIPCHK(S.h_res.ensure(8ull * n));
     HIPCHK(hipMemcpyAsync(S.d_in.p, S.h_in.p, nin, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S.d_meta.p, S.h_meta.p, 24ull * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.d_meta.p, S.h_meta.p, nmeta, hipMemcpyHostToDevice, st));
     const uint8_t* src = S.d_in.as<uint8_t>();
-    uint8_t* dm = S.d_meta.as<uint8_t>();
-    const uint64_t* d_fo = (const uint64_t*)dm;
-    const uint64_t* d_do = (const uint64_t*)(dm + 8ull * n);
-    const uint32_t* d_fl = (const uint32_t*)(dm + 16ull * n);
-    const uint32_t* d_dc = (const uint32_t*)(dm + 20ull * n);
+    const uint8_t* dm = S.d_meta.as<uint8_t>();
+    const DecBlock* d_blk = (const DecBlock*)(dm + o_blk);
     uint32_t* d_olen = S.d_res.as<uint32_t>();
     int32_t* d_st = (int32_t*)(S.d_res.as<uint8_t>() + 4ull * n);
     KTimer T(r->ctx, st);
-    T.begin("dec_plan");
-    HIPCHK(launch_dframe_count(src, d_fo, d_fl, d_dc, n, S.d_nblk.as<uint32_t>(), d_st, st));
-    HIPCHK(launch_scan(S.d_nblk.as<uint32_t>(), n, S.d_blk_base.as<uint64_t>(), S.d_total.as<uint64_t>(), st));
-    HIPCHK(hipMemsetAsync(S.d_units.p, 0, blk_cap * sizeof(DecUnit), st));
-    HIPCHK(launch_dframe_fill(src, d_fo, d_fl, n, d_do, d_dc, S.d_blk_base.as<uint64_t>(), d_st,
-                              S.d_dblocks.as<DecBlock>(), S.d_units.as<DecUnit>(), S.d_fwant.as<uint32_t>(), st));
-    T.end();
     T.begin("decode");
-    HIPCHK(decode_launch(&S.lb, src, S.d_out.as<uint8_t>(), S.d_dblocks.as<DecBlock>(), S.d_units.as<DecUnit>(),
-                         (uint32_t)blk_cap, S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), st));
+    HIPCHK(decode_launch(&S.lb, src, S.d_out.as<uint8_t>(), d_blk, (const DecUnit*)(dm + o_u), nu,
+                         S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), st));
     T.end();
-    T.begin("dec_finish");
-    HIPCHK(launch_dframe_finish(S.d_blk_base.as<uint64_t>(), n, S.d_nblk.as<uint32_t>(), S.d_dblocks.as<DecBlock>(),
-                                S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), d_st, d_olen, st));
-    T.end();
-    T.begin("xxh32");
-    HIPCHK(launch_xxh32(S.d_out.as<uint8_t>(), d_do, d_olen, n, S.d_got.as<uint32_t>(), st));
-    T.end();
-    T.begin("dec_finish");
-    HIPCHK(launch_dframe_verify(src, d_fo, n, S.d_fwant.as<uint32_t>(), S.d_got.as<uint32_t>(), d_olen, d_st, st));
+    T.begin("dec_close");
+    HIPCHK(launch_dframe_close(src, (const uint64_t*)(dm + o_fo), (const uint64_t*)(dm + o_bb),
+                               (const uint32_t*)(dm + o_nb), d_blk, S.d_blk_out.as<uint32_t>(),
+                               S.d_blk_status.as<int32_t>(), S.d_out.as<uint8_t>(), (const uint64_t*)(dm + o_oo),
+                               (const uint32_t*)(dm + o_w), n, nullptr, d_st, d_olen, st));
     T.end();
     HIPCHK(hipMemcpyAsync(S.h_res.p, S.d_res.p, 8ull * n, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(S.ev, st));
@@ -1580,7 +1741,10 @@ static int reader_pump(s3hc_reader* r) {
         // walk only what one batch can use (a frame cut by the limit counts as incomplete);
         // the whole buffer only when no frame completes within it (frames larger than that)
         const size_t avail = r->in.size() - r->in_head;
-        const size_t lim = std::min(avail, r->batch_bytes + ((size_t)8 << 20));
+        // an idle pipeline starts with batch_bytes (time to first byte); behind running batches
+        // a batch may take up to batch_max of the buffered frames
+        const size_t want = r->inflight.empty() ? r->batch_bytes : r->batch_max;
+        const size_t lim = std::min(avail, want + ((size_t)8 << 20));
         HWalk W;
         walk_frames(r->in.data() + r->in_head, lim, W, true, false);
         size_t nf = W.frames.size();
@@ -1602,7 +1766,7 @@ static int reader_pump(s3hc_reader* r) {
         }
         // batch = frames up to batch_bytes of input (at least one)
         size_t k = 1;
-        while (k < nf && W.frames[k].pos - W.frames[0].pos < r->batch_bytes) ++k;
+        while (k < nf && W.frames[k].pos - W.frames[0].pos < want) ++k;
         if (k < nf || W.end - W.frames[0].pos >= r->batch_bytes || r->finished) {
             // full batch (or all that will ever come)
         } else if (!r->inflight.empty()) {
@@ -1699,6 +1863,7 @@ extern "C" int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3
         std::unique_ptr<s3hc_reader> r(new s3hc_reader);
         r->ctx = ctx;
         r->batch_bytes = batch_bytes;
+        r->batch_max = batch_bytes;
         r->slots.resize(depth);
         for (auto& S : r->slots) {
             HIPCHK(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
@@ -1706,6 +1871,13 @@ extern "C" int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3
             HIPCHK(hipEventCreateWithFlags(&S.ev2, hipEventDisableTiming));
         }
         *out = r.release();
+        return S3HC_OK;
+    });
+}
+extern "C" int s3hc_reader_set_batch_max(s3hc_reader* r, size_t max_bytes) {
+    return guarded([&]() -> int {
+        if (!r || max_bytes < r->batch_bytes) return fail(S3HC_INVALID_ARG, "bad arguments");
+        r->batch_max = max_bytes;
         return S3HC_OK;
     });
 }

@@ -110,6 +110,7 @@ def _load():
         "s3hc_queue_sync": (i32, [vp, vp]),
         "s3hc_memcpy_async": (i32, [vp, vp, vp, sz, i32, vp]),
         "s3hc_reader_open": (i32, [vp, sz, i32, ctypes.POINTER(vp)]),
+        "s3hc_reader_set_batch_max": (i32, [vp, sz]),
         "s3hc_reader_feed": (i32, [vp, u8p, sz]),
         "s3hc_reader_finish": (i32, [vp]),
         "s3hc_reader_read": (i32, [vp, u8p, sz, szp]),
@@ -256,7 +257,7 @@ class Engine:
         """{kernel name: (total ms, launches)} since the last reset."""
         _check(lib.s3hc_timing_collect(self.h))
         out = {}
-        for name in ("xxh32_side", "xxh32", "enc_parse", "enc_sizes", "enc_emit", "dec_plan", "decode", "dec_finish",
+        for name in ("xxh32_side", "xxh32", "enc_parse", "enc_sizes", "enc_emit", "dec_plan", "decode", "dec_finish", "dec_close",
                      "compat"):
             n = lib.s3hc_kernel_count(self.h, name.encode())
             if n:
@@ -498,12 +499,15 @@ class FrameStream:
 
 class RangeReader:
     """Pipelined stream_range_data: feed compressed bytes, read decoded bytes in stream order;
-    batches of ~batch_bytes run on `depth` HIP queues."""
+    batches of ~batch_bytes run on `depth` HIP queues. batch_max (optional): batches queued behind
+    running ones may take up to batch_max bytes of buffered frames (s3hc_reader_set_batch_max)."""
 
-    def __init__(self, eng: Engine, batch_bytes: int = 256 << 10, depth: int = 3):
+    def __init__(self, eng: Engine, batch_bytes: int = 256 << 10, depth: int = 3, batch_max: int | None = None):
         h = ctypes.c_void_p()
         _check(lib.s3hc_reader_open(eng.h, batch_bytes, depth, ctypes.byref(h)))
         self.h = h
+        if batch_max is not None:
+            _check(lib.s3hc_reader_set_batch_max(h, batch_max))
 
     def feed(self, data):
         p, keep = _ptr(data)

@@ -534,3 +534,37 @@ def test_decompress_with_algorithm_none_and_decoder_fault(engine):
     assert h.decompress_with_algorithm(raw, S.ALG_NONE) == raw  # the None arm never decodes
     h.debug_set_faults(0)
     assert h.decompress_with_algorithm(frame, S.ALG_LZ4) == raw
+
+
+def _short_block_frame(oracle, parts, checksum=True):
+    """An independent-block BD 64 KiB frame whose non-final blocks are SHORT (valid for
+    lz4_flex's FrameDecoder, never written by its encoder): each part is one compressed block."""
+    import struct
+    flg = 0x64 if checksum else 0x60
+    hdr = bytes([0x04, 0x22, 0x4D, 0x18, flg, 0x40])
+    hdr += bytes([(oracle.xxh32(hdr[4:6]) >> 8) & 0xFF])
+    body = b""
+    for p in parts:
+        blk = oracle.lz4flex_compress_block(p)
+        body += struct.pack("<I", len(blk)) + blk
+    tail = struct.pack("<I", 0) + (struct.pack("<I", oracle.xxh32(b"".join(parts))) if checksum else b"")
+    return hdr + body + tail
+
+
+@pytest.mark.parametrize("checksum", [True, False])
+def test_short_nonfinal_independent_blocks(engine, oracle, checksum):
+    """Host-buffer decode of short non-final independent blocks: the output slots are not
+    contiguous on the device, so decode_walk compacts them before the content checksum."""
+    parts = [synth.log_text(5000, 61), synth.log_text(65536, 62), synth.log_text(123, 63), synth.log_text(40_000, 64)]
+    f = _short_block_frame(oracle, parts, checksum)
+    want = b"".join(parts)
+    assert oracle.decompress_data(f) == want
+    assert engine.decompress_frames(f) == want
+    # the same frame between two ordinary frames (delivery order across compaction)
+    a, b = synth.log_text(70_000, 65), synth.log_text(3_000, 66)
+    blob = engine.compress_frame(a) + f + engine.compress_frame(b)
+    assert engine.decompress_frames(blob) == a + want + b
+    bad = bytearray(f)
+    if checksum:
+        bad[-1] ^= 1
+        assert engine.decompress_status(bytes(bad))[0] == oracle.decompress_status(bytes(bad))[0]

@@ -18,10 +18,10 @@ def _drain(r, out, cap=MiB):
         out += c
 
 
-def _run(engine, frames, piece, batch, depth=3, cap=MiB):
+def _run(engine, frames, piece, batch, depth=3, cap=MiB, batch_max=None):
     import s3hc_lz4 as S
 
-    r = S.RangeReader(engine, batch, depth)
+    r = S.RangeReader(engine, batch, depth, batch_max)
     out = bytearray()
     for i in range(0, len(frames), piece):
         r.feed(frames[i:i + piece])
@@ -31,20 +31,23 @@ def _run(engine, frames, piece, batch, depth=3, cap=MiB):
     return bytes(out), r
 
 
-@pytest.mark.parametrize("piece,batch,depth", [(1000, 256 << 10, 3), (65536, 256 << 10, 3), (3 * MiB, 64 << 10, 2),
-                                               (777_777, 4 * MiB, 4), (10 * MiB, 1, 1)])
-def test_reader_matches_oracle(engine, oracle, piece, batch, depth):
+@pytest.mark.parametrize("piece,batch,depth,batch_max", [(1000, 256 << 10, 3, None), (65536, 256 << 10, 3, None),
+                                                         (3 * MiB, 64 << 10, 2, None), (777_777, 4 * MiB, 4, None),
+                                                         (10 * MiB, 1, 1, None), (3 * MiB, 64 << 10, 3, 2 * MiB),
+                                                         (10 * MiB, 256 << 10, 2, 8 * MiB)])
+def test_reader_matches_oracle(engine, oracle, piece, batch, depth, batch_max):
     data = synth.log_text(5 * MiB + 321, 41)
     # mixed layouts: 64 KiB frames, a reference-style 1 MiB frame, a store-mode frame, an empty frame
     frames = (engine.compress_frame(data[:2 * MiB], 1) + engine.compress_frame(data[2 * MiB:3 * MiB]) +
               engine.compress_frame(b"") + oracle.store_mode_frame(data[3 * MiB:3 * MiB + 70_000]) +
               engine.compress_frame(data[3 * MiB + 70_000:], 1))
-    out, r = _run(engine, frames, piece, batch, depth)
+    out, r = _run(engine, frames, piece, batch, depth, batch_max=batch_max)
     assert out == data
     assert r.total == len(data)
 
 
-def test_reader_corrupt_frame_stops_after_earlier_frames(engine, oracle):
+@pytest.mark.parametrize("batch_max", [None, 8 * MiB])
+def test_reader_corrupt_frame_stops_after_earlier_frames(engine, oracle, batch_max):
     import s3hc_lz4 as S
 
     data = synth.log_text(16 * 65536, 42)
@@ -52,7 +55,7 @@ def test_reader_corrupt_frame_stops_after_earlier_frames(engine, oracle):
     bad = bytearray(fr[9])
     bad[-1] ^= 0x5A  # content checksum of frame 9
     frames = b"".join(fr[:9]) + bytes(bad) + b"".join(fr[10:])
-    r = S.RangeReader(engine, 3 * 65536, 3)
+    r = S.RangeReader(engine, 3 * 65536, 3, batch_max)
     r.feed(frames)
     r.finish()
     out = bytearray()
@@ -92,12 +95,13 @@ def test_reader_garbage_after_frames(engine):
 
 
 @pytest.mark.parametrize("policy", [1, 0])
-@pytest.mark.parametrize("batch", [256 << 10, 4 << 20, 64 << 20])
-def test_reader_large_object_4mib_feeds(engine, policy, batch):
+@pytest.mark.parametrize("batch,batch_max", [(256 << 10, None), (4 << 20, None), (64 << 20, None),
+                                             (256 << 10, 16 << 20)])
+def test_reader_large_object_4mib_feeds(engine, policy, batch, batch_max):
     # config-4 shape at 1/64 scale: 128 MiB object, 4 MiB file reads, 1 MiB chunk reads
     data = synth.log_text(128 * MiB, 45)
     item = 65536 if policy == 1 else MiB
     frames = b"".join(engine.compress_frame(data[i:i + item], 0) for i in range(0, len(data), item)) if policy == 0 \
         else engine.compress_frame(data, 1)
-    out, r = _run(engine, frames, 4 * MiB, batch, 3)
+    out, r = _run(engine, frames, 4 * MiB, batch, 3, batch_max=batch_max)
     assert len(out) == len(data) and out == data
