@@ -2184,22 +2184,27 @@ __global__ void k_dframe_verify(const uint8_t* __restrict__ src, const uint64_t*
 // k_dframe_finish + k_xxh32_ranges + k_dframe_verify in one launch (same rules, same results):
 // lanes 4f..4f+3 own frame f; each sums the frame's block results (frames hold few blocks), the
 // four hash the frame's output, lane 4f checks the EndMark. fstat_in: statuses set before the
-// decode (nullptr: none).
+// decode (nullptr: none). blk_hash (nullable): hashes the large-block path computed while
+// decoding (1 << 32 | xxh32 per block); a frame of one such block skips its own pass.
+// got_hash (nullable): each frame's content xxh32.
 __global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__ src, const uint64_t* __restrict__ frame_off,
                                                      const uint64_t* __restrict__ blk_base, const uint32_t* __restrict__ nblk,
                                                      const DecBlock* __restrict__ blocks, const uint32_t* __restrict__ blk_out,
-                                                     const int32_t* __restrict__ blk_status, const uint8_t* __restrict__ out,
+                                                     const int32_t* __restrict__ blk_status,
+                                                     const uint64_t* __restrict__ blk_hash, const uint8_t* __restrict__ out,
                                                      const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ fwant,
                                                      uint32_t n, const int32_t* fstat_in, int32_t* fstatus,
-                                                     uint32_t* __restrict__ out_len) {
+                                                     uint32_t* __restrict__ out_len, uint32_t* __restrict__ got_hash) {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, f = gid >> 2, a = gid & 3;
     const bool act = f < n;
     int st = S3HC_OK;
     uint64_t tot = 0;
+    uint64_t pre = 0;  // 1 << 32 | hash when the large-block path hashed the frame's only block
     if (act) {
         st = fstat_in ? fstat_in[f] : S3HC_OK;
         if (st == S3HC_OK) {
             const uint32_t b0 = (uint32_t)blk_base[f], nb = nblk[f];
+            if (blk_hash && nb == 1) pre = blk_hash[b0];
             for (uint32_t k = 0; k < nb; ++k) {
                 const int bs = blk_status[b0 + k];
                 if (bs != S3HC_OK) { st = bs; break; }
@@ -2210,9 +2215,12 @@ __global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__
         }
     }
     const uint32_t L = st == S3HC_OK ? (uint32_t)tot : 0u;
-    const uint32_t h = xxh32_lanes<32, true>(out + (act ? out_off[f] : 0), L, act, a);
+    const bool have = (pre >> 32) != 0;
+    uint32_t h = xxh32_lanes<32, true>(out + (act ? out_off[f] : 0), have ? 0u : L, act, a);
     if (!act || a != 0) return;
+    if (have) h = (uint32_t)pre;
     out_len[f] = L;
+    if (got_hash) got_hash[f] = h;
     if (st == S3HC_OK) {
         const uint8_t* fp = src + frame_off[f];
         const uint32_t flg = fp[4];
@@ -2313,12 +2321,13 @@ hipError_t launch_dframe_finish(const uint64_t* blk_base, uint32_t n, const uint
 }
 hipError_t launch_dframe_close(const uint8_t* src, const uint64_t* frame_off, const uint64_t* blk_base,
                                const uint32_t* nblk, const DecBlock* blocks, const uint32_t* blk_out,
-                               const int32_t* blk_status, const uint8_t* out, const uint64_t* out_off,
-                               const uint32_t* fwant, uint32_t n, const int32_t* fstat_in, int32_t* fstatus,
-                               uint32_t* out_len, hipStream_t st) {
+                               const int32_t* blk_status, const uint64_t* blk_hash, const uint8_t* out,
+                               const uint64_t* out_off, const uint32_t* fwant, uint32_t n, const int32_t* fstat_in,
+                               int32_t* fstatus, uint32_t* out_len, uint32_t* got_hash, hipStream_t st) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_dframe_close, dim3(cdiv((uint64_t)n * 4, 64)), dim3(64), 0, st, src, frame_off, blk_base, nblk,
-                       blocks, blk_out, blk_status, out, out_off, fwant, n, fstat_in, fstatus, out_len);
+                       blocks, blk_out, blk_status, blk_hash, out, out_off, fwant, n, fstat_in, fstatus, out_len,
+                       got_hash);
     return hipGetLastError();
 }
 hipError_t launch_dframe_verify(const uint8_t* src, const uint64_t* frame_off, uint32_t n, const uint32_t* fwant,

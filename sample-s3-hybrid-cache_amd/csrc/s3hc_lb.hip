@@ -49,8 +49,29 @@ constexpr uint32_t BAD = 0xFFFFFFFFu;          // next-token value: malformed to
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t INF = 0xFFFFFFFFu;
 constexpr uint32_t kLevels = 13;               // 2^13 > kLbChunk / 3 tokens in a chunk
-constexpr uint32_t kXT = 1024;                 // threads of an executing workgroup
+constexpr uint32_t kXT = 960;                  // decoding threads of an executing workgroup (15 waves)
+constexpr uint32_t kXWG = kXT + 64;            // + one hashing wave
 constexpr uint32_t kXPer = kLbStep / kXT;      // output bytes per executing thread per step (8)
+// stripes the hashing wave takes in each phase of a step, sized to what the decoding waves
+// spend there (measured phase lengths): one step needs kLbStep / 16 = 480
+#ifndef S3HC_LBH_CLASSIFY  // (diagnostic builds sweep these)
+#define S3HC_LBH_CLASSIFY 120
+#endif
+#ifndef S3HC_LBH_STORES
+#define S3HC_LBH_STORES 90
+#endif
+#ifndef S3HC_LBH_INSTALL
+#define S3HC_LBH_INSTALL 60
+#endif
+#ifndef S3HC_LBH_ROUND
+#define S3HC_LBH_ROUND 80
+#endif
+#ifndef S3HC_LBH_LAG  // the classify phase hashes only while the wave lags more than this (bytes)
+#define S3HC_LBH_LAG 0
+#endif
+constexpr uint32_t kHashClassify = S3HC_LBH_CLASSIFY, kHashStores = S3HC_LBH_STORES, kHashInstall = S3HC_LBH_INSTALL,
+                   kHashRound = S3HC_LBH_ROUND, kHashLag = S3HC_LBH_LAG;
+static_assert(kXPer * kXT == kLbStep, "step geometry");
 constexpr uint32_t kRing = 65536;              // recent output kept in LDS (match sources)
 constexpr uint32_t kMaxSeqS = kLbStep / 4 + 3; // sequences touching one step (all but the last have sl >= 4)
 constexpr uint32_t FIN = 0xFFFFFFFFu;          // source pointer of a final byte
@@ -221,6 +242,7 @@ __global__ __launch_bounds__(1024) void k_lb_classify(const DecBlock* __restrict
             if (U.n == 1) {
                 bi = U.first;
                 B = blk[bi];
+                A.blk_hash[bi] = 0;  // k_lb_run sets it for the blocks it decodes
                 cand = !(B.flags & (DB_STORED | DB_LINKED)) && B.limit >= A.min_limit && B.csize > 0 &&
                        B.limit <= kLbMaxSteps * kLbStep;
             }
@@ -550,13 +572,28 @@ __global__ void k_lb_fin(LbArgs A, uint32_t* __restrict__ blk_out, int32_t* __re
 }
 
 // ---------------------------------------------------------------- execute
-// One 1024-thread workgroup per block writes the block in kLbStep-byte steps, in order. LDS
-// keeps a 64 KiB ring of the block's recent output (match sources) and the step's sequences.
-// Each byte of a step gets its value right away when it is a literal or its match source lies
-// before the step (the ring still holds [R - 64 KiB, R) until the step stores its own bytes, and
-// LZ4 offsets are < 64 KiB); otherwise it gets a pointer to its source inside the step, and the
-// pointers are jumped (a final source gives the value) until every byte is final: every chain
-// ends in a literal or a byte before the step, so no byte is left over. Then the step is flushed.
+// One 1024-thread workgroup per block writes the block in kLbStep-byte steps, in order: 15
+// waves decode, the 16th hashes. LDS keeps a 64 KiB ring of the block's recent output (match
+// sources) and the step's sequences. Each byte of a step gets its value right away when it is a
+// literal or its match source lies before the step (the ring still holds [R - 64 KiB, R) until
+// the step stores its own bytes, and LZ4 offsets are < 64 KiB); otherwise it gets a pointer to
+// its source inside the step, and the pointers are jumped (a final source gives the value) until
+// every byte is final: every chain ends in a literal or a byte before the step, so no byte is
+// left over. Then the step is flushed.
+//
+// The hashing wave runs xxh32 (seed 0) over the block's output behind the decode: in each
+// barrier phase of a step it hashes a slice of the bytes finished by earlier steps (from the
+// LDS ring), sized to that phase's length, so its serial chain hides in the other waves' LDS
+// and memory phases; the tail and the final avalanche follow the last flush. The result goes to blk_hash[blk] (1 << 32 | hash): when the
+// block is its frame's only block this is the frame's content checksum, and k_dframe_close
+// skips its own serial pass over the frame (0.7 ms per MiB).
+namespace {
+constexpr uint32_t XH1 = 2654435761U, XH2 = 2246822519U, XH3 = 3266489917U, XH4 = 668265263U, XH5 = 374761393U;
+__device__ __forceinline__ uint32_t xh_rotl(uint32_t x, int r) { return __builtin_amdgcn_alignbit(x, x, 32 - r); }
+__device__ __forceinline__ uint32_t xh_round(uint32_t acc, uint32_t in) { return xh_rotl(acc + in * XH2, 13) * XH1; }
+typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+}  // namespace
+
 __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, LbArgs A) {
     using namespace lb;
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
@@ -575,6 +612,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
     const uint8_t* g = src + B.src_off;
     uint8_t* ob = dst + B.dst_off;
     const uint32_t t = threadIdx.x;
+    const bool dec = t < kXT;  // decoding thread (else: the hashing wave)
     const int lane = lane64();
     constexpr uint32_t kMask = kRing - 1;
     const uint32_t nsteps = (size + kLbStep - 1) / kLbStep;
@@ -588,8 +626,34 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
 #define LB_T(k)
 #define LB_ADD(k, v)
 #endif
+    // hashing wave state: lane a = lane & 3 runs accumulator a (every lane computes; lanes of a
+    // quad share addresses), hs = stripes hashed so far
+    const uint32_t ha = (uint32_t)lane & 3u;
+    uint32_t hacc = ha == 0 ? XH1 + XH2 : (ha == 1 ? XH2 : (ha == 2 ? 0u : 0u - XH1));
+    uint32_t hs = 0;
+    const uint32_t hns = size >> 4;
+    // hash stripes [hs, min(avail / 16, hs + budget)) of the finished output, read from the LDS
+    // ring (aligned dwords: ring slots are output positions mod 64 KiB; the hashing wave lags the
+    // decode by about one step, far less than the ring's 8)
+#ifdef S3HC_LB_NOHASH  // diagnostic builds: no hashing wave work (k_dframe_close hashes)
+#define LB_HASH(avail, budget)
+#else
+#define LB_HASH(avail, budget)                                                                  \
+    if (!dec) {                                                                                 \
+        uint32_t lim_ = (avail) >> 4;                                                           \
+        lim_ = lim_ < hns ? lim_ : hns;                                                         \
+        lim_ = lim_ < hs + (budget) ? lim_ : hs + (budget);                                     \
+        for (; hs + 16u <= lim_; hs += 16u) {                                                   \
+            uint32_t v_[16];                                                                    \
+            _Pragma("unroll") for (uint32_t k = 0; k < 16; ++k)                                 \
+                v_[k] = *(const uint32_t*)(ring + ((16u * (hs + k) + 4u * ha) & kMask));        \
+            _Pragma("unroll") for (uint32_t k = 0; k < 16; ++k) hacc = xh_round(hacc, v_[k]);   \
+        }                                                                                       \
+        for (; hs < lim_; ++hs) hacc = xh_round(hacc, *(const uint32_t*)(ring + ((16u * hs + 4u * ha) & kMask))); \
+    }
+#endif
     // step q covers sequences [rf[q], rf[q+1]) (+1 when the next step starts inside one)
-    for (uint32_t q = t; q <= nsteps; q += kXT)
+    for (uint32_t q = t; q <= nsteps; q += kXWG)
         rf[q] = q < nsteps ? A.rfirst[(size_t)i * kLbMaxSteps + q] : ntok;
     __syncthreads();
     // sequences of a step: loaded into registers one step ahead, stored (with the start marks)
@@ -603,7 +667,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
                             ? ((q) + 1 < nsteps ? rf[(q) + 1] + 1u : ntok) - s0      \
                             : kMaxSeqS;
 #define LB_PREFETCH(q)                                                                   \
-    {                                                                                    \
+    if (dec) {                                                                           \
         LB_STEP_SEQS(q, s0p, nsp)                                                        \
         const uint32_t j0 = t, j1 = t + kXT, j2 = t + 2 * kXT;                           \
         const uint32_t g0 = tok0 + s0p + (j0 < nsp ? j0 : 0u), g1 = tok0 + s0p + (j1 < nsp ? j1 : 0u); \
@@ -619,13 +683,13 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         if (rel_ < kLbStep && ((j) == 0 || (pe).x > (R))) marks[rel_] = (uint16_t)((j) + 1); \
     }
 #define LB_INSTALL(q)                                                                    \
-    {                                                                                    \
+    if (dec) {                                                                           \
         LB_STEP_SEQS(q, s0i, nsi)                                                        \
         const uint32_t Rq = (q) * kLbStep;                                               \
         (void)s0i;                                                                       \
         LB_PUT(t, pe0, po0, Rq) LB_PUT(t + kXT, pe1, po1, Rq) LB_PUT(t + 2 * kXT, pe2, po2, Rq) \
     }
-    ((uint4*)marks)[t] = make_uint4(0, 0, 0, 0);  // kLbStep u16 = kXT x 16 B
+    if (dec) ((uint4*)marks)[t] = make_uint4(0, 0, 0, 0);  // kLbStep u16 = kXT x 16 B
     LB_PREFETCH(0)
     __syncthreads();
     LB_INSTALL(0)
@@ -636,7 +700,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         LB_T(0);
         LB_ADD(7, 1);
         // owner of each byte: running max of the start marks (thread t: bytes 8t .. 8t+7)
-        const uint4 m4 = ((const uint4*)marks)[t];
+        const uint4 m4 = dec ? ((const uint4*)marks)[t] : make_uint4(0, 0, 0, 0);
         const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
         uint32_t mx = 0;
 #pragma unroll
@@ -656,7 +720,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         uint32_t cur = __shfl_up(inc, 1);
         if (lane == 0) cur = 0;
         for (uint32_t w = 0; w < (t >> 6); ++w) cur = shm[w] > cur ? shm[w] : cur;
-        {
+        if (dec) {
             // owners written over the marks (then read with the interleaved byte mapping)
             uint32_t ow[4];
 #pragma unroll
@@ -670,6 +734,9 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
             ((uint4*)marks)[t] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
         }
         __syncthreads();
+        // (a hashing wave more than 3 steps behind catches up here: the ring keeps 8)
+        LB_HASH(R, R - 16u * hs > 3u * kLbStep ? (R - 16u * hs - 2u * kLbStep) / 16u
+                                                : (R - 16u * hs > kHashLag ? kHashClassify : 0u))
         // classify the bytes (thread t: bytes t + kXT*j, so lanes touch consecutive bytes):
         // literal (input address), source before the step (ring value: the ring still holds
         // [R - 64 KiB, R) until this step's bytes are stored below, and LZ4 offsets are
@@ -685,7 +752,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
             pv[j] = FIN;
             la[j] = 0;
             vb[j] = 0;
-            if (x < size) {
+            if (dec && x < size) {
                 const uint32_t k = marks[l] - 1u;
                 const uint4 e = sq[k];
                 const uint32_t rel = x - e.x;
@@ -714,18 +781,22 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         for (uint32_t j = 0; j < kXPer; ++j) vb[j] = (litm >> j) & 1u ? lv[j] & 0xFFu : vb[j];
         LB_T(2);
         __syncthreads();  // every read of the ring slots this step overwrites, and of marks/sq, is done
+        if (dec) {
 #pragma unroll
-        for (uint32_t j = 0; j < kXPer; ++j) {
-            const uint32_t l = t + kXT * j;
-            ring[(R + l) & kMask] = (uint8_t)vb[j];
-            ptr[l] = pv[j];
+            for (uint32_t j = 0; j < kXPer; ++j) {
+                const uint32_t l = t + kXT * j;
+                ring[(R + l) & kMask] = (uint8_t)vb[j];
+                ptr[l] = pv[j];
+            }
+            ((uint4*)marks)[t] = make_uint4(0, 0, 0, 0);
         }
-        ((uint4*)marks)[t] = make_uint4(0, 0, 0, 0);
         if (t == 0) jflag[0] = 0u;
+        LB_HASH(R, kHashStores)
         __syncthreads();
         LB_T(3);
         if (q + 1 < nsteps) LB_INSTALL(q + 1)
         if (q + 2 < nsteps) LB_PREFETCH(q + 2)
+        LB_HASH(R, kHashInstall)
         LB_T(4);
         // chains inside the step: each round every pending byte reads its source's pointer; a
         // final source gives the value, a pending one is jumped over (pointer doubling). A
@@ -768,6 +839,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
                 if (pend) jflag[it % 3u] = 1u;
             }
             if (t == 0) jflag[(it + 1u) % 3u] = 0u;
+            LB_HASH(R, kHashRound)
 #ifdef S3HC_LBPROF
             lbp[11] += __builtin_amdgcn_s_memtime() - tb1;
 #endif
@@ -777,21 +849,46 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         }
         LB_T(5);
         // flush the step (thread t: dwords t and t + kXT of the step)
-        const bool al = (((uintptr_t)(ob + R)) & 3u) == 0;
+        if (dec) {
+            const bool al = (((uintptr_t)(ob + R)) & 3u) == 0;
 #pragma unroll
-        for (uint32_t h = 0; h < 2; ++h) {
-            const uint32_t x0 = R + 4u * (t + kXT * h);
-            const uint32_t v4 = *(const uint32_t*)(ring + (x0 & kMask));
-            if (al && x0 + 4u <= size) {
-                *(uint32_t*)(ob + x0) = v4;
-            } else {
+            for (uint32_t h = 0; h < 2; ++h) {
+                const uint32_t x0 = R + 4u * (t + kXT * h);
+                const uint32_t v4 = *(const uint32_t*)(ring + (x0 & kMask));
+                if (al && x0 + 4u <= size) {
+                    *(uint32_t*)(ob + x0) = v4;
+                } else {
 #pragma unroll
-                for (uint32_t j = 0; j < 4; ++j)
-                    if (x0 + j < size) ob[x0 + j] = (uint8_t)(v4 >> (8 * j));
+                    for (uint32_t j = 0; j < 4; ++j)
+                        if (x0 + j < size) ob[x0 + j] = (uint8_t)(v4 >> (8 * j));
+                }
             }
         }
         LB_T(6);
     }
+    // every step is flushed: the hashing wave finishes the stripes, the tail and the avalanche
+    __syncthreads();
+    LB_HASH(size, hns)
+#ifndef S3HC_LB_NOHASH
+    if (!dec) {
+        const int qb = lane & ~3;
+        const uint32_t v1 = __shfl(hacc, qb), v2 = __shfl(hacc, qb + 1), v3 = __shfl(hacc, qb + 2),
+                       v4 = __shfl(hacc, qb + 3);
+        if (lane == 0) {
+            uint32_t h = size >= 16 ? xh_rotl(v1, 1) + xh_rotl(v2, 7) + xh_rotl(v3, 12) + xh_rotl(v4, 18) : XH5;
+            h += size;
+            uint32_t p = hns * 16u;
+            for (; p + 4u <= size; p += 4u) h = xh_rotl(h + *(const u32_unaligned*)(ob + p) * XH3, 17) * XH4;
+            for (; p < size; ++p) h = xh_rotl(h + (uint32_t)ob[p] * XH5, 11) * XH1;
+            h ^= h >> 15;
+            h *= XH2;
+            h ^= h >> 13;
+            h *= XH3;
+            h ^= h >> 16;
+            A.blk_hash[B.blk] = (1ull << 32) | h;
+        }
+    }
+#endif
 #ifdef S3HC_LBPROF
     if (t == 0)
         for (int k = 0; k < 12; ++k) atomicAdd(&g_lbprof[k], (unsigned long long)lbp[k]);
@@ -800,6 +897,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
 
 #undef LB_T
 #undef LB_ADD
+#undef LB_HASH
 #undef LB_STEP_SEQS
 #undef LB_PREFETCH
 #undef LB_PUT
@@ -829,7 +927,7 @@ hipError_t launch_lb_parse(const LbArgs& A, const uint8_t* src, const DecBlock* 
 
 // Execute stage: one workgroup per taken block.
 hipError_t launch_lb_exec(const LbArgs& A, const uint8_t* src, uint8_t* dst, hipStream_t st) {
-    hipLaunchKernelGGL(k_lb_run, dim3(A.lb_cap), dim3(lb::kXT), 0, st, src, dst, A);
+    hipLaunchKernelGGL(k_lb_run, dim3(A.lb_cap), dim3(lb::kXWG), 0, st, src, dst, A);
     return hipGetLastError();
 }
 }  // namespace s3hc

@@ -89,11 +89,13 @@ struct DecUnit {         // a run of blocks decoded in order by one wave
 // reference's ~1 MiB cache batches) are decoded by a whole workgroup each instead of one wave:
 // the token chain is found by pointer doubling over 16 Ki-position chunks of the compressed
 // block (all chunks of all blocks in parallel), the sequence table comes from scans, and one
-// 1024-thread workgroup per block then writes the output in 8 KiB steps, resolving each step's
-// match chains in LDS by pointer jumping against a 64 KiB ring of recent output.
+// 1024-thread workgroup per block then writes the output in 7.5 KiB steps (15 waves, 8 bytes per
+// lane), resolving each step's match chains in LDS by pointer jumping against a 64 KiB ring of
+// recent output, while its 16th wave hashes the flushed output (the frame's content xxh32 when
+// the block is the whole frame).
 constexpr uint32_t kLbChunk = 16384;      // compressed positions per tokenizing workgroup
-constexpr uint32_t kLbStep = 8192;        // output bytes per step of the executing workgroup
-constexpr uint32_t kLbMaxSteps = 512;     // steps of one block (4 MiB / kLbStep)
+constexpr uint32_t kLbStep = 7680;        // output bytes per step of the executing workgroup
+constexpr uint32_t kLbMaxSteps = 547;     // steps of one block (ceil(4 MiB / kLbStep))
 constexpr uint32_t kLbMinLimit = 65537;   // frame max block size above 64 KiB selects the path
 constexpr uint32_t kLbFewBlocks = 256;    // batches with at most this many blocks: every compressed
                                           // independent block takes the path (latency: one wave per
@@ -142,6 +144,8 @@ struct LbArgs {
     uint32_t* lb_tok0;     // per LB block: global index of its first sequence
     uint32_t* lb_ntok;
     uint32_t* rfirst;      // per LB block x kLbMaxSteps: sequence covering each step's first byte
+    uint64_t* blk_hash;    // per DecBlock: 1 << 32 | xxh32 of its output (written by k_lb_run; cleared
+                           // by k_lb_classify for every single-block unit)
 };
 
 

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -54,8 +55,8 @@ hipError_t launch_dframe_finish(const uint64_t*, uint32_t, const uint32_t*, cons
 hipError_t launch_dframe_verify(const uint8_t*, const uint64_t*, uint32_t, const uint32_t*, const uint32_t*,
                                 const uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_dframe_close(const uint8_t*, const uint64_t*, const uint64_t*, const uint32_t*, const DecBlock*,
-                               const uint32_t*, const int32_t*, const uint8_t*, const uint64_t*, const uint32_t*,
-                               uint32_t, const int32_t*, int32_t*, uint32_t*, hipStream_t);
+                               const uint32_t*, const int32_t*, const uint64_t*, const uint8_t*, const uint64_t*,
+                               const uint32_t*, uint32_t, const int32_t*, int32_t*, uint32_t*, uint32_t*, hipStream_t);
 }  // namespace s3hc
 
 using namespace s3hc;
@@ -354,10 +355,11 @@ static bool lb_candidate(const DecBlock& D, bool unit_single, uint32_t min_limit
 
 struct LbScratch {
     DevBuf lbt, ctl, unit_lb, chunk_blk, nzg, E, J0, entry, bits, ntok, slsum, badrel, tokbase, outbase, total, seq4,
-        seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst;
+        seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst, blk_hash;
     LbArgs a{};
     bool active = false;
-    hipError_t prepare(uint32_t nunits, const LbCaps& c) {
+    // nunits: units of the launch; nblocks: its DecBlock count (block hashes are per DecBlock)
+    hipError_t prepare(uint32_t nunits, uint32_t nblocks, const LbCaps& c) {
         active = c.lb > 0 && c.chunks > 0;
         if (!active) return hipSuccess;
         const size_t nch = c.chunks, nlb = c.lb;
@@ -369,7 +371,7 @@ struct LbScratch {
         LBE(bits, nch * (kLbChunk / 32) * 4) LBE(ntok, nch * 4) LBE(slsum, nch * 4) LBE(badrel, nch * 4)
         LBE(tokbase, nch * 8) LBE(outbase, nch * 8) LBE(total, 32) LBE(seq4, nseq * 16) LBE(seqoff, nseq * 2)
         LBE(lb_err, nlb * 4) LBE(lb_size, nlb * 4) LBE(lb_stat, nlb * 4) LBE(lb_tok0, nlb * 4) LBE(lb_ntok, nlb * 4)
-        LBE(rfirst, nlb * kLbMaxSteps * 4)
+        LBE(rfirst, nlb * kLbMaxSteps * 4) LBE(blk_hash, (size_t)std::max(nunits, nblocks) * 8)
 #undef LBE
         a.lb_cap = c.lb;
         a.chunk_cap = c.chunks;
@@ -382,17 +384,20 @@ struct LbScratch {
         a.seqoff = seqoff.as<uint16_t>(); a.lb_err = lb_err.as<uint32_t>(); a.lb_size = lb_size.as<uint32_t>();
         a.lb_stat = lb_stat.as<uint32_t>(); a.lb_tok0 = lb_tok0.as<uint32_t>(); a.lb_ntok = lb_ntok.as<uint32_t>();
         a.rfirst = rfirst.as<uint32_t>();
+        a.blk_hash = blk_hash.as<uint64_t>();
         return hipSuccess;
     }
 };
 
 // Block decode of a batch: large blocks by the large-block path (when L is active), the rest
-// one wave per unit.
+// one wave per unit. *blk_hash: the large-block path's per-block output hashes (single-block
+// units: 1 << 32 | xxh32, or 0), nullptr when the path did not run.
 static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, const DecBlock* blk,
                                 const DecUnit* units, uint32_t nunits, uint32_t* blk_out, int32_t* blk_status,
-                                hipStream_t st) {
+                                hipStream_t st, const uint64_t** blk_hash = nullptr) {
     // S3HC_LB_DISABLE (tests, comparisons): every block goes to the one-wave decoder
     const bool lb = L && L->active && nunits && !getenv("S3HC_LB_DISABLE");
+    if (blk_hash) *blk_hash = lb ? L->a.blk_hash : nullptr;
     hipError_t e;
     if (lb && (e = launch_lb_parse(L->a, src, blk, units, nunits, blk_out, blk_status, st)) != hipSuccess) return e;
     if ((e = launch_decode_units(src, dst, blk, units, nunits, blk_out, blk_status, lb ? L->a.unit_lb : nullptr,
@@ -759,7 +764,7 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
                 lc.chunks += frame_len[i] / kLbChunk + nl;
             }
         }
-        HIPCHK(P->lb.prepare(P->blk_cap, lc));
+        HIPCHK(P->lb.prepare(P->blk_cap, P->blk_cap, lc));
         HIPCHK(hipStreamSynchronize(st));
         *out = P.release();
         return S3HC_OK;
@@ -787,15 +792,16 @@ extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src
                                   P->d_fwant.as<uint32_t>(), st));
         T.end();
         T.begin("decode");
+        const uint64_t* bh = nullptr;
         HIPCHK(decode_launch(&P->lb, d_src, d_dst, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(), P->blk_cap,
-                             P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st));
+                             P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st, &bh));
         T.end();
         // frame results, content xxh32 and EndMark checks (one launch)
         T.begin("dec_close");
         HIPCHK(launch_dframe_close(d_src, P->d_frame_off.as<uint64_t>(), P->d_blk_base.as<uint64_t>(),
                                    P->d_nblk.as<uint32_t>(), P->d_dblocks.as<DecBlock>(), P->d_blk_out.as<uint32_t>(),
-                                   P->d_blk_status.as<int32_t>(), d_dst, P->d_dst_off.as<uint64_t>(),
-                                   P->d_fwant.as<uint32_t>(), n, d_status, d_status, d_out_len, st));
+                                   P->d_blk_status.as<int32_t>(), bh, d_dst, P->d_dst_off.as<uint64_t>(),
+                                   P->d_fwant.as<uint32_t>(), n, d_status, d_status, d_out_len, nullptr, st));
         T.end();
         return S3HC_OK;
     });
@@ -1092,9 +1098,15 @@ extern "C" int s3hc_decompressed_bound(const uint8_t* src, size_t n, size_t* bou
 // one synchronisation, the host resolves frames in order and copies the delivered bytes out.
 // Frames whose output is not contiguous on the device (a short non-final independent block)
 // take the second round trip below (device compaction, checksum, copy).
+static double host_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bool stream_mode,
                        std::vector<uint8_t>* vout, uint8_t* dst, size_t cap, size_t* out_len,
                        bool upload_in = true, bool* stopped_out = nullptr) {
+    static const bool trace = getenv("S3HC_HOST_TRACE") != nullptr;  // diagnostics: stage times
+    const double t_0 = trace ? host_us() : 0.0;
+#define HTRACE(tag) if (trace) fprintf(stderr, "[s3hc host] %-10s %8.1f us\n", tag, host_us() - t_0);
     hipStream_t st = ctx->stream;
     HostStage& hs = ctx->hs;
     const size_t nb = W.blocks.size(), nf = W.frames.size();
@@ -1124,10 +1136,12 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         if (W.blocks.size() <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
         for (auto& U : units)
             if (lb_candidate(W.blocks[U.first], U.n == 1, lc.min_limit)) lc.add_block(W.blocks[U.first].csize);
-        HIPCHK(ctx->lb.prepare((uint32_t)units.size(), lc));
+        HIPCHK(ctx->lb.prepare((uint32_t)units.size(), (uint32_t)nb, lc));
+        const uint64_t* bh = nullptr;
+        HTRACE("launch")
         HIPCHK(decode_launch(&ctx->lb, ctx->d_in.as<uint8_t>(), ctx->d_out.as<uint8_t>(), ctx->d_blocks.as<DecBlock>(),
                              ctx->d_units.as<DecUnit>(), (uint32_t)units.size(), ctx->d_blk_out.as<uint32_t>(),
-                             ctx->d_blk_status.as<int32_t>(), st));
+                             ctx->d_blk_status.as<int32_t>(), st, &bh));
         // block checksums (FLG bit 4) over the compressed payloads
         bool any_cs = false;
         for (auto h : W.blk_has_cs) any_cs |= h != 0;
@@ -1142,25 +1156,29 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
                                 (uint32_t)nb, ctx->d_hash.as<uint32_t>(), st));
         }
         // per-frame output length (blocks in order, contiguous slots) and content checksum
+        // (k_dframe_close; its statuses are not used here: the host resolves frames itself)
         {
-            std::vector<uint64_t> ft(2 * nf + (nf + 1) / 2);
-            uint32_t* fnb = (uint32_t*)(ft.data() + 2 * nf);
+            std::vector<uint64_t> ft(3 * nf + (nf + 1) / 2 + (nf + 1) / 2);
+            uint32_t* fnb = (uint32_t*)(ft.data() + 3 * nf);
+            uint32_t* fw = fnb + nf + (nf & 1);
             for (size_t f = 0; f < nf; ++f) {
-                ft[f] = W.frames[f].blk0;
-                ft[nf + f] = W.frames[f].out_off;
+                ft[f] = W.frames[f].pos;
+                ft[nf + f] = W.frames[f].blk0;
+                ft[2 * nf + f] = W.frames[f].out_off;
                 fnb[f] = W.frames[f].nblk;
+                fw[f] = W.frames[f].want;
             }
             HIPCHK(upload(ctx->d_ftab, ft, st));
             HIPCHK(ctx->d_fstat.ensure(nf * 4));
             HIPCHK(ctx->d_flen.ensure(nf * 4));
             HIPCHK(ctx->d_fhash.ensure(nf * 4));
-            HIPCHK(hipMemsetAsync(ctx->d_fstat.p, 0, nf * 4, st));
             const uint64_t* d_ft = ctx->d_ftab.as<uint64_t>();
-            HIPCHK(launch_dframe_finish(d_ft, (uint32_t)nf, (const uint32_t*)(d_ft + 2 * nf), ctx->d_blocks.as<DecBlock>(),
-                                        ctx->d_blk_out.as<uint32_t>(), ctx->d_blk_status.as<int32_t>(),
-                                        ctx->d_fstat.as<int32_t>(), ctx->d_flen.as<uint32_t>(), st));
-            HIPCHK(launch_xxh32(ctx->d_out.as<uint8_t>(), d_ft + nf, ctx->d_flen.as<uint32_t>(), (uint32_t)nf,
-                                ctx->d_fhash.as<uint32_t>(), st));
+            const uint32_t* d_fnb = (const uint32_t*)(d_ft + 3 * nf);
+            HIPCHK(launch_dframe_close(ctx->d_in.as<uint8_t>(), d_ft, d_ft + nf, d_fnb, ctx->d_blocks.as<DecBlock>(),
+                                       ctx->d_blk_out.as<uint32_t>(), ctx->d_blk_status.as<int32_t>(), bh,
+                                       ctx->d_out.as<uint8_t>(), d_ft + 2 * nf, d_fnb + nf + (nf & 1), (uint32_t)nf,
+                                       nullptr, ctx->d_fstat.as<int32_t>(), ctx->d_flen.as<uint32_t>(),
+                                       ctx->d_fhash.as<uint32_t>(), st));
         }
         HIPCHK(hs.small.ensure((3 * nb + 2 * nf) * 4 + 16));
         uint32_t* rb = (uint32_t*)hs.small.p;
@@ -1176,7 +1194,9 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
             HIPCHK(hs.buf[0].ensure(W.slot_total + 16));
             HIPCHK(hipMemcpyAsync(hs.buf[0].p, ctx->d_out.p, W.slot_total, hipMemcpyDeviceToHost, st));
         }
+        HTRACE("queued")
         HIPCHK(hipStreamSynchronize(st));
+        HTRACE("synced")
         bo = rb;
         bs = (const int32_t*)(rb + nb);
         cs_got = rb + 2 * nb;
@@ -1278,6 +1298,7 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
                 return fail(S3HC_CHECKSUM, "content checksum mismatch");
         }
     }
+    HTRACE("resolved")
     if (err_status != S3HC_OK) return fail(err_status, "frame decode failed");
     // Deliver
     uint8_t* hdst = dst;
@@ -1307,6 +1328,8 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         for (auto& sp : spans) runs.push_back({dev_out + sp.first, sp.second});
         HIPCHK(hs.d2h(hdst, runs, st));
     }
+    HTRACE("delivered")
+#undef HTRACE
     if (out_len) *out_len = total;
     return S3HC_OK;
 }
@@ -1706,7 +1729,7 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
         if (nbk <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
         for (auto& U : units)
             if (lb_candidate(mb[U.first], U.n == 1, lc.min_limit)) lc.add_block(mb[U.first].csize);
-        HIPCHK(S.lb.prepare(nu, lc));
+        HIPCHK(S.lb.prepare(nu, nbk, lc));
     }
     HIPCHK(S.h_res.ensure(8ull * n));
     HIPCHK(hipMemcpyAsync(S.d_in.p, S.h_in.p, nin, hipMemcpyHostToDevice, st));
@@ -1718,14 +1741,15 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     int32_t* d_st = (int32_t*)(S.d_res.as<uint8_t>() + 4ull * n);
     KTimer T(r->ctx, st);
     T.begin("decode");
+    const uint64_t* bh = nullptr;
     HIPCHK(decode_launch(&S.lb, src, S.d_out.as<uint8_t>(), d_blk, (const DecUnit*)(dm + o_u), nu,
-                         S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), st));
+                         S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), st, &bh));
     T.end();
     T.begin("dec_close");
     HIPCHK(launch_dframe_close(src, (const uint64_t*)(dm + o_fo), (const uint64_t*)(dm + o_bb),
                                (const uint32_t*)(dm + o_nb), d_blk, S.d_blk_out.as<uint32_t>(),
-                               S.d_blk_status.as<int32_t>(), S.d_out.as<uint8_t>(), (const uint64_t*)(dm + o_oo),
-                               (const uint32_t*)(dm + o_w), n, nullptr, d_st, d_olen, st));
+                               S.d_blk_status.as<int32_t>(), bh, S.d_out.as<uint8_t>(), (const uint64_t*)(dm + o_oo),
+                               (const uint32_t*)(dm + o_w), n, nullptr, d_st, d_olen, nullptr, st));
     T.end();
     HIPCHK(hipMemcpyAsync(S.h_res.p, S.d_res.p, 8ull * n, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(S.ev, st));
