@@ -179,6 +179,12 @@ int s3hc_queue_create(s3hc_ctx* ctx, void** out);
 int s3hc_queue_destroy(s3hc_ctx* ctx, void* q);
 int s3hc_queue_sync(s3hc_ctx* ctx, void* q);
 int s3hc_memcpy_async(s3hc_ctx* ctx, void* dst, const void* src, size_t n, int kind, void* q);
+/* Cross-queue ordering: a mark records the point reached by the work queued on q so far;
+ * work queued on another queue after s3hc_queue_wait_mark starts only once that point is
+ * passed (q NULL: the context's own queue). Marks are freed with s3hc_mark_free (any time). */
+int s3hc_queue_mark(s3hc_ctx* ctx, void* q, void** mark);
+int s3hc_queue_wait_mark(s3hc_ctx* ctx, void* q, void* mark);
+int s3hc_mark_free(s3hc_ctx* ctx, void* mark);
 
 /* ---- CompressionHandler mirror (compression.rs:169-604) ------------------- */
 /* The host-side mirror of the reference's handler: same decision inputs, same six

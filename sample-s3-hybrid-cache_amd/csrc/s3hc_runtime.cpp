@@ -1614,6 +1614,34 @@ extern "C" int s3hc_queue_sync(s3hc_ctx* ctx, void* q) {
         return S3HC_OK;
     });
 }
+extern "C" int s3hc_queue_mark(s3hc_ctx* ctx, void* q, void** mark) {
+    return guarded([&]() -> int {
+        if (!ctx || !mark) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        const hipError_t r = hipEventRecord(e, q ? (hipStream_t)q : ctx->stream);
+        if (r != hipSuccess) (void)hipEventDestroy(e);
+        HIPCHK(r);
+        *mark = (void*)e;
+        return S3HC_OK;
+    });
+}
+extern "C" int s3hc_queue_wait_mark(s3hc_ctx* ctx, void* q, void* mark) {
+    return guarded([&]() -> int {
+        if (!ctx || !mark) return fail(S3HC_INVALID_ARG, "bad arguments");
+        HIPCHK(hipSetDevice(ctx->device));
+        HIPCHK(hipStreamWaitEvent(q ? (hipStream_t)q : ctx->stream, (hipEvent_t)mark, 0));
+        return S3HC_OK;
+    });
+}
+extern "C" int s3hc_mark_free(s3hc_ctx* ctx, void* mark) {
+    return guarded([&]() -> int {
+        if (!ctx) return fail(S3HC_INVALID_ARG, "bad arguments");
+        if (mark) HIPCHK(hipEventDestroy((hipEvent_t)mark));
+        return S3HC_OK;
+    });
+}
 extern "C" int s3hc_memcpy_async(s3hc_ctx* ctx, void* dst, const void* src, size_t n, int kind, void* q) {
     return guarded([&]() -> int {
         if (!ctx || kind < 1 || kind > 3) return fail(S3HC_INVALID_ARG, "bad arguments");

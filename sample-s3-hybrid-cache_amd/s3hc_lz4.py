@@ -109,6 +109,9 @@ def _load():
         "s3hc_queue_destroy": (i32, [vp, vp]),
         "s3hc_queue_sync": (i32, [vp, vp]),
         "s3hc_memcpy_async": (i32, [vp, vp, vp, sz, i32, vp]),
+        "s3hc_queue_mark": (i32, [vp, vp, ctypes.POINTER(vp)]),
+        "s3hc_queue_wait_mark": (i32, [vp, vp, vp]),
+        "s3hc_mark_free": (i32, [vp, vp]),
         "s3hc_reader_open": (i32, [vp, sz, i32, ctypes.POINTER(vp)]),
         "s3hc_reader_set_batch_max": (i32, [vp, sz]),
         "s3hc_reader_feed": (i32, [vp, u8p, sz]),
@@ -281,6 +284,20 @@ class Engine:
 
     def queue(self) -> "Queue":
         return Queue(self)
+
+    def mark(self, queue: "Queue" = None) -> int:
+        """Record the point reached by the work queued on `queue` so far (None: the context
+        queue); pass it to wait_mark, release it with free_mark."""
+        m = ctypes.c_void_p()
+        _check(lib.s3hc_queue_mark(self.h, _q(queue), ctypes.byref(m)))
+        return m.value
+
+    def wait_mark(self, mark: int, queue: "Queue" = None):
+        """Later work on `queue` starts only after `mark` is passed."""
+        _check(lib.s3hc_queue_wait_mark(self.h, _q(queue), ctypes.c_void_p(mark)))
+
+    def free_mark(self, mark: int):
+        _check(lib.s3hc_mark_free(self.h, ctypes.c_void_p(mark)))
 
     def copy_async(self, dst, src, n: int, kind: int, queue: "Queue" = None, dst_off: int = 0, src_off: int = 0):
         """kind 1 H2D, 2 D2H, 3 D2D; dst/src: DeviceBuffer or HostBuffer (data_ptr())."""
