@@ -217,9 +217,10 @@ def config4(eng, data2, nq=3, total_gib=8, batch_bytes_list=(256 << 10, 64 << 20
             for L in lanes:
                 L[0].close()
         # the C++ pipelined range reader (s3hc_reader): the object's frames fed in 4 MiB file
-        # reads, decoded bytes read back in 1 MiB chunks (stream_range_data's chunk size)
-        for bb in (256 << 10, 4 << 20, 64 << 20):
-            rd = S.RangeReader(eng, bb, nq)
+        # reads, decoded bytes read back in 1 MiB chunks (stream_range_data's chunk size); fixed
+        # batches, and 256 KiB batches that may grow to 16 MiB behind running ones (batch_max)
+        for bb, bmax in ((256 << 10, None), (256 << 10, 16 << 20), (4 << 20, None), (64 << 20, None)):
+            rd = S.RangeReader(eng, bb, nq, bmax)
             hp, op = h_fr.data_ptr(), h_out.data_ptr()
             ctot, got = C1 * tiles, 0
             t0 = time.perf_counter()
@@ -238,8 +239,9 @@ def config4(eng, data2, nq=3, total_gib=8, batch_bytes_list=(256 << 10, 64 << 20
                 got += k
             dt = time.perf_counter() - t0
             assert got == total_u and rd.total == total_u
-            res[f"reader_decode_GiBps_batch_{bb >> 10}KiB"] = round(total_u / dt / GiB, 3)
-            res[f"reader_check_batch_{bb >> 10}KiB"] = bytes(h_out.view()[-item:]) == data2[-item:]
+            tag = f"{bb >> 10}KiB" + (f"_adaptive_max{bmax >> 20}MiB" if bmax else "")
+            res[f"reader_decode_GiBps_batch_{tag}"] = round(total_u / dt / GiB, 3)
+            res[f"reader_check_batch_{tag}"] = bytes(h_out.view()[-item:]) == data2[-item:]
             rd.close()
         out[fmt] = res
         h_out.free()

@@ -8,4 +8,5 @@ step lb 300 python tools_lb.py
 step config3 400 python tools_config3.py
 step compat 300 python tools_compat.py
 step e2e 600 python tools_e2e.py
+step small 300 python tools_small.py
 echo sec-ok
