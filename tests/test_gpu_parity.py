@@ -568,3 +568,36 @@ def test_short_nonfinal_independent_blocks(engine, oracle, checksum):
     if checksum:
         bad[-1] ^= 1
         assert engine.decompress_status(bytes(bad))[0] == oracle.decompress_status(bytes(bad))[0]
+
+
+# ---- host-buffer staging (pinned chunks / direct DMA for pinned caller buffers, one readback)
+@pytest.mark.parametrize("mib,policy", [(20, 1), (20, 0), (3, 1)])
+def test_host_calls_large_and_pinned_buffers(engine, oracle, mib, policy):
+    """Outputs above the 8 MiB readback size go through the chunked pinned staging; pinned
+    caller buffers (hipHostMalloc) are copied directly. Same bytes either way."""
+    import ctypes
+
+    data = synth.log_text(mib * MiB + 77, 70 + mib)
+    frame = engine.compress_frame(data, policy)
+    assert oracle.decompress_data(frame) == data
+    assert engine.decompress_frames(frame) == data                # pageable output (library-owned)
+    assert engine.decompress_frames(frame, len(data) + 5) == data  # pageable caller buffer
+    # pinned source and pinned destination through the raw C ABI
+    h_in, h_out = engine.host_alloc(len(frame)), engine.host_alloc(len(data) + 64)
+    h_in.view()[:] = np.frombuffer(frame, dtype=np.uint8)
+    n = ctypes.c_size_t()
+    rc = S.lib.s3hc_decompress_frames(engine.h, ctypes.c_void_p(h_in.data_ptr()), len(frame),
+                                      ctypes.c_void_p(h_out.data_ptr()), len(data) + 64, ctypes.byref(n))
+    assert rc == 0 and n.value == len(data)
+    assert bytes(h_out.view()[:len(data)]) == data
+    # encode from a pinned source into a pinned destination: the same frame bytes
+    h_src = engine.host_alloc(len(data))
+    h_src.view()[:] = np.frombuffer(data, dtype=np.uint8)
+    cap = S.frame_bound(len(data))
+    h_dst = engine.host_alloc(cap)
+    wc = ctypes.c_int()
+    rc = S.lib.s3hc_compress_frame(engine.h, ctypes.c_void_p(h_src.data_ptr()), len(data), policy,
+                                   ctypes.c_void_p(h_dst.data_ptr()), cap, ctypes.byref(n), ctypes.byref(wc))
+    assert rc == 0 and bytes(h_dst.view()[:n.value]) == frame
+    for h in (h_in, h_out, h_src, h_dst):
+        h.free()
