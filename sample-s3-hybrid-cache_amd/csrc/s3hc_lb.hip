@@ -644,10 +644,13 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         lim_ = lim_ < hns ? lim_ : hns;                                                         \
         lim_ = lim_ < hs + (budget) ? lim_ : hs + (budget);                                     \
         for (; hs + 16u <= lim_; hs += 16u) {                                                   \
-            uint32_t v_[16];                                                                    \
-            _Pragma("unroll") for (uint32_t k = 0; k < 16; ++k)                                 \
-                v_[k] = *(const uint32_t*)(ring + ((16u * (hs + k) + 4u * ha) & kMask));        \
-            _Pragma("unroll") for (uint32_t k = 0; k < 16; ++k) hacc = xh_round(hacc, v_[k]);   \
+            /* lane 4k + a loads stripe k's dword a and multiplies it by P2 (off the chain, one */ \
+            /* load and one multiply for 16 stripes); the chain then only adds, rotates and     */ \
+            /* multiplies by P1                                                                 */ \
+            const uint32_t mv_ = *(const uint32_t*)(ring + ((16u * hs + 4u * (uint32_t)lane) & kMask)) * XH2; \
+            uint32_t m_[16];                                                                    \
+            _Pragma("unroll") for (uint32_t k = 0; k < 16; ++k) m_[k] = __shfl(mv_, (int)(4u * k + ha)); \
+            _Pragma("unroll") for (uint32_t k = 0; k < 16; ++k) hacc = xh_rotl(hacc + m_[k], 13) * XH1; \
         }                                                                                       \
         for (; hs < lim_; ++hs) hacc = xh_round(hacc, *(const uint32_t*)(ring + ((16u * hs + 4u * ha) & kMask))); \
     }
