@@ -31,6 +31,9 @@
 // All of it is integer byte work (no MFMA); every kernel is bound by memory latency or LDS.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 #include "s3hc_lz4.h"
 #include "s3hc_plan.hpp"
@@ -606,6 +609,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
     __shared__ uint32_t jflag[3];
     const uint32_t i = blockIdx.x;
     if (i >= A.ctl->nlb || A.lb_stat[i] != S3HC_OK) return;
+    if (A.wcap && A.wbase[i] != lb::NONE) return;  // spread execution decodes it (k_lbw_*)
     const LbBlock B = A.lbt[i];
     const uint32_t size = A.lb_size[i];
     const uint32_t tok0 = A.lb_tok0[i], ntok = A.lb_ntok[i];
@@ -906,6 +910,336 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
 #undef LB_PUT
 #undef LB_INSTALL
 
+// ---------------------------------------------------------------- spread execution
+// k_lb_run writes a block with ONE workgroup, step after step: right for a batch that gives every
+// CU a block, but one reference cache file (a 1 MiB frame = one block) then keeps 1 of 256 CUs
+// busy for 137 serial steps. With few blocks the output is instead cut into tiles of kLbStep
+// bytes that are all decoded at once, by as many workgroups as the chip holds:
+//
+//   k_lbw_plan    (1 workgroup) P positions and tiles of the blocks that fit P (wcap);
+//   k_lbw_init    per tile: every byte gets its value (literal) or its source (matches: the
+//                 first period of an overlapping copy), chains inside the tile are jumped in LDS;
+//                 final bytes are stored, every other byte leaves a pointer to a byte of an
+//                 earlier tile in P (global positions);
+//   k_lbw_round   x kLbwRounds: pointer jumping over P (each pending byte reads its source's
+//                 entry: final -> that source is its root; resolved -> take the root; else jump),
+//                 up to kLbwHops hops per launch. Entries only move along their chain, so reading
+//                 a value another workgroup is replacing in the same launch is harmless; roots are
+//                 always bytes k_lbw_init stored (earlier launch: visible). A launch with nothing
+//                 pending returns at once;
+//   k_lbw_gather  every pending byte copies its root's byte (walking what the rounds left: every
+//                 pointer goes to a smaller position, so every chain ends).
+namespace lb {
+constexpr uint32_t PFIN = 0xFFFFFFFFu;  // P: the byte in dst is final
+constexpr uint32_t PRES = 0x80000000u;  // P: flag of a resolved entry (1 << 31 | root); PFIN has it too
+constexpr uint32_t LOUT = 0x80000000u;  // k_lbw_init LDS pointer: source before the tile (P position)
+}  // namespace lb
+
+__global__ __launch_bounds__(1024) void k_lbw_plan(LbArgs A) {
+    using namespace lb;
+    __shared__ uint64_t shs[16];
+    __shared__ uint32_t sht[16];
+    __shared__ uint64_t cpos;
+    __shared__ uint32_t ctile;
+    const uint32_t t = threadIdx.x;
+    if (t < kLbwRounds + 2) A.ctl->rflag[t] = 0u;
+    if (t == 0) { cpos = 0; ctile = 0; }
+    __syncthreads();
+    const uint32_t nlb = A.ctl->nlb;
+    for (uint32_t base = 0; base < nlb; base += 1024) {
+        const uint32_t i = base + t;
+        const bool ok = i < nlb && A.lb_stat[i] == S3HC_OK && A.lb_size[i] > 0;
+        const uint32_t size = ok ? A.lb_size[i] : 0u;
+        uint64_t tots;
+        uint32_t tott;
+        // positions grow with the block index, so the spread blocks are a prefix of the decodable ones
+        const uint64_t pp = wg_excl_add<uint64_t, 16>((uint64_t)size, shs, tots) + cpos;
+        // (with more than kLbwMaxBlocks blocks the step loop has a block for most CUs: spread off)
+        const bool wide = ok && pp + size <= A.wcap && nlb <= kLbwMaxBlocks;
+        const uint32_t nt = wide ? (size + kLbStep - 1) / kLbStep : 0u;
+        const uint32_t tp = wg_excl_add<uint32_t, 16>(nt, sht, tott) + ctile;
+        if (i < nlb) {
+            A.wbase[i] = wide ? (uint32_t)pp : NONE;
+            A.wtile0[i] = tp;
+        }
+        __syncthreads();
+        if (t == 0) { cpos += tots; ctile += tott; }
+        __syncthreads();
+    }
+    if (t == 0) A.ctl->ntiles = ctile;
+}
+
+// LB block holding tile T: the last block whose first tile is <= T (blocks without tiles repeat
+// their successor's first tile and are skipped by that rule)
+__device__ __forceinline__ uint32_t lbw_block(const LbArgs& A, uint32_t nlb, uint32_t T) {
+    uint32_t lo = 0, hi = nlb;
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (A.wtile0[mid] <= T) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(960) void k_lbw_init(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, LbArgs A) {
+    using namespace lb;
+    __shared__ __attribute__((aligned(16))) uint16_t marks[kLbStep];
+    __shared__ __attribute__((aligned(16))) uint32_t sqp[kMaxSeqS * 4];  // the tile's sequences, then its pointers
+    __shared__ uint16_t so[kMaxSeqS];
+    __shared__ __attribute__((aligned(16))) uint8_t val[kLbStep];
+    __shared__ uint32_t shm[16];
+    __shared__ uint32_t jflag[3];
+    static_assert(kLbStep <= kMaxSeqS * 4, "pointers fit the sequence table's space");
+    uint4* sq = (uint4*)sqp;
+    uint32_t* ptr = sqp;
+    const uint32_t t = threadIdx.x;
+    const int lane = lane64();
+    const uint32_t ntiles = A.ctl->ntiles, nlb = A.ctl->nlb;
+    for (uint32_t T = blockIdx.x; T < ntiles; T += gridDim.x) {
+        const uint32_t i = lbw_block(A, nlb, T);
+        const uint32_t q = T - A.wtile0[i];
+        const LbBlock B = A.lbt[i];
+        const uint32_t size = A.lb_size[i], wb = A.wbase[i], tok0 = A.lb_tok0[i], ntok = A.lb_ntok[i];
+        const uint32_t nsteps = (size + kLbStep - 1) / kLbStep;
+        const uint32_t R = q * kLbStep;
+        const uint8_t* g = src + B.src_off;
+        uint8_t* ob = dst + B.dst_off;
+        const uint32_t s0 = A.rfirst[(size_t)i * kLbMaxSteps + q];
+        const uint32_t s1 = q + 1 < nsteps ? A.rfirst[(size_t)i * kLbMaxSteps + q + 1] + 1u : ntok;
+        const uint32_t ns = s1 - s0 < kMaxSeqS ? s1 - s0 : kMaxSeqS;
+        ((uint4*)marks)[t] = make_uint4(0, 0, 0, 0);  // kLbStep u16 = 960 x 16 B
+        __syncthreads();
+        for (uint32_t j = t; j < ns; j += kXT) {
+            const uint4 e = A.seq4[tok0 + s0 + j];
+            sq[j] = e;
+            so[j] = A.seqoff[tok0 + s0 + j];
+            const uint32_t rel = e.x > R ? e.x - R : 0u;
+            if (rel < kLbStep && (j == 0 || e.x > R)) marks[rel] = (uint16_t)(j + 1u);
+        }
+        __syncthreads();
+        // owner of each byte: running max of the start marks (thread t: bytes 8t .. 8t+7)
+        const uint4 m4 = ((const uint4*)marks)[t];
+        const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
+        uint32_t mx = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t lo = mw[k] & 0xFFFFu, hi = mw[k] >> 16;
+            mx = lo > mx ? lo : mx;
+            mx = hi > mx ? hi : mx;
+        }
+        uint32_t inc = mx;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d);
+            if (lane >= d) inc = y > inc ? y : inc;
+        }
+        if (lane == 63) shm[t >> 6] = inc;
+        __syncthreads();
+        uint32_t cur = __shfl_up(inc, 1);
+        if (lane == 0) cur = 0;
+        for (uint32_t w = 0; w < (t >> 6); ++w) cur = shm[w] > cur ? shm[w] : cur;
+        {
+            uint32_t ow[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t lo = mw[k] & 0xFFFFu, hi = mw[k] >> 16;
+                cur = lo > cur ? lo : cur;
+                const uint32_t o0 = cur;
+                cur = hi > cur ? hi : cur;
+                ow[k] = o0 | (cur << 16);
+            }
+            ((uint4*)marks)[t] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        }
+        __syncthreads();
+        // classify (thread t: bytes t + kXT*j): literal (input address) or match source, taken in
+        // the first period of an overlapping copy; sources inside the tile become LDS pointers,
+        // sources before it P positions
+        uint32_t la[kXPer], pv[kXPer];
+        uint32_t litm = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) {
+            const uint32_t l = t + kXT * j;
+            const uint32_t x = R + l;
+            pv[j] = FIN;
+            la[j] = 0;
+            if (x < size) {
+                const uint32_t k = marks[l] - 1u;
+                const uint4 e = sq[k];
+                const uint32_t rel = x - e.x;
+                if (rel < e.z) {
+                    la[j] = e.y + rel;
+                    litm |= 1u << j;
+                } else {
+                    const uint32_t off = so[k];
+                    const uint32_t ee = rel - e.z;  // position inside the match
+                    const uint32_t y = ee >= off ? e.x + e.z - off + ee % off : x - off;
+                    pv[j] = y >= R ? y - R : (LOUT | (wb + y));
+                }
+            }
+        }
+        uint32_t lv[kXPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) lv[j] = g[(litm >> j) & 1u ? la[j] : 0u];
+        __syncthreads();  // every read of sq is done before the pointers overwrite it
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) {
+            const uint32_t l = t + kXT * j;
+            val[l] = (uint8_t)((litm >> j) & 1u ? lv[j] : 0u);
+            ptr[l] = pv[j];
+        }
+        if (t == 0) jflag[0] = 0u;
+        __syncthreads();
+        // chains inside the tile (as in k_lb_run): a final source gives the value, a source that
+        // points before the tile hands over its P position, a pending one is jumped over
+        uint32_t pend = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) pend |= (!(pv[j] & LOUT) ? 1u : 0u) << j;
+        for (uint32_t it = 0; it < 16; ++it) {
+            if (pend) {
+                uint32_t pp[kXPer];
+#pragma unroll
+                for (uint32_t j = 0; j < kXPer; ++j) pp[j] = (pend >> j) & 1u ? ptr[pv[j]] : 0u;
+                uint32_t rv[kXPer];
+                uint32_t fin = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < kXPer; ++j) {
+                    const bool f = ((pend >> j) & 1u) && pp[j] == FIN;
+                    fin |= (f ? 1u : 0u) << j;
+                    rv[j] = f ? val[pv[j]] : 0u;
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < kXPer; ++j)
+                    if ((fin >> j) & 1u) val[t + kXT * j] = (uint8_t)rv[j];
+                if (fin) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                uint32_t done = fin;
+#pragma unroll
+                for (uint32_t j = 0; j < kXPer; ++j) {
+                    if ((pend >> j) & 1u) {
+                        pv[j] = (fin >> j) & 1u ? FIN : pp[j];
+                        done |= ((pv[j] & LOUT) ? 1u : 0u) << j;
+                        ptr[t + kXT * j] = pv[j];
+                    }
+                }
+                pend &= ~done;
+                if (pend) jflag[it % 3u] = 1u;
+            }
+            if (t == 0) jflag[(it + 1u) % 3u] = 0u;
+            __syncthreads();
+            if (!jflag[it % 3u]) break;
+        }
+        // store: final bytes (coalesced dwords from LDS), every byte's P entry
+        const bool al = (((uintptr_t)(ob + R)) & 3u) == 0;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+            const uint32_t l0 = 4u * (t + kXT * h);
+            const uint32_t x0 = R + l0;
+            const uint32_t v4 = *(const uint32_t*)(val + l0);
+            if (al && x0 + 4u <= size) {
+                *(uint32_t*)(ob + x0) = v4;
+            } else {
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (x0 + j < size) ob[x0 + j] = (uint8_t)(v4 >> (8 * j));
+            }
+        }
+        bool out = false;
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) {
+            const uint32_t x = R + t + kXT * j;
+            if (x < size) {
+                const bool o = pv[j] != FIN;
+                out |= o;
+                A.P[wb + x] = o ? (pv[j] & ~LOUT) : PFIN;
+            }
+        }
+        const int po = __syncthreads_or(out);  // also: every read of val/marks of this tile is done
+        if (t == 0) {
+            A.tpend[T] = po ? 1 : 0;
+            A.tinit[T] = po ? 1 : 0;
+            if (po) atomicAdd(&A.ctl->rflag[0], 1u);
+        }
+    }
+}
+
+__global__ __launch_bounds__(960) void k_lbw_round(LbArgs A, uint32_t r) {
+    using namespace lb;
+    if (!A.ctl->rflag[r]) return;
+    const uint32_t t = threadIdx.x;
+    const uint32_t ntiles = A.ctl->ntiles, nlb = A.ctl->nlb;
+    uint32_t npend = 0;  // tiles of this workgroup still pending after the launch
+    for (uint32_t T = blockIdx.x; T < ntiles; T += gridDim.x) {
+        if (!A.tpend[T]) continue;
+        const uint32_t i = lbw_block(A, nlb, T);
+        const uint32_t q = T - A.wtile0[i];
+        const uint32_t size = A.lb_size[i], wb = A.wbase[i];
+        const uint32_t R = q * kLbStep;
+        uint32_t v[kXPer];
+        uint32_t pend = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) {
+            const uint32_t x = R + t + kXT * j;
+            v[j] = x < size ? A.P[wb + x] : PFIN;
+            pend |= ((v[j] & PRES) ? 0u : 1u) << j;
+        }
+        const uint32_t touched = pend;
+        // up to kLbwHops hops per launch (entries read here may already be this launch's)
+        for (uint32_t h = 0; h < kLbwHops && pend; ++h) {
+            uint32_t w[kXPer];
+#pragma unroll
+            for (uint32_t j = 0; j < kXPer; ++j) w[j] = (pend >> j) & 1u ? A.P[v[j]] : 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < kXPer; ++j) {
+                if ((pend >> j) & 1u) {
+                    v[j] = w[j] == PFIN ? (v[j] | PRES) : w[j];
+                    if (v[j] & PRES) pend &= ~(1u << j);
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j)
+            if ((touched >> j) & 1u) A.P[wb + R + t + kXT * j] = v[j];
+        const int ps = __syncthreads_or(pend != 0);
+        if (t == 0) A.tpend[T] = ps ? 1 : 0;
+        npend += ps ? 1u : 0u;
+    }
+    if (t == 0 && npend) atomicAdd(&A.ctl->rflag[r + 1], npend);
+}
+
+__global__ __launch_bounds__(960) void k_lbw_gather(uint8_t* __restrict__ dst, LbArgs A) {
+    using namespace lb;
+    const uint32_t t = threadIdx.x;
+    const uint32_t ntiles = A.ctl->ntiles, nlb = A.ctl->nlb;
+    for (uint32_t T = blockIdx.x; T < ntiles; T += gridDim.x) {
+        if (!A.tinit[T]) continue;
+        const uint32_t i = lbw_block(A, nlb, T);
+        const uint32_t q = T - A.wtile0[i];
+        const uint32_t size = A.lb_size[i], wb = A.wbase[i];
+        uint8_t* ob = dst + A.lbt[i].dst_off;
+        const uint32_t R = q * kLbStep;
+        uint32_t v[kXPer], b[kXPer];
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) {
+            const uint32_t x = R + t + kXT * j;
+            v[j] = x < size ? A.P[wb + x] : PFIN;
+        }
+        // a chain the rounds did not finish (only for chains far longer than data holds) is
+        // walked here: P no longer changes, and every pointer goes to a smaller position
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) {
+            while (!(v[j] & PRES)) {
+                const uint32_t w = A.P[v[j]];
+                v[j] = w == PFIN ? (v[j] | PRES) : w;
+            }
+        }
+        // roots: 1 << 31 | position of a byte k_lbw_init stored
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j) b[j] = v[j] != PFIN ? ob[(v[j] & ~PRES) - wb] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < kXPer; ++j)
+            if (v[j] != PFIN) ob[R + t + kXT * j] = (uint8_t)b[j];
+    }
+}
+
 // ================================================================ launchers
 static inline uint32_t cdiv_lb(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 hipError_t launch_scan(const uint32_t* in, uint32_t n, uint64_t* out, uint64_t* total, hipStream_t st);
@@ -930,6 +1264,17 @@ hipError_t launch_lb_parse(const LbArgs& A, const uint8_t* src, const DecBlock* 
 
 // Execute stage: one workgroup per taken block.
 hipError_t launch_lb_exec(const LbArgs& A, const uint8_t* src, uint8_t* dst, hipStream_t st) {
+    if (A.wcap) {  // spread execution of the blocks that fit P, then the step loop for the rest
+        const uint32_t tiles = A.tile_cap;
+        hipLaunchKernelGGL(k_lbw_plan, dim3(1), dim3(1024), 0, st, A);
+        hipLaunchKernelGGL(k_lbw_init, dim3(tiles < 512u ? tiles : 512u), dim3(lb::kXT), 0, st, src, dst, A);
+        // S3HC_LBW_ROUNDS (tests): fewer launches, so k_lbw_gather walks long chains itself
+        uint32_t rounds = kLbwRounds;
+        if (const char* ev = getenv("S3HC_LBW_ROUNDS")) rounds = std::min<uint32_t>(rounds, (uint32_t)atoi(ev));
+        for (uint32_t r = 0; r < rounds; ++r)
+            hipLaunchKernelGGL(k_lbw_round, dim3(tiles < 512u ? tiles : 512u), dim3(lb::kXT), 0, st, A, r);
+        hipLaunchKernelGGL(k_lbw_gather, dim3(tiles < 1024u ? tiles : 1024u), dim3(lb::kXT), 0, st, dst, A);
+    }
     hipLaunchKernelGGL(k_lb_run, dim3(A.lb_cap), dim3(lb::kXWG), 0, st, src, dst, A);
     return hipGetLastError();
 }

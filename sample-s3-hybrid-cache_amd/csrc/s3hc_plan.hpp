@@ -100,6 +100,14 @@ constexpr uint32_t kLbMinLimit = 65537;   // frame max block size above 64 KiB s
 constexpr uint32_t kLbFewBlocks = 256;    // batches with at most this many blocks: every compressed
                                           // independent block takes the path (latency: one wave per
                                           // 64 KiB block needs 0.85 ms)
+constexpr uint32_t kLbwRounds = 6;        // spread execution: pointer-jumping launches (k_lbw_gather
+                                          // walks whatever chains they leave)
+constexpr uint32_t kLbwHops = 4;          // ... hops per byte and launch, at most
+constexpr uint32_t kLbwCapMax = 1u << 30; // spread execution: pointer-array positions, at most
+constexpr uint32_t kLbwMaxBlocks = 64;        // ... and so do launches of more blocks than this
+constexpr uint32_t kLbwMaxOut = 96u << 20;     // launches whose large blocks may decode to more than
+                                              // this run the step loop (k_lb_run): with a block per CU
+                                              // it is as fast, and P stays small (measured, §4b)
 
 struct LbBlock {         // 48 bytes; one per block taken by the large-block path
     uint64_t src_off;    // compressed payload
@@ -112,7 +120,8 @@ struct LbBlock {         // 48 bytes; one per block taken by the large-block pat
 };
 
 struct LbCtl {           // device-side counters of one large-block launch
-    uint32_t nlb, nchunks, pad0, pad1;
+    uint32_t nlb, nchunks, ntiles, pad0;
+    uint32_t rflag[kLbwRounds + 2];  // spread execution: [r] = tiles still pending before round r
 };
 
 // Device scratch of the large-block path (sized by the host: lb_cap blocks, chunk_cap chunks;
@@ -120,7 +129,9 @@ struct LbCtl {           // device-side counters of one large-block launch
 struct LbArgs {
     uint32_t lb_cap, chunk_cap;
     uint32_t min_limit;    // frame max block size that selects the path (kLbMinLimit; 1 for few-block batches)
-    uint32_t pad;
+    uint32_t wcap;         // spread execution: positions of P (0: every block runs the step loop)
+    uint32_t tile_cap;     // spread execution: tiles (kLbStep output bytes) of the spread blocks, at most
+    uint32_t pad2;
     LbBlock* lbt;
     LbCtl* ctl;
     uint8_t* unit_lb;      // per unit: 1 = decoded by this path
@@ -146,6 +157,13 @@ struct LbArgs {
     uint32_t* rfirst;      // per LB block x kLbMaxSteps: sequence covering each step's first byte
     uint64_t* blk_hash;    // per DecBlock: 1 << 32 | xxh32 of its output (written by k_lb_run; cleared
                            // by k_lb_classify for every single-block unit)
+    // spread execution (few blocks): every byte of a block gets a source pointer
+    // at once, chains are resolved by global pointer jumping over all tiles of all spread blocks
+    uint32_t* wbase;       // per LB block: first position in P, or ~0 (the block runs k_lb_run)
+    uint32_t* wtile0;      // per LB block: first tile (exclusive scan of the spread blocks' tiles)
+    uint32_t* P;           // per output byte of the spread blocks: ~0 final, 1 << 31 | root, or source
+    uint8_t* tpend;        // per tile: some byte still has a plain pointer
+    uint8_t* tinit;        // per tile: some byte was left pending by k_lbw_init (needs the gather)
 };
 
 

@@ -343,9 +343,11 @@ struct HostStage {
 struct LbCaps {
     uint32_t lb = 0, chunks = 0;
     uint32_t min_limit = kLbMinLimit;
-    void add_block(uint32_t csize) {
+    uint64_t outb = 0;  // decoded bytes of the candidate blocks, at most (sizes the spread execution)
+    void add_block(uint32_t csize, uint32_t out_bound) {
         ++lb;
         chunks += (csize + kLbChunk - 1) / kLbChunk;
+        outb += std::min<uint64_t>(out_bound, (uint64_t)kLbMaxSteps * kLbStep);
     }
 };
 static bool lb_candidate(const DecBlock& D, bool unit_single, uint32_t min_limit) {
@@ -355,7 +357,7 @@ static bool lb_candidate(const DecBlock& D, bool unit_single, uint32_t min_limit
 
 struct LbScratch {
     DevBuf lbt, ctl, unit_lb, chunk_blk, nzg, E, J0, entry, bits, ntok, slsum, badrel, tokbase, outbase, total, seq4,
-        seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst, blk_hash;
+        seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst, blk_hash, wbase, wtile0, wP, tpend, tinit;
     LbArgs a{};
     bool active = false;
     // nunits: units of the launch; nblocks: its DecBlock count (block hashes are per DecBlock)
@@ -372,6 +374,17 @@ struct LbScratch {
         LBE(tokbase, nch * 8) LBE(outbase, nch * 8) LBE(total, 32) LBE(seq4, nseq * 16) LBE(seqoff, nseq * 2)
         LBE(lb_err, nlb * 4) LBE(lb_size, nlb * 4) LBE(lb_stat, nlb * 4) LBE(lb_tok0, nlb * 4) LBE(lb_ntok, nlb * 4)
         LBE(rfirst, nlb * kLbMaxSteps * 4) LBE(blk_hash, (size_t)std::max(nunits, nblocks) * 8)
+        // spread execution (few blocks, §4b): P holds one u32 per decoded byte of the spread blocks;
+        // S3HC_LBW_CAP (positions, 0 = off; tests split a launch with it) replaces the size rule,
+        // S3HC_LBW_DISABLE=1 turns it off
+        uint64_t wcap = c.outb <= kLbwMaxOut ? c.outb : 0;
+        if (const char* ev = getenv("S3HC_LBW_CAP")) wcap = std::min<uint64_t>(c.outb, strtoull(ev, nullptr, 10));
+        if (getenv("S3HC_LBW_DISABLE")) wcap = 0;
+        wcap = std::min<uint64_t>(wcap, kLbwCapMax);
+        const size_t tcap = wcap ? wcap / kLbStep + nlb + 1 : 0;
+        if (wcap) {
+            LBE(wbase, nlb * 4) LBE(wtile0, nlb * 4) LBE(wP, wcap * 4) LBE(tpend, tcap) LBE(tinit, tcap)
+        }
 #undef LBE
         a.lb_cap = c.lb;
         a.chunk_cap = c.chunks;
@@ -385,6 +398,13 @@ struct LbScratch {
         a.lb_stat = lb_stat.as<uint32_t>(); a.lb_tok0 = lb_tok0.as<uint32_t>(); a.lb_ntok = lb_ntok.as<uint32_t>();
         a.rfirst = rfirst.as<uint32_t>();
         a.blk_hash = blk_hash.as<uint64_t>();
+        a.wcap = (uint32_t)wcap;
+        a.tile_cap = (uint32_t)tcap;
+        a.wbase = wcap ? wbase.as<uint32_t>() : nullptr;
+        a.wtile0 = wcap ? wtile0.as<uint32_t>() : nullptr;
+        a.P = wcap ? wP.as<uint32_t>() : nullptr;
+        a.tpend = wcap ? tpend.as<uint8_t>() : nullptr;
+        a.tinit = wcap ? tinit.as<uint8_t>() : nullptr;
         return hipSuccess;
     }
 };
@@ -408,7 +428,10 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
         LbCtl c;
         if ((e = hipMemcpyAsync(&c, L->a.ctl, sizeof c, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-        fprintf(stderr, "[s3hc lb] blocks %u chunks %u\n", c.nlb, c.nchunks);
+        fprintf(stderr, "[s3hc lb] blocks %u chunks %u spread tiles %u pending tiles per round", c.nlb, c.nchunks,
+                c.ntiles);
+        for (uint32_t r = 0; r <= kLbwRounds; ++r) fprintf(stderr, " %u", c.rflag[r]);
+        fprintf(stderr, "\n");
     }
     return hipSuccess;
 }
@@ -755,6 +778,7 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
                 const uint32_t nl = dst_cap[i] / 65536u + 1u;
                 lc.lb += nl;
                 lc.chunks += frame_len[i] / kLbChunk + nl;
+                lc.outb += dst_cap[i];
             }
         } else {
             for (uint32_t i = 0; i < n; ++i) {
@@ -762,6 +786,7 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
                 const uint32_t nl = dst_cap[i] / 262144u + 1u;
                 lc.lb += nl;
                 lc.chunks += frame_len[i] / kLbChunk + nl;
+                lc.outb += dst_cap[i];
             }
         }
         HIPCHK(P->lb.prepare(P->blk_cap, P->blk_cap, lc));
@@ -1135,7 +1160,7 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         LbCaps lc;
         if (W.blocks.size() <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
         for (auto& U : units)
-            if (lb_candidate(W.blocks[U.first], U.n == 1, lc.min_limit)) lc.add_block(W.blocks[U.first].csize);
+            if (lb_candidate(W.blocks[U.first], U.n == 1, lc.min_limit)) lc.add_block(W.blocks[U.first].csize, std::min(W.blocks[U.first].limit, W.blocks[U.first].cap));
         HIPCHK(ctx->lb.prepare((uint32_t)units.size(), (uint32_t)nb, lc));
         const uint64_t* bh = nullptr;
         HTRACE("launch")
@@ -1756,7 +1781,7 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
         LbCaps lc;
         if (nbk <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
         for (auto& U : units)
-            if (lb_candidate(mb[U.first], U.n == 1, lc.min_limit)) lc.add_block(mb[U.first].csize);
+            if (lb_candidate(mb[U.first], U.n == 1, lc.min_limit)) lc.add_block(mb[U.first].csize, std::min(mb[U.first].limit, mb[U.first].cap));
         HIPCHK(S.lb.prepare(nu, nbk, lc));
     }
     HIPCHK(S.h_res.ensure(8ull * n));

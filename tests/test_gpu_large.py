@@ -4,7 +4,9 @@ Frames that allow blocks above 64 KiB (BD 0x50 / 0x70) are what the reference wr
 own cache files (flush_batch compresses ~1 MiB batches with lz4_flex BlockSize::Auto,
 disk_cache.rs:1820-1870); their blocks are decoded by many workgroups each. Bar: decoded bytes
 bit-exact with the oracle, statuses identical to the oracle's on corrupt inputs, and identical
-to the one-wave decoder (S3HC_LB_DISABLE=1) on every input.
+to the one-wave decoder (S3HC_LB_DISABLE=1) on every input. Few-block launches run the spread
+execution (k_lbw_*: all tiles of a block at once, global pointer jumping); S3HC_LBW_DISABLE=1 sends
+the same blocks through the step loop (k_lb_run), and S3HC_LBW_CAP splits one launch between both.
 """
 import os
 import random
@@ -67,12 +69,20 @@ def _data(name):
     return _CACHE[name]
 
 
-def _wave_path(fn):
-    os.environ["S3HC_LB_DISABLE"] = "1"
+def _with_env(var, value, fn):
+    os.environ[var] = value
     try:
         return fn()
     finally:
-        del os.environ["S3HC_LB_DISABLE"]
+        del os.environ[var]
+
+
+def _wave_path(fn):
+    return _with_env("S3HC_LB_DISABLE", "1", fn)
+
+
+def _step_path(fn):  # large blocks through k_lb_run instead of the spread execution
+    return _with_env("S3HC_LBW_DISABLE", "1", fn)
 
 
 @pytest.mark.parametrize("name", sorted(INPUTS))
@@ -80,6 +90,7 @@ def test_lb_decodes_oracle_frames(engine, oracle, name):
     data = _data(name)
     frame = oracle.lz4flex_compress_frame(data)
     assert engine.decompress_frames(frame) == data
+    assert _step_path(lambda: engine.decompress_frames(frame)) == data
 
 
 @pytest.mark.parametrize("name", sorted(INPUTS))
@@ -136,8 +147,9 @@ def test_lb_random_corruption_matches_oracle_and_wave_path(engine, oracle):
         st_o, out_o = oracle.decompress_status(blob)
         st_g, out_g = engine.decompress_status(blob)
         st_w, out_w = _wave_path(lambda: engine.decompress_status(blob))
-        assert st_g == st_o == st_w, (t, kind)
-        assert out_g == out_o == out_w
+        st_s, out_s = _step_path(lambda: engine.decompress_status(blob))
+        assert st_g == st_o == st_w == st_s, (t, kind)
+        assert out_g == out_o == out_w == out_s
         n_err += st_o != 0
     assert n_err > 50
 
@@ -228,7 +240,7 @@ def test_lb_dst_too_small_matches_wave_path(engine, oracle, short):
     caps = [len(parts[0]) - short, len(parts[1]), len(parts[2]) - short]
     got = _decode_dev(engine, frames, caps)
     want = _wave_path(lambda: _decode_dev(engine, frames, caps))
-    assert got == want
+    assert got == want == _step_path(lambda: _decode_dev(engine, frames, caps))
     assert got[0][0] == 3 and got[0][1] == 0 and got[0][2] == 3  # S3HC_DST_TOO_SMALL
 
 
@@ -257,3 +269,45 @@ def test_lb_randomized_structures_match_wave_path(engine, oracle):
             got = engine.decompress_frames(frame)
             assert got == data, case
             assert _wave_path(lambda: engine.decompress_frames(frame)) == data, case
+            assert _step_path(lambda: engine.decompress_frames(frame)) == data, case
+
+
+@pytest.mark.parametrize("rounds", ["0", "1", "2"])
+def test_lb_spread_gather_walks_unfinished_chains(engine, oracle, rounds):
+    # with fewer pointer-jumping launches than the chains need, k_lbw_gather walks the rest
+    for name in ("deep_1MiB", "log_1MiB", "runs_2MiB", "p251_1MiB+1"):
+        data = _data(name)
+        frame = oracle.lz4flex_compress_frame(data)
+        assert _with_env("S3HC_LBW_ROUNDS", rounds, lambda: engine.decompress_frames(frame)) == data, name
+
+
+@pytest.mark.parametrize("cap", [0, 1, 1_500_000, 3 * MiB])
+def test_lb_spread_cap_splits_launch(engine, oracle, cap):
+    # P capacity below the launch's output: the first blocks run spread, the rest the step loop
+    # (cap 0 = spread execution off), all in one decode launch
+    parts = [_data("log_1MiB"), _data("deep_1MiB"), _data("zeros_1MiB+7"), _data("json_1MiB"), _data("runs_2MiB")]
+    frames = [oracle.lz4flex_compress_frame(p) for p in parts]
+    blob = b"".join(frames)
+    assert _with_env("S3HC_LBW_CAP", str(cap), lambda: engine.decompress_frames(blob)) == b"".join(parts)
+
+
+def test_lb_spread_many_frames_device_plan(engine):
+    # 32 reference-format 1 MiB frames in one device launch (every tile of every block at once)
+    data = synth.log_text(16 * MiB, 60) + _deep_chain(8 * MiB, 61) + bytes(4 * MiB) + synth.json_records(4 * MiB, 62)
+    import oracle as O
+
+    frames = [O.lz4flex_compress_frame(data[i:i + MiB]) for i in range(0, len(data), MiB)]
+    n = len(frames)
+    fo = [sum(len(f) for f in frames[:i]) for i in range(n)]
+
+    def run():
+        plan = engine.plan_decode(fo, [len(f) for f in frames], [i * MiB for i in range(n)], [MiB] * n)
+        src = engine.upload(b"".join(frames))
+        dst = engine.alloc(n * MiB + 64)
+        olen, st = engine.alloc(4 * n), engine.alloc(4 * n)
+        engine.decode_dev(plan, src, dst, olen, st)
+        engine.sync()
+        return st.i32(n), olen.u32(n), dst.read(n * MiB)
+
+    assert run() == ([0] * n, [MiB] * n, data)
+    assert _step_path(run) == ([0] * n, [MiB] * n, data)
