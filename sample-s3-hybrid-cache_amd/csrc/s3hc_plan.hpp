@@ -93,7 +93,10 @@ struct DecUnit {         // a run of blocks decoded in order by one wave
 // lane), resolving each step's match chains in LDS by pointer jumping against a 64 KiB ring of
 // recent output, while its 16th wave hashes the flushed output (the frame's content xxh32 when
 // the block is the whole frame).
-constexpr uint32_t kLbChunk = 16384;      // compressed positions per tokenizing workgroup
+#ifndef S3HC_LB_CHUNK  // (diagnostic builds try other sizes)
+#define S3HC_LB_CHUNK 8192  // A/B (tools_lbchunk_ab.sh): 1 MiB frame 0.98 -> 0.90 ms, 16 and 256 frames equal; 4096 loses at 256
+#endif
+constexpr uint32_t kLbChunk = S3HC_LB_CHUNK;  // compressed positions per tokenizing workgroup
 constexpr uint32_t kLbStep = 7680;        // output bytes per step of the executing workgroup
 constexpr uint32_t kLbMaxSteps = 547;     // steps of one block (ceil(4 MiB / kLbStep))
 constexpr uint32_t kLbMinLimit = 65537;   // frame max block size above 64 KiB selects the path
