@@ -51,7 +51,6 @@ constexpr uint32_t END = 0xFFFFFFFEu;          // next-token value: last sequenc
 constexpr uint32_t BAD = 0xFFFFFFFFu;          // next-token value: malformed token
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t INF = 0xFFFFFFFFu;
-constexpr uint32_t kLevels = 13;               // 2^13 > kLbChunk / 3 tokens in a chunk
 constexpr uint32_t kXT = 960;                  // decoding threads of an executing workgroup (15 waves)
 constexpr uint32_t kXWG = kXT + 64;            // + one hashing wave
 constexpr uint32_t kXPer = kLbStep / kXT;      // output bytes per executing thread per step (8)
@@ -85,7 +84,7 @@ constexpr uint32_t FIN = 0xFFFFFFFFu;          // source pointer of a final byte
 // diagnostic builds: k_lb_run phase times (s_memtime sums of every workgroup's thread 0):
 // 0 owners, 1 classify + literal loads, 2 ring/pointer stores, 3 next step's sequences,
 // 4 chain jumping, 5 flush, 6 -, 7 steps, 8 jump rounds, 9 loop top
-__device__ unsigned long long g_lbprof[12];
+__device__ unsigned long long g_lbprof[20];  // 12..17: k_lb_mark phases (thread 0 of each chunk)
 #endif
 
 namespace {
@@ -376,11 +375,23 @@ __global__ void k_lb_entry(LbArgs A) {
 }
 
 // ---------------------------------------------------------------- token marks
+// The chain from the chunk's entry is found in three steps instead of pointer doubling over the
+// whole chunk: (A) every position learns where its chain leaves its 128-position sub-range (jumping
+// inside the sub-range: <= 43 tokens, so a few levels), (B) one thread hops from sub-range to
+// sub-range from the entry (<= kSubs hops), (C) one lane per sub-range walks the chain inside it and
+// marks the tokens (about 20 hops). Positions are chunk-relative; J0[r] == r: the chain leaves
+// the chunk (or ends) after r.
+namespace lb {
+constexpr uint32_t kSub = 128;                  // positions per sub-range
+constexpr uint32_t kSubs = kLbChunk / kSub;     // sub-ranges per chunk
+static_assert(kSubs <= 64, "one lane per sub-range");
+}  // namespace lb
 __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ src, LbArgs A) {
     using namespace lb;
     __shared__ __attribute__((aligned(16))) uint8_t raw[kStage + 16];
-    __shared__ uint16_t Ja[kLbChunk], Jb[kLbChunk];
+    __shared__ uint16_t J[kLbChunk], X[kLbChunk];
     __shared__ uint8_t mk[kLbChunk];
+    __shared__ uint16_t first[kSubs];
     __shared__ uint32_t shc[16];
     __shared__ uint64_t shs[16];
     __shared__ uint32_t bad_s;
@@ -393,42 +404,69 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
             for (uint32_t w = threadIdx.x; w < kWords; w += kT) A.bits[(size_t)c * kWords + w] = 0;
         return;
     }
+#ifdef S3HC_LBPROF
+    uint64_t mt = __builtin_amdgcn_s_memtime();
+#define MK_T(k) { __syncthreads(); const uint64_t n_ = __builtin_amdgcn_s_memtime(); if (threadIdx.x == 0) atomicAdd(&g_lbprof[12 + (k)], (unsigned long long)(n_ - mt)); mt = n_; }
+#else
+#define MK_T(k)
+#endif
     const LbBlock B = A.lbt[A.chunk_blk[c]];
     const uint32_t cs = (c - B.chunk0) * kLbChunk;
     const uint32_t n = B.C - cs < kLbChunk ? B.C - cs : kLbChunk;
     const LbView v = lb_view(src, B, A.nzg, cs, lb_stage(src + B.src_off, cs, B.C - cs < kStage ? B.C - cs : kStage, raw));
     if (threadIdx.x == 0) bad_s = NONE;
-    __syncthreads();
+    if (threadIdx.x < kSubs) first[threadIdx.x] = 0xFFFFu;
     for (uint32_t k = 0; k < kPer; ++k) {
         const uint32_t r = threadIdx.x + k * kT;
         if (r < n) {
-            Ja[r] = A.J0[(size_t)c * kLbChunk + r];
-            mk[r] = r == e ? 1 : 0;
+            const uint16_t j = A.J0[(size_t)c * kLbChunk + r];
+            J[r] = j;
+            X[r] = j;
+            mk[r] = 0;
         }
     }
-    // marks reachable from the entry: level k adds J_k(T_k) with J_k = nxt^(2^k) (exact powers:
-    // the jump table is double-buffered; marks may be set early, they are still chain nodes)
-    uint16_t* Jc = Ja;
-    uint16_t* Jn = Jb;
-    // a level that adds no mark ends the marking: J_(k+1) = J_k o J_k then maps the marked set
-    // into itself too
     __syncthreads();
-    for (uint32_t lev = 0; lev < kLevels; ++lev) {
-        bool added = false;
+    MK_T(0)
+    // (A) X[r]: the first chain node after r outside r's sub-range, or the node the chain ends on
+    // inside it (values only move forward along the chain: reading a fresher one is harmless)
+    for (uint32_t lev = 0; lev < 8; ++lev) {
+        bool ch = false;
         for (uint32_t k = 0; k < kPer; ++k) {
             const uint32_t r = threadIdx.x + k * kT;
             if (r < n) {
-                const uint32_t j = Jc[r];
-                if (mk[r] && !mk[j]) {
-                    mk[j] = 1;
-                    added = true;
+                const uint32_t j = X[r];
+                if (j != r && j / kSub == r / kSub) {
+                    const uint32_t jj = X[j];
+                    if (jj != j) { X[r] = (uint16_t)jj; ch = true; }
                 }
-                Jn[r] = Jc[j];
             }
         }
-        uint16_t* tmp = Jc; Jc = Jn; Jn = tmp;
-        if (!__syncthreads_or(added)) break;
+        if (!__syncthreads_or(ch)) break;
     }
+    MK_T(1)
+    // (B) the chain's first node in each sub-range it visits
+    if (threadIdx.x == 0) {
+        uint32_t cur = e;
+        while (true) {
+            first[cur / kSub] = (uint16_t)cur;
+            const uint32_t nx = X[cur];
+            if (nx == cur || nx / kSub == cur / kSub) break;  // the chain ends inside this sub-range
+            cur = nx;
+        }
+    }
+    __syncthreads();
+    // (C) lane s walks the chain inside sub-range s
+    if (threadIdx.x < kSubs && first[threadIdx.x] != 0xFFFFu) {
+        uint32_t cur = first[threadIdx.x];
+        while (true) {
+            mk[cur] = 1;
+            const uint32_t nx = J[cur];
+            if (nx == cur || nx / kSub != threadIdx.x) break;
+            cur = nx;
+        }
+    }
+    __syncthreads();
+    MK_T(2)
     uint32_t cnt = 0;
     uint64_t sl = 0;
     for (uint32_t k = 0; k < kPer; ++k) {
@@ -453,10 +491,13 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
             A.bits[(size_t)c * kWords + w0 + 1] = (uint32_t)(bm >> 32);
         }
     }
+    MK_T(3)
     uint32_t ctot;
     uint64_t stot;
     (void)wg_excl_add<uint32_t, 16>(cnt, shc, ctot);
     (void)wg_excl_add<uint64_t, 16>(sl, shs, stot);
+    MK_T(4)
+#undef MK_T
     if (threadIdx.x == 0) {
         A.ntok[c] = ctot;
         A.slsum[c] = stot < 0xFFFFFFFFull ? (uint32_t)stot : 0xFFFFFFFFu;
@@ -1275,7 +1316,7 @@ hipError_t launch_lb_exec(const LbArgs& A, const uint8_t* src, uint8_t* dst, hip
             hipLaunchKernelGGL(k_lbw_round, dim3(tiles < 512u ? tiles : 512u), dim3(lb::kXT), 0, st, A, r);
         hipLaunchKernelGGL(k_lbw_gather, dim3(tiles < 1024u ? tiles : 1024u), dim3(lb::kXT), 0, st, dst, A);
     }
-    hipLaunchKernelGGL(k_lb_run, dim3(A.lb_cap), dim3(lb::kXWG), 0, st, src, dst, A);
+    if (!A.all_spread) hipLaunchKernelGGL(k_lb_run, dim3(A.lb_cap), dim3(lb::kXWG), 0, st, src, dst, A);
     return hipGetLastError();
 }
 }  // namespace s3hc
@@ -1283,9 +1324,9 @@ hipError_t launch_lb_exec(const LbArgs& A, const uint8_t* src, uint8_t* dst, hip
 #ifdef S3HC_LBPROF
 extern "C" int s3hc_diag_lbprof(unsigned long long* out, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(s3hc::g_lbprof), sizeof(unsigned long long) * 12) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(s3hc::g_lbprof), sizeof(unsigned long long) * 20) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[12] = {0};
+        unsigned long long z[20] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(s3hc::g_lbprof), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

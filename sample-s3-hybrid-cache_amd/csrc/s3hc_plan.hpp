@@ -103,9 +103,9 @@ constexpr uint32_t kLbMinLimit = 65537;   // frame max block size above 64 KiB s
 constexpr uint32_t kLbFewBlocks = 256;    // batches with at most this many blocks: every compressed
                                           // independent block takes the path (latency: one wave per
                                           // 64 KiB block needs 0.85 ms)
-constexpr uint32_t kLbwRounds = 6;        // spread execution: pointer-jumping launches (k_lbw_gather
+constexpr uint32_t kLbwRounds = 4;        // spread execution: pointer-jumping launches (k_lbw_gather
                                           // walks whatever chains they leave)
-constexpr uint32_t kLbwHops = 4;          // ... hops per byte and launch, at most
+constexpr uint32_t kLbwHops = 8;          // ... hops per byte and launch, at most
 constexpr uint32_t kLbwCapMax = 1u << 30; // spread execution: pointer-array positions, at most
 constexpr uint32_t kLbwMaxBlocks = 64;        // ... and so do launches of more blocks than this
 constexpr uint32_t kLbwMaxOut = 96u << 20;     // launches whose large blocks may decode to more than
@@ -134,7 +134,7 @@ struct LbArgs {
     uint32_t min_limit;    // frame max block size that selects the path (kLbMinLimit; 1 for few-block batches)
     uint32_t wcap;         // spread execution: positions of P (0: every block runs the step loop)
     uint32_t tile_cap;     // spread execution: tiles (kLbStep output bytes) of the spread blocks, at most
-    uint32_t pad2;
+    uint32_t all_spread;   // the host's bounds show every taken block runs spread: no k_lb_run launch
     LbBlock* lbt;
     LbCtl* ctl;
     uint8_t* unit_lb;      // per unit: 1 = decoded by this path

@@ -400,6 +400,9 @@ struct LbScratch {
         a.blk_hash = blk_hash.as<uint64_t>();
         a.wcap = (uint32_t)wcap;
         a.tile_cap = (uint32_t)tcap;
+        // every taken block spreads when the candidates (an upper bound) are few enough and their
+        // decoded bytes (an upper bound) fit P (k_lbw_plan's rule)
+        a.all_spread = wcap && c.lb <= kLbwMaxBlocks && c.outb <= wcap ? 1u : 0u;
         a.wbase = wcap ? wbase.as<uint32_t>() : nullptr;
         a.wtile0 = wcap ? wtile0.as<uint32_t>() : nullptr;
         a.P = wcap ? wP.as<uint32_t>() : nullptr;

@@ -72,13 +72,15 @@ def main():
         print(json.dumps(case(eng, data, MiB, reps=2)))
         if hasattr(S.lib, "s3hc_diag_lbprof"):  # diagnostic build: k_lb_run phase times per step
             import ctypes
-            buf = (ctypes.c_ulonglong * 12)()
+            buf = (ctypes.c_ulonglong * 20)()
             S.lib.s3hc_diag_lbprof(buf, 1)
             v = list(buf)
             steps = max(v[7], 1)
             names = ["owners", "classify_loads", "stores", "next_seqs", "jumps", "flush", "-", "steps",
                      "jump_rounds", "loop_top", "jump_top_barrier", "jump_work_t0"]
             print(json.dumps({nm: (round(v[k] / steps, 1) if k not in (7,) else v[k]) for k, nm in enumerate(names)}))
+            # k_lb_mark phases (cycles summed over chunks): load/stage, sub-range jumps, walks, tokenize, scans
+            print(json.dumps({"mark_phases_Mcycles": [round(x / 1e6, 2) for x in v[12:17]]}))
         return
     for n in (1, 4, 16, 64, 256):
         out[f"log_1MiB_x{n}"] = case(eng, text[:n * MiB], MiB)
