@@ -536,14 +536,23 @@ __global__ __launch_bounds__(1024) void k_lb_seq(const uint8_t* __restrict__ src
     const uint32_t r0 = kPer * threadIdx.x;
     const uint32_t wv = A.bits[(size_t)c * kWords + (r0 >> 5)];
     const uint32_t m = (wv >> (r0 & 31u)) & ((1u << kPer) - 1u);
+    // tokens of a chain are >= 3 positions apart, so a thread's kPer = 8 positions hold <= 3: they
+    // are parsed once and kept in registers for the second pass
+    static_assert(kPer <= 9, "at most 3 tokens per thread");
+    uint32_t tl[3], tll[3], tml[3], tof[3];
+    bool tlast[3];
     uint32_t cnt = 0;
     uint64_t sl = 0;
+#pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
         if ((m >> k) & 1u) {
             const LbTok T = lb_token(v, cs + r0 + k);
-            ++cnt;
             const uint64_t s = (uint64_t)T.ll + T.ml;
             sl += s < (uint64_t)B.limit + 1u ? s : (uint64_t)B.limit + 1u;
+#pragma unroll
+            for (uint32_t i = 0; i < 3; ++i)
+                if (cnt == i) { tl[i] = T.lit; tll[i] = T.ll; tml[i] = T.ml; tof[i] = T.off; tlast[i] = T.nxt == END; }
+            ++cnt;
         }
     }
     uint32_t ctot;
@@ -556,10 +565,12 @@ __global__ __launch_bounds__(1024) void k_lb_seq(const uint8_t* __restrict__ src
     const uint32_t brank0 = (uint32_t)(gbase - tb0);
     uint64_t produced = A.outbase[c] - ob0 + opre;
     uint32_t bad = 0xFFFFFFFFu;
-    for (uint32_t k = 0; k < kPer; ++k) {
-        if ((m >> k) & 1u) {
-            const LbTok S = lb_token(v, cs + r0 + k);
-            const bool last = S.nxt == END;
+#pragma unroll
+    for (uint32_t i = 0; i < 3; ++i) {
+        if (i < cnt) {
+            LbTok S;
+            S.lit = tl[i]; S.ll = tll[i]; S.ml = tml[i]; S.off = tof[i];
+            const bool last = tlast[i];
             const uint32_t st = lb_check(produced, S.ll, S.ml, S.off, last, B.limit, B.cap);
             const uint32_t br = brank0 + rank;
             if (st != S3HC_OK && bad == 0xFFFFFFFFu) bad = (br << 3) | st;
@@ -987,16 +998,22 @@ __global__ __launch_bounds__(1024) void k_lbw_plan(LbArgs A) {
     if (t == 0) { cpos = 0; ctile = 0; }
     __syncthreads();
     const uint32_t nlb = A.ctl->nlb;
+    // blocks of frames that allow more than 64 KiB spread (small blocks gain little from it and
+    // lose the step loop's overlap with other queues), and only when there are few of them
+    uint32_t nbig = 0;
+    for (uint32_t i = t; i < nlb; i += 1024) nbig += A.lbt[i].limit > 65536u ? 1u : 0u;
+    uint32_t totbig;
+    (void)wg_excl_add<uint32_t, 16>(nbig, sht, totbig);
+    const bool few = totbig <= kLbwMaxBlocks;
     for (uint32_t base = 0; base < nlb; base += 1024) {
         const uint32_t i = base + t;
-        const bool ok = i < nlb && A.lb_stat[i] == S3HC_OK && A.lb_size[i] > 0;
+        const bool ok = few && i < nlb && A.lb_stat[i] == S3HC_OK && A.lb_size[i] > 0 && A.lbt[i].limit > 65536u;
         const uint32_t size = ok ? A.lb_size[i] : 0u;
         uint64_t tots;
         uint32_t tott;
         // positions grow with the block index, so the spread blocks are a prefix of the decodable ones
         const uint64_t pp = wg_excl_add<uint64_t, 16>((uint64_t)size, shs, tots) + cpos;
-        // (with more than kLbwMaxBlocks blocks the step loop has a block for most CUs: spread off)
-        const bool wide = ok && pp + size <= A.wcap && nlb <= kLbwMaxBlocks;
+        const bool wide = ok && pp + size <= A.wcap;
         const uint32_t nt = wide ? (size + kLbStep - 1) / kLbStep : 0u;
         const uint32_t tp = wg_excl_add<uint32_t, 16>(nt, sht, tott) + ctile;
         if (i < nlb) {

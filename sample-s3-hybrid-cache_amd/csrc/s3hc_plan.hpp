@@ -107,7 +107,9 @@ constexpr uint32_t kLbwRounds = 4;        // spread execution: pointer-jumping l
                                           // walks whatever chains they leave)
 constexpr uint32_t kLbwHops = 8;          // ... hops per byte and launch, at most
 constexpr uint32_t kLbwCapMax = 1u << 30; // spread execution: pointer-array positions, at most
-constexpr uint32_t kLbwMaxBlocks = 64;        // ... and so do launches of more blocks than this
+constexpr uint32_t kLbwMaxBlocks = 16;        // ... and so do launches of more large blocks than this:
+                                              // the step loop's one workgroup per block lets the reader's
+                                              // queues overlap batches (config-4 A/B, §4b)
 constexpr uint32_t kLbwMaxOut = 96u << 20;     // launches whose large blocks may decode to more than
                                               // this run the step loop (k_lb_run): with a block per CU
                                               // it is as fast, and P stays small (measured, §4b)

@@ -344,10 +344,15 @@ struct LbCaps {
     uint32_t lb = 0, chunks = 0;
     uint32_t min_limit = kLbMinLimit;
     uint64_t outb = 0;  // decoded bytes of the candidate blocks, at most (sizes the spread execution)
-    void add_block(uint32_t csize, uint32_t out_bound) {
+    bool exact = false; // lb is the candidate count itself (host walk), not a bound (device plans)
+    uint32_t nbig = 0;  // candidates of frames that allow more than 64 KiB (the spread ones; exact only)
+    void add_block(uint32_t csize, uint32_t out_bound, uint32_t limit) {
         ++lb;
         chunks += (csize + kLbChunk - 1) / kLbChunk;
-        outb += std::min<uint64_t>(out_bound, (uint64_t)kLbMaxSteps * kLbStep);
+        if (limit > 65536u) {
+            ++nbig;
+            outb += std::min<uint64_t>(out_bound, (uint64_t)kLbMaxSteps * kLbStep);
+        }
     }
 };
 static bool lb_candidate(const DecBlock& D, bool unit_single, uint32_t min_limit) {
@@ -379,7 +384,8 @@ struct LbScratch {
         // S3HC_LBW_DISABLE=1 turns it off
         uint64_t wcap = c.outb <= kLbwMaxOut ? c.outb : 0;
         if (const char* ev = getenv("S3HC_LBW_CAP")) wcap = std::min<uint64_t>(c.outb, strtoull(ev, nullptr, 10));
-        if (getenv("S3HC_LBW_DISABLE")) wcap = 0;
+        // (a host walk knows its candidates: no spread launches that would find nothing to do)
+        if (getenv("S3HC_LBW_DISABLE") || (c.exact && (c.nbig == 0 || c.nbig > kLbwMaxBlocks))) wcap = 0;
         wcap = std::min<uint64_t>(wcap, kLbwCapMax);
         const size_t tcap = wcap ? wcap / kLbStep + nlb + 1 : 0;
         if (wcap) {
@@ -402,7 +408,7 @@ struct LbScratch {
         a.tile_cap = (uint32_t)tcap;
         // every taken block spreads when the candidates (an upper bound) are few enough and their
         // decoded bytes (an upper bound) fit P (k_lbw_plan's rule)
-        a.all_spread = wcap && c.lb <= kLbwMaxBlocks && c.outb <= wcap ? 1u : 0u;
+        a.all_spread = wcap && c.exact && c.nbig == c.lb && c.nbig <= kLbwMaxBlocks && c.outb <= wcap ? 1u : 0u;
         a.wbase = wcap ? wbase.as<uint32_t>() : nullptr;
         a.wtile0 = wcap ? wtile0.as<uint32_t>() : nullptr;
         a.P = wcap ? wP.as<uint32_t>() : nullptr;
@@ -1162,8 +1168,9 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         HIPCHK(ctx->d_blk_status.ensure(nb * 4));
         LbCaps lc;
         if (W.blocks.size() <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
+        lc.exact = true;
         for (auto& U : units)
-            if (lb_candidate(W.blocks[U.first], U.n == 1, lc.min_limit)) lc.add_block(W.blocks[U.first].csize, std::min(W.blocks[U.first].limit, W.blocks[U.first].cap));
+            if (lb_candidate(W.blocks[U.first], U.n == 1, lc.min_limit)) lc.add_block(W.blocks[U.first].csize, std::min(W.blocks[U.first].limit, W.blocks[U.first].cap), W.blocks[U.first].limit);
         HIPCHK(ctx->lb.prepare((uint32_t)units.size(), (uint32_t)nb, lc));
         const uint64_t* bh = nullptr;
         HTRACE("launch")
@@ -1783,8 +1790,9 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
         // large blocks of the batch (the host walk knows every block)
         LbCaps lc;
         if (nbk <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
+        lc.exact = true;
         for (auto& U : units)
-            if (lb_candidate(mb[U.first], U.n == 1, lc.min_limit)) lc.add_block(mb[U.first].csize, std::min(mb[U.first].limit, mb[U.first].cap));
+            if (lb_candidate(mb[U.first], U.n == 1, lc.min_limit)) lc.add_block(mb[U.first].csize, std::min(mb[U.first].limit, mb[U.first].cap), mb[U.first].limit);
         HIPCHK(S.lb.prepare(nu, nbk, lc));
     }
     HIPCHK(S.h_res.ensure(8ull * n));
