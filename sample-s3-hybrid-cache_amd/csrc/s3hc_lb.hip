@@ -46,7 +46,7 @@ constexpr uint32_t kLook = 2048;               // staged bytes past the chunk
 constexpr uint32_t kStage = kLbChunk + kLook;  // staged bytes per chunk
 constexpr uint32_t kGran = 64;                 // 255-run index granule
 constexpr uint32_t kGpc = kLbChunk / kGran;    // granules per chunk
-constexpr uint32_t kWords = kLbChunk / 32;     // bitmap words per chunk
+constexpr uint32_t kTokSlot = kLbTokSlot;       // token records per chunk (trec)
 constexpr uint32_t END = 0xFFFFFFFEu;          // next-token value: last sequence
 constexpr uint32_t BAD = 0xFFFFFFFFu;          // next-token value: malformed token
 constexpr uint32_t NONE = 0xFFFFFFFFu;
@@ -400,8 +400,6 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
     const uint32_t e = live ? A.entry[c] : NONE;
     if (e == NONE) {  // no token of the block starts in this chunk (or a chunk beyond the count)
         if (threadIdx.x == 0) { A.ntok[c] = 0; A.slsum[c] = 0; A.badrel[c] = NONE; }
-        if (live)
-            for (uint32_t w = threadIdx.x; w < kWords; w += kT) A.bits[(size_t)c * kWords + w] = 0;
         return;
     }
 #ifdef S3HC_LBPROF
@@ -467,28 +465,32 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
     }
     __syncthreads();
     MK_T(2)
+    // the chunk's tokens in position order: thread t parses positions [kPer*t, kPer*t + kPer) and
+    // writes their records at their rank in the chunk's slot of trec, so k_lb_seq only scans.
+    // Ranks come from the marks alone: the one marked position that is not a token (the
+    // malformed token ending a corrupt chain) is the chain's last node, after every token.
+    const uint32_t r0 = kPer * threadIdx.x;
+    uint32_t nm = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) nm += (r0 + k < n && mk[r0 + k]) ? 1u : 0u;
+    uint32_t mtot;
+    uint32_t rank = wg_excl_add<uint32_t, 16>(nm, shc, mtot);
     uint32_t cnt = 0;
     uint64_t sl = 0;
     for (uint32_t k = 0; k < kPer; ++k) {
-        const uint32_t r = threadIdx.x + k * kT;
-        bool tok = false;
+        const uint32_t r = r0 + k;
         if (r < n && mk[r]) {
             const LbTok T = lb_token(v, cs + r);
             if (T.nxt == BAD) {
                 bad_s = r;  // the chain's last node (unique)
             } else {
-                tok = true;
+                const uint64_t s1 = (uint64_t)T.ll + T.ml;
+                sl += s1 < (uint64_t)B.limit + 1u ? s1 : (uint64_t)B.limit + 1u;
+                A.trec[(size_t)c * kTokSlot + rank] =
+                    make_uint4(T.lit | (T.nxt == END ? 0x80000000u : 0u), T.ll, T.ml, T.off);  // lit < 2^31
+                ++rank;
                 ++cnt;
-                const uint64_t s = (uint64_t)T.ll + T.ml;
-                sl += s < (uint64_t)B.limit + 1u ? s : (uint64_t)B.limit + 1u;
             }
-        }
-        const uint64_t bm = __ballot(tok);
-        // wave w covers positions k*kT + 64w .. +63
-        if (lane64() == 0) {
-            const uint32_t w0 = (k * kT + (threadIdx.x & ~63u)) >> 5;
-            A.bits[(size_t)c * kWords + w0] = (uint32_t)bm;
-            A.bits[(size_t)c * kWords + w0 + 1] = (uint32_t)(bm >> 32);
         }
     }
     MK_T(3)
@@ -521,43 +523,24 @@ __device__ __forceinline__ uint32_t lb_check(uint64_t produced, uint32_t ll, uin
 
 __global__ __launch_bounds__(1024) void k_lb_seq(const uint8_t* __restrict__ src, LbArgs A) {
     using namespace lb;
-    __shared__ __attribute__((aligned(16))) uint8_t raw[kStage + 16];
-    __shared__ uint32_t shc[16];
     __shared__ uint64_t shs[16];
     const uint32_t c = blockIdx.x;
     if (c >= A.ctl->nchunks || A.entry[c] == NONE) return;
     const uint32_t bi = A.chunk_blk[c];
     const LbBlock B = A.lbt[bi];
     const uint32_t cs = (c - B.chunk0) * kLbChunk;
-    const uint32_t n = B.C - cs < kLbChunk ? B.C - cs : kLbChunk;
-    const LbView v = lb_view(src, B, A.nzg, cs, lb_stage(src + B.src_off, cs, B.C - cs < kStage ? B.C - cs : kStage, raw));
-    __syncthreads();
-    // thread t owns positions [kPer*t, kPer*t + kPer) (contiguous: ranks follow position order)
-    const uint32_t r0 = kPer * threadIdx.x;
-    const uint32_t wv = A.bits[(size_t)c * kWords + (r0 >> 5)];
-    const uint32_t m = (wv >> (r0 & 31u)) & ((1u << kPer) - 1u);
-    // tokens of a chain are >= 3 positions apart, so a thread's kPer = 8 positions hold <= 3: they
-    // are parsed once and kept in registers for the second pass
-    static_assert(kPer <= 9, "at most 3 tokens per thread");
-    uint32_t tl[3], tll[3], tml[3], tof[3];
-    bool tlast[3];
-    uint32_t cnt = 0;
+    const uint32_t ntc = A.ntok[c];
+    // thread t: the chunk's tokens [3t, 3t + 3) (records written by k_lb_mark, in stream order)
+    static_assert(3 * kT >= kTokSlot, "three records per thread cover a chunk");
+    const uint32_t i0 = 3 * threadIdx.x;
     uint64_t sl = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {
-        if ((m >> k) & 1u) {
-            const LbTok T = lb_token(v, cs + r0 + k);
-            const uint64_t s = (uint64_t)T.ll + T.ml;
-            sl += s < (uint64_t)B.limit + 1u ? s : (uint64_t)B.limit + 1u;
-#pragma unroll
-            for (uint32_t i = 0; i < 3; ++i)
-                if (cnt == i) { tl[i] = T.lit; tll[i] = T.ll; tml[i] = T.ml; tof[i] = T.off; tlast[i] = T.nxt == END; }
-            ++cnt;
-        }
+    for (uint32_t i = 0; i < 3; ++i) {
+        const uint32_t* rw = (const uint32_t*)&A.trec[(size_t)c * kTokSlot + i0 + i];
+        const uint64_t s1 = i0 + i < ntc ? (uint64_t)rw[1] + rw[2] : 0u;
+        sl += s1 < (uint64_t)B.limit + 1u ? s1 : (uint64_t)B.limit + 1u;
     }
-    uint32_t ctot;
     uint64_t stot;
-    uint32_t rank = wg_excl_add<uint32_t, 16>(cnt, shc, ctot);
     uint64_t opre = wg_excl_add<uint64_t, 16>(sl, shs, stot);
     const uint64_t tb0 = A.tokbase[B.chunk0];
     const uint64_t ob0 = A.outbase[B.chunk0];
@@ -567,10 +550,12 @@ __global__ __launch_bounds__(1024) void k_lb_seq(const uint8_t* __restrict__ src
     uint32_t bad = 0xFFFFFFFFu;
 #pragma unroll
     for (uint32_t i = 0; i < 3; ++i) {
-        if (i < cnt) {
+        if (i0 + i < ntc) {
+            const uint4 rec = A.trec[(size_t)c * kTokSlot + i0 + i];  // (second read: L2)
             LbTok S;
-            S.lit = tl[i]; S.ll = tll[i]; S.ml = tml[i]; S.off = tof[i];
-            const bool last = tlast[i];
+            S.lit = rec.x & 0x7FFFFFFFu; S.ll = rec.y; S.ml = rec.z; S.off = rec.w;
+            const bool last = (rec.x >> 31) != 0;
+            const uint32_t rank = i0 + i;
             const uint32_t st = lb_check(produced, S.ll, S.ml, S.off, last, B.limit, B.cap);
             const uint32_t br = brank0 + rank;
             if (st != S3HC_OK && bad == 0xFFFFFFFFu) bad = (br << 3) | st;
@@ -584,7 +569,6 @@ __global__ __launch_bounds__(1024) void k_lb_seq(const uint8_t* __restrict__ src
                 for (uint64_t q = r_lo; q <= r_hi && q < kLbMaxSteps; ++q) A.rfirst[(size_t)bi * kLbMaxSteps + q] = br;
             }
             produced += sl1 < (uint64_t)B.limit + 1u ? sl1 : (uint64_t)B.limit + 1u;
-            ++rank;
         }
     }
     if (bad != 0xFFFFFFFFu) atomicMin(&A.lb_err[bi], bad);
@@ -592,9 +576,12 @@ __global__ __launch_bounds__(1024) void k_lb_seq(const uint8_t* __restrict__ src
         const uint32_t br = A.badrel[c];
         if (br != NONE) {
             // the malformed token ending the chain: after every sequence of the block
+            LbView v;  // one token, read from HBM
+            v.g = src + B.src_off; v.s = nullptr; v.nzg = A.nzg; v.cs = cs; v.ns = 0; v.C = B.C;
+            v.chunk0 = B.chunk0; v.nch = B.nchunks;
             const LbTok S = lb_token(v, cs + br);
             const uint64_t pr = A.outbase[c] - ob0 + stot;
-            uint32_t st = S3HC_CORRUPT, rk = brank0 + ctot;
+            uint32_t st = S3HC_CORRUPT, rk = brank0 + ntc;
             if (S.late == 1) {  // literal checks, then the cut-off offset / length run
                 st = ((int64_t)S.ll > (int64_t)B.cap - (int64_t)pr) ? S3HC_DST_TOO_SMALL : st;
                 st = ((int64_t)S.ll > (int64_t)B.limit - (int64_t)pr) ? S3HC_CORRUPT : st;
@@ -606,7 +593,6 @@ __global__ __launch_bounds__(1024) void k_lb_seq(const uint8_t* __restrict__ src
             atomicMin(&A.lb_err[bi], (rk << 3) | st);
         }
     }
-    (void)n;
 }
 
 // ---------------------------------------------------------------- finish parse

@@ -97,6 +97,7 @@ struct DecUnit {         // a run of blocks decoded in order by one wave
 #define S3HC_LB_CHUNK 8192  // A/B (tools_lbchunk_ab.sh): 1 MiB frame 0.98 -> 0.90 ms, 16 and 256 frames equal; 4096 loses at 256
 #endif
 constexpr uint32_t kLbChunk = S3HC_LB_CHUNK;  // compressed positions per tokenizing workgroup
+constexpr uint32_t kLbTokSlot = kLbChunk / 3 + 2;  // tokens of one chunk, at most (nodes >= 3 apart)
 constexpr uint32_t kLbStep = 7680;        // output bytes per step of the executing workgroup
 constexpr uint32_t kLbMaxSteps = 547;     // steps of one block (ceil(4 MiB / kLbStep))
 constexpr uint32_t kLbMinLimit = 65537;   // frame max block size above 64 KiB selects the path
@@ -145,7 +146,7 @@ struct LbArgs {
     uint32_t* E;           // per compressed position: chain exit of its chunk
     uint16_t* J0;          // per compressed position: next token inside its chunk (chunk-relative; itself if none)
     uint32_t* entry;       // per chunk: first chain position (chunk-relative) or ~0
-    uint32_t* bits;        // per chunk: token bitmap
+    uint4* trec;           // per chunk, kLbTokSlot slots: its tokens in order (lit | last << 31, ll, ml, off)
     uint32_t* ntok;        // per chunk: sequences
     uint32_t* slsum;       // per chunk: output bytes (saturating)
     uint32_t* badrel;      // per chunk: malformed token ending the chain, or ~0

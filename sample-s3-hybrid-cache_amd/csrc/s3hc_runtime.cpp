@@ -361,7 +361,7 @@ static bool lb_candidate(const DecBlock& D, bool unit_single, uint32_t min_limit
 }
 
 struct LbScratch {
-    DevBuf lbt, ctl, unit_lb, chunk_blk, nzg, E, J0, entry, bits, ntok, slsum, badrel, tokbase, outbase, total, seq4,
+    DevBuf lbt, ctl, unit_lb, chunk_blk, nzg, E, J0, entry, trec, ntok, slsum, badrel, tokbase, outbase, total, seq4,
         seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst, blk_hash, wbase, wtile0, wP, tpend, tinit;
     LbArgs a{};
     bool active = false;
@@ -370,12 +370,12 @@ struct LbScratch {
         active = c.lb > 0 && c.chunks > 0;
         if (!active) return hipSuccess;
         const size_t nch = c.chunks, nlb = c.lb;
-        const size_t nseq = nch * (kLbChunk / 3 + 2);
+        const size_t nseq = nch * kLbTokSlot;
         hipError_t e = hipSuccess;
 #define LBE(buf, bytes) if ((e = (buf).ensure((size_t)(bytes) + 64)) != hipSuccess) return e;
         LBE(lbt, nlb * sizeof(LbBlock)) LBE(ctl, sizeof(LbCtl)) LBE(unit_lb, nunits) LBE(chunk_blk, nch * 4)
         LBE(nzg, nch * (kLbChunk / 64) * 4) LBE(E, nch * kLbChunk * 4) LBE(J0, nch * kLbChunk * 2) LBE(entry, nch * 4)
-        LBE(bits, nch * (kLbChunk / 32) * 4) LBE(ntok, nch * 4) LBE(slsum, nch * 4) LBE(badrel, nch * 4)
+        LBE(trec, nch * kLbTokSlot * 16) LBE(ntok, nch * 4) LBE(slsum, nch * 4) LBE(badrel, nch * 4)
         LBE(tokbase, nch * 8) LBE(outbase, nch * 8) LBE(total, 32) LBE(seq4, nseq * 16) LBE(seqoff, nseq * 2)
         LBE(lb_err, nlb * 4) LBE(lb_size, nlb * 4) LBE(lb_stat, nlb * 4) LBE(lb_tok0, nlb * 4) LBE(lb_ntok, nlb * 4)
         LBE(rfirst, nlb * kLbMaxSteps * 4) LBE(blk_hash, (size_t)std::max(nunits, nblocks) * 8)
@@ -397,7 +397,7 @@ struct LbScratch {
         a.min_limit = c.min_limit;
         a.lbt = lbt.as<LbBlock>(); a.ctl = ctl.as<LbCtl>(); a.unit_lb = unit_lb.as<uint8_t>();
         a.chunk_blk = chunk_blk.as<uint32_t>(); a.nzg = nzg.as<uint32_t>(); a.E = E.as<uint32_t>(); a.J0 = J0.as<uint16_t>();
-        a.entry = entry.as<uint32_t>(); a.bits = bits.as<uint32_t>(); a.ntok = ntok.as<uint32_t>();
+        a.entry = entry.as<uint32_t>(); a.trec = trec.as<uint4>(); a.ntok = ntok.as<uint32_t>();
         a.slsum = slsum.as<uint32_t>(); a.badrel = badrel.as<uint32_t>(); a.tokbase = tokbase.as<uint64_t>();
         a.outbase = outbase.as<uint64_t>(); a.total = total.as<uint64_t>(); a.seq4 = seq4.as<uint4>();
         a.seqoff = seqoff.as<uint16_t>(); a.lb_err = lb_err.as<uint32_t>(); a.lb_size = lb_size.as<uint32_t>();
