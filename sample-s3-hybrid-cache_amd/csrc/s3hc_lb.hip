@@ -71,6 +71,10 @@ constexpr uint32_t kXPer = kLbStep / kXT;      // output bytes per executing thr
 #ifndef S3HC_LBH_LAG  // the classify phase hashes only while the wave lags more than this (bytes)
 #define S3HC_LBH_LAG 0
 #endif
+#ifndef S3HC_LB_HOPS
+#define S3HC_LB_HOPS 2  // A/B (tools_hops_ab.sh): 1 MiB step loop 2.00 -> 1.85 ms, 256 frames 4.58 -> 4.47; 3 and 4 lose
+#endif
+constexpr uint32_t kJumpHops = S3HC_LB_HOPS;  // pointer hops per jumping round of k_lb_run
 constexpr uint32_t kHashClassify = S3HC_LBH_CLASSIFY, kHashStores = S3HC_LBH_STORES, kHashInstall = S3HC_LBH_INSTALL,
                    kHashRound = S3HC_LBH_ROUND, kHashLag = S3HC_LBH_LAG;
 static_assert(kXPer * kXT == kLbStep, "step geometry");
@@ -857,7 +861,9 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
 #ifdef S3HC_LBPROF
             const uint64_t tb1 = __builtin_amdgcn_s_memtime();
 #endif
-            if (pend) {
+            // up to kJumpHops hops per round between barriers: pointers other threads stored in
+            // this round are read as soon as they land (LDS), which only shortens the chains
+            for (uint32_t h = 0; h < kJumpHops && pend; ++h) {
                 uint32_t pp[kXPer];
 #pragma unroll
                 for (uint32_t j = 0; j < kXPer; ++j) pp[j] = (pend >> j) & 1u ? ptr[pv[j]] : 0u;
@@ -881,8 +887,8 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
                     }
                 }
                 pend &= ~fin;
-                if (pend) jflag[it % 3u] = 1u;
             }
+            if (pend) jflag[it % 3u] = 1u;
             if (t == 0) jflag[(it + 1u) % 3u] = 0u;
             LB_HASH(R, kHashRound)
 #ifdef S3HC_LBPROF
