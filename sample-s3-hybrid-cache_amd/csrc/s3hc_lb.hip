@@ -288,6 +288,7 @@ __global__ __launch_bounds__(1024) void k_lb_classify(const DecBlock* __restrict
         const uint32_t n = ntaken;  // the taken candidates are a prefix
         A.ctl->nlb = n;
         A.ctl->nchunks = n ? A.lbt[n - 1].chunk0 + A.lbt[n - 1].nchunks : 0u;
+        A.ctl->ntiles = 0;  // k_lbw_plan sets it when the spread execution runs
     }
 }
 

@@ -291,9 +291,12 @@ def test_lb_spread_cap_splits_launch(engine, oracle, cap):
     assert _with_env("S3HC_LBW_CAP", str(cap), lambda: engine.decompress_frames(blob)) == b"".join(parts)
 
 
-def test_lb_spread_many_frames_device_plan(engine):
-    # 32 reference-format 1 MiB frames in one device launch (every tile of every block at once)
-    data = synth.log_text(16 * MiB, 60) + _deep_chain(8 * MiB, 61) + bytes(4 * MiB) + synth.json_records(4 * MiB, 62)
+@pytest.mark.parametrize("nframes", [16, 32])
+def test_lb_spread_many_frames_device_plan(engine, nframes):
+    # reference-format 1 MiB frames in one device launch: 16 spread (every tile of every block at
+    # once), 32 run the step loop (more than kLbwMaxBlocks); both against the step loop
+    data = (synth.log_text(16 * MiB, 60) + _deep_chain(8 * MiB, 61) + bytes(4 * MiB) +
+            synth.json_records(4 * MiB, 62))[:nframes * MiB]
     import oracle as O
 
     frames = [O.lz4flex_compress_frame(data[i:i + MiB]) for i in range(0, len(data), MiB)]
@@ -311,3 +314,16 @@ def test_lb_spread_many_frames_device_plan(engine):
 
     assert run() == ([0] * n, [MiB] * n, data)
     assert _step_path(run) == ([0] * n, [MiB] * n, data)
+
+
+def test_lb_spread_execution_is_taken(engine, oracle, capfd):
+    # the trace (S3HC_LB_TRACE) shows which execution ran: a lone 1 MiB reference frame spreads
+    # over 137 tiles; with S3HC_LBW_DISABLE=1 it has none (step loop)
+    frame = oracle.lz4flex_compress_frame(_data("log_1MiB"))
+    capfd.readouterr()
+    assert _with_env("S3HC_LB_TRACE", "1", lambda: engine.decompress_frames(frame)) == _data("log_1MiB")
+    err = capfd.readouterr().err
+    assert "blocks 1 " in err and "spread tiles 137 " in err, err
+    assert _with_env("S3HC_LB_TRACE", "1", lambda: _step_path(lambda: engine.decompress_frames(frame))) == _data("log_1MiB")
+    err = capfd.readouterr().err
+    assert "spread tiles 0 " in err, err
