@@ -74,6 +74,10 @@ constexpr uint32_t kXPer = kLbStep / kXT;      // output bytes per executing thr
 #ifndef S3HC_LB_HOPS
 #define S3HC_LB_HOPS 2  // A/B (tools_hops_ab.sh): 1 MiB step loop 2.00 -> 1.85 ms, 256 frames 4.58 -> 4.47; 3 and 4 lose
 #endif
+#ifndef S3HC_LB_XHOPS
+#define S3HC_LB_XHOPS 2  // A/B (tools_xhops_ab.sh): 256 reference frames 4.39 -> 4.25 ms; 3 loses
+#endif
+constexpr uint32_t kXHops = S3HC_LB_XHOPS;    // hops per doubling level in k_lb_exit / k_lb_mark
 constexpr uint32_t kJumpHops = S3HC_LB_HOPS;  // pointer hops per jumping round of k_lb_run
 constexpr uint32_t kHashClassify = S3HC_LBH_CLASSIFY, kHashStores = S3HC_LBH_STORES, kHashInstall = S3HC_LBH_INSTALL,
                    kHashRound = S3HC_LBH_ROUND, kHashLag = S3HC_LBH_LAG;
@@ -349,8 +353,15 @@ __global__ __launch_bounds__(1024) void k_lb_exit(const uint8_t* __restrict__ sr
         for (uint32_t k = 0; k < kPer; ++k) {
             const uint32_t r = threadIdx.x + k * kT;
             if (r < n) {
-                const uint32_t j = J[r], jj = J[j];
-                if (jj != j) { J[r] = (uint16_t)jj; ch = true; }
+                uint32_t j = J[r];
+#pragma unroll
+                for (uint32_t h = 0; h < kXHops; ++h) {  // (hops past fresh values between barriers)
+                    const uint32_t jj = J[j];
+                    if (jj == j) break;
+                    j = jj;
+                    ch = true;
+                }
+                J[r] = (uint16_t)j;
             }
         }
         if (!__syncthreads_or(ch)) break;
@@ -437,11 +448,17 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
         for (uint32_t k = 0; k < kPer; ++k) {
             const uint32_t r = threadIdx.x + k * kT;
             if (r < n) {
-                const uint32_t j = X[r];
-                if (j != r && j / kSub == r / kSub) {
+                uint32_t j = X[r];
+                bool mv = false;
+#pragma unroll
+                for (uint32_t h = 0; h < kXHops; ++h) {
+                    if (j == r || j / kSub != r / kSub) break;
                     const uint32_t jj = X[j];
-                    if (jj != j) { X[r] = (uint16_t)jj; ch = true; }
+                    if (jj == j) break;
+                    j = jj;
+                    mv = true;
                 }
+                if (mv) { X[r] = (uint16_t)j; ch = true; }
             }
         }
         if (!__syncthreads_or(ch)) break;
