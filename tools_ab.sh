@@ -8,7 +8,7 @@ for r in 1 2 3; do
     lib=$A; [ $tag = B ] && lib=$B
     for nb in $NB; do
       S3HC_LIB_PATH=$lib timeout -k 10 120 python bench.py --blocks $nb --steps 10 --warmup 3 --no-cpu-baseline --skip-check > gpurun_out/ab/$tag.$nb.$r.out 2>&1 || exit 1
-      python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=d['kernel_ms_per_step']; print(sys.argv[2], sys.argv[3], 'decode', k['decode'], 'enc_parse', k['enc_parse'])" gpurun_out/ab/$tag.$nb.$r.out $tag $nb
+      python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=d['kernel_ms_per_step']; print(sys.argv[2], sys.argv[3], 'decode', k['decode'], 'enc_parse', k['enc_parse'], 'enc_emit', k['enc_emit'], 'value', d['value'])" gpurun_out/ab/$tag.$nb.$r.out $tag $nb
     done
   done
 done
