@@ -408,6 +408,7 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
     __shared__ uint16_t J[kLbChunk], X[kLbChunk];
     __shared__ uint8_t mk[kLbChunk];
     __shared__ uint16_t first[kSubs];
+    __shared__ uint16_t tokpos[kTokSlot];  // marked positions in order
     __shared__ uint32_t shc[16];
     __shared__ uint64_t shs[16];
     __shared__ uint32_t bad_s;
@@ -487,32 +488,34 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
     }
     __syncthreads();
     MK_T(2)
-    // the chunk's tokens in position order: thread t parses positions [kPer*t, kPer*t + kPer) and
-    // writes their records at their rank in the chunk's slot of trec, so k_lb_seq only scans.
-    // Ranks come from the marks alone: the one marked position that is not a token (the
-    // malformed token ending a corrupt chain) is the chain's last node, after every token.
+    // the chunk's tokens in position order: the marked positions are listed at their rank (from
+    // the marks alone: the one marked position that is not a token — the malformed token ending a
+    // corrupt chain — is the chain's last node, after every token), then thread t parses list
+    // entries t, t + kT, ... and writes their records at that rank in the chunk's slot of trec,
+    // so k_lb_seq only scans
     const uint32_t r0 = kPer * threadIdx.x;
     uint32_t nm = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) nm += (r0 + k < n && mk[r0 + k]) ? 1u : 0u;
     uint32_t mtot;
     uint32_t rank = wg_excl_add<uint32_t, 16>(nm, shc, mtot);
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k)
+        if (r0 + k < n && mk[r0 + k]) tokpos[rank++] = (uint16_t)(r0 + k);
+    __syncthreads();
     uint32_t cnt = 0;
     uint64_t sl = 0;
-    for (uint32_t k = 0; k < kPer; ++k) {
-        const uint32_t r = r0 + k;
-        if (r < n && mk[r]) {
-            const LbTok T = lb_token(v, cs + r);
-            if (T.nxt == BAD) {
-                bad_s = r;  // the chain's last node (unique)
-            } else {
-                const uint64_t s1 = (uint64_t)T.ll + T.ml;
-                sl += s1 < (uint64_t)B.limit + 1u ? s1 : (uint64_t)B.limit + 1u;
-                A.trec[(size_t)c * kTokSlot + rank] =
-                    make_uint4(T.lit | (T.nxt == END ? 0x80000000u : 0u), T.ll, T.ml, T.off);  // lit < 2^31
-                ++rank;
-                ++cnt;
-            }
+    for (uint32_t idx = threadIdx.x; idx < mtot; idx += kT) {
+        const uint32_t r = tokpos[idx];
+        const LbTok T = lb_token(v, cs + r);
+        if (T.nxt == BAD) {
+            bad_s = r;  // the chain's last node (unique)
+        } else {
+            const uint64_t s1 = (uint64_t)T.ll + T.ml;
+            sl += s1 < (uint64_t)B.limit + 1u ? s1 : (uint64_t)B.limit + 1u;
+            A.trec[(size_t)c * kTokSlot + idx] =
+                make_uint4(T.lit | (T.nxt == END ? 0x80000000u : 0u), T.ll, T.ml, T.off);  // lit < 2^31
+            ++cnt;
         }
     }
     MK_T(3)
