@@ -216,6 +216,35 @@ __device__ LbTok lb_token(const LbView& v, uint32_t p) {
     return T;
 }
 
+// lb_token(v, p).nxt without reading the offset: the token (and one literal-length byte), then
+// the match-length byte after the offset; length runs with a 255 byte take lb_token.
+__device__ __forceinline__ uint32_t lb_next(const LbView& v, uint32_t p) {
+    using namespace lb;
+    const uint32_t C = v.C;
+    const uint32_t t = lb_byte(v, p);
+    const uint32_t L = t >> 4;
+    uint32_t pos, ll;
+    if (L < 15u) {
+        ll = L;
+        pos = p + 1u;
+    } else {
+        const uint32_t e1 = p + 1u < C ? lb_byte(v, p + 1u) : 255u;
+        if (e1 == 255u) return lb_token(v, p).nxt;
+        ll = 15u + e1;
+        pos = p + 2u;
+    }
+    if (ll > C - pos) return BAD;
+    pos += ll;
+    if (pos == C) return END;
+    if (C - pos < 2u) return BAD;
+    pos += 2u;
+    if (pos >= C) return BAD;  // a token must follow the match (and a length run needs its byte)
+    if ((t & 15u) < 15u) return pos;
+    const uint32_t f1 = lb_byte(v, pos);
+    if (f1 == 255u) return lb_token(v, p).nxt;
+    return pos + 1u >= C ? BAD : pos + 1u;
+}
+
 __device__ __forceinline__ LbView lb_view(const uint8_t* src, const LbBlock& B, const uint32_t* nzg, uint32_t cs,
                                           const uint8_t* s) {
     LbView v;
@@ -338,9 +367,9 @@ __global__ __launch_bounds__(1024) void k_lb_exit(const uint8_t* __restrict__ sr
     for (uint32_t k = 0; k < kPer; ++k) {
         const uint32_t r = threadIdx.x + k * kT;
         if (r < n) {
-            const LbTok T = lb_token(v, cs + r);
-            nx[r] = T.nxt;
-            const uint16_t j0 = (uint16_t)(T.nxt < ce ? T.nxt - cs : r);  // END / BAD / beyond: the chain leaves here
+            const uint32_t nxt = lb_next(v, cs + r);
+            nx[r] = nxt;
+            const uint16_t j0 = (uint16_t)(nxt < ce ? nxt - cs : r);  // END / BAD / beyond: the chain leaves here
             J[r] = j0;
             A.J0[(size_t)c * kLbChunk + r] = j0;  // k_lb_mark starts from it
         }
