@@ -134,7 +134,20 @@ __device__ __forceinline__ const uint8_t* lb_stage(const uint8_t* g, uint32_t cs
     const uint32_t mis = (uint32_t)(a0 & 3u);
     const uint32_t* aw = (const uint32_t*)(a0 - mis);
     const uint32_t nd = (mis + ns + 3u) >> 2;
-    for (uint32_t d = threadIdx.x; d < nd; d += blockDim.x) ((uint32_t*)raw)[d] = aw[d];
+    // four loads per thread in flight before the LDS stores (one HBM round trip per 16 KiB)
+    for (uint32_t base = 0; base < nd; base += 4u * blockDim.x) {
+        uint32_t x[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t d = base + threadIdx.x + k * blockDim.x;
+            x[k] = d < nd ? aw[d] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t d = base + threadIdx.x + k * blockDim.x;
+            if (d < nd) ((uint32_t*)raw)[d] = x[k];
+        }
+    }
     return raw + mis;
 }
 
@@ -457,15 +470,22 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
     const LbBlock B = A.lbt[A.chunk_blk[c]];
     const uint32_t cs = (c - B.chunk0) * kLbChunk;
     const uint32_t n = B.C - cs < kLbChunk ? B.C - cs : kLbChunk;
+    // the chain table's loads are issued before the input staging so both HBM round trips overlap
+    uint16_t j0r[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t r = threadIdx.x + k * kT;
+        j0r[k] = r < n ? A.J0[(size_t)c * kLbChunk + r] : (uint16_t)0;
+    }
     const LbView v = lb_view(src, B, A.nzg, cs, lb_stage(src + B.src_off, cs, B.C - cs < kStage ? B.C - cs : kStage, raw));
     if (threadIdx.x == 0) bad_s = NONE;
     if (threadIdx.x < kSubs) first[threadIdx.x] = 0xFFFFu;
+#pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
         const uint32_t r = threadIdx.x + k * kT;
         if (r < n) {
-            const uint16_t j = A.J0[(size_t)c * kLbChunk + r];
-            J[r] = j;
-            X[r] = j;
+            J[r] = j0r[k];
+            X[r] = j0r[k];
             mk[r] = 0;
         }
     }
