@@ -85,6 +85,7 @@ static_assert(kXPer * kXT == kLbStep, "step geometry");
 constexpr uint32_t kRing = 65536;              // recent output kept in LDS (match sources)
 constexpr uint32_t kMaxSeqS = kLbStep / 4 + 3; // sequences touching one step (all but the last have sl >= 4)
 constexpr uint32_t FIN = 0xFFFFFFFFu;          // source pointer of a final byte
+constexpr uint32_t VALF = 0x80000000u;         // k_lb_run pointer-array entry of a final byte: VALF | value
 }  // namespace lb
 
 #if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 10
@@ -905,7 +906,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
             for (uint32_t j = 0; j < kXPer; ++j) {
                 const uint32_t l = t + kXT * j;
                 ring[(R + l) & kMask] = (uint8_t)vb[j];
-                ptr[l] = pv[j];
+                ptr[l] = pv[j] == FIN ? (VALF | vb[j]) : pv[j];  // a final byte's entry carries its value
             }
             ((uint4*)marks)[t] = make_uint4(0, 0, 0, 0);
         }
@@ -933,27 +934,20 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
 #endif
             // up to kJumpHops hops per round between barriers: pointers other threads stored in
             // this round are read as soon as they land (LDS), which only shortens the chains
+            // (a final entry is VALF | byte value: one gather gives both the state and the value)
             for (uint32_t h = 0; h < kJumpHops && pend; ++h) {
                 uint32_t pp[kXPer];
 #pragma unroll
                 for (uint32_t j = 0; j < kXPer; ++j) pp[j] = (pend >> j) & 1u ? ptr[pv[j]] : 0u;
-                uint32_t rv[kXPer];
                 uint32_t fin = 0;
 #pragma unroll
                 for (uint32_t j = 0; j < kXPer; ++j) {
-                    const bool f = ((pend >> j) & 1u) && pp[j] == FIN;
-                    fin |= (f ? 1u : 0u) << j;
-                    rv[j] = f ? ring[(R + pv[j]) & kMask] : 0u;
-                }
-#pragma unroll
-                for (uint32_t j = 0; j < kXPer; ++j)
-                    if ((fin >> j) & 1u) ring[(R + t + kXT * j) & kMask] = (uint8_t)rv[j];
-                if (fin) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#pragma unroll
-                for (uint32_t j = 0; j < kXPer; ++j) {
                     if ((pend >> j) & 1u) {
-                        pv[j] = (fin >> j) & 1u ? FIN : pp[j];
-                        ptr[t + kXT * j] = pv[j];
+                        const bool f = (pp[j] & VALF) != 0;
+                        fin |= (f ? 1u : 0u) << j;
+                        if (f) ring[(R + t + kXT * j) & kMask] = (uint8_t)pp[j];
+                        pv[j] = f ? FIN : pp[j];
+                        ptr[t + kXT * j] = pp[j];
                     }
                 }
                 pend &= ~fin;
