@@ -1040,7 +1040,8 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
 namespace lb {
 constexpr uint32_t PFIN = 0xFFFFFFFFu;  // P: the byte in dst is final
 constexpr uint32_t PRES = 0x80000000u;  // P: flag of a resolved entry (1 << 31 | root); PFIN has it too
-constexpr uint32_t LOUT = 0x80000000u;  // k_lbw_init LDS pointer: source before the tile (P position)
+constexpr uint32_t LOUT = 0x80000000u;  // k_lbw_init LDS pointer: source before the tile (P position < 2^30)
+constexpr uint32_t LFIN = 0x40000000u;  // k_lbw_init LDS entry of a final byte: LFIN | value
 }  // namespace lb
 
 __global__ __launch_bounds__(1024) void k_lbw_plan(LbArgs A) {
@@ -1057,13 +1058,13 @@ __global__ __launch_bounds__(1024) void k_lbw_plan(LbArgs A) {
     // blocks of frames that allow more than 64 KiB spread (small blocks gain little from it and
     // lose the step loop's overlap with other queues), and only when there are few of them
     uint32_t nbig = 0;
-    for (uint32_t i = t; i < nlb; i += 1024) nbig += A.lbt[i].limit > 65536u ? 1u : 0u;
+    for (uint32_t i = t; i < nlb; i += 1024) nbig += A.lbt[i].limit > kLbwMinLimit ? 1u : 0u;
     uint32_t totbig;
     (void)wg_excl_add<uint32_t, 16>(nbig, sht, totbig);
     const bool few = totbig <= kLbwMaxBlocks;
     for (uint32_t base = 0; base < nlb; base += 1024) {
         const uint32_t i = base + t;
-        const bool ok = few && i < nlb && A.lb_stat[i] == S3HC_OK && A.lb_size[i] > 0 && A.lbt[i].limit > 65536u;
+        const bool ok = few && i < nlb && A.lb_stat[i] == S3HC_OK && A.lb_size[i] > 0 && A.lbt[i].limit > kLbwMinLimit;
         const uint32_t size = ok ? A.lb_size[i] : 0u;
         uint64_t tots;
         uint32_t tott;
@@ -1199,44 +1200,35 @@ __global__ __launch_bounds__(960) void k_lbw_init(const uint8_t* __restrict__ sr
         for (uint32_t j = 0; j < kXPer; ++j) {
             const uint32_t l = t + kXT * j;
             val[l] = (uint8_t)((litm >> j) & 1u ? lv[j] : 0u);
-            ptr[l] = pv[j];
+            ptr[l] = pv[j] == FIN ? (LFIN | lv[j]) : pv[j];  // a final byte's entry carries its value
         }
         if (t == 0) jflag[0] = 0u;
         __syncthreads();
-        // chains inside the tile (as in k_lb_run): a final source gives the value, a source that
-        // points before the tile hands over its P position, a pending one is jumped over
+        // chains inside the tile (as in k_lb_run): a final source gives the value (its entry is
+        // LFIN | byte), a source that points before the tile hands over its P position, a pending
+        // one is jumped over; two hops per round
         uint32_t pend = 0;
 #pragma unroll
         for (uint32_t j = 0; j < kXPer; ++j) pend |= (!(pv[j] & LOUT) ? 1u : 0u) << j;
         for (uint32_t it = 0; it < 16; ++it) {
-            if (pend) {
+            for (uint32_t h = 0; h < kJumpHops && pend; ++h) {
                 uint32_t pp[kXPer];
 #pragma unroll
                 for (uint32_t j = 0; j < kXPer; ++j) pp[j] = (pend >> j) & 1u ? ptr[pv[j]] : 0u;
-                uint32_t rv[kXPer];
-                uint32_t fin = 0;
-#pragma unroll
-                for (uint32_t j = 0; j < kXPer; ++j) {
-                    const bool f = ((pend >> j) & 1u) && pp[j] == FIN;
-                    fin |= (f ? 1u : 0u) << j;
-                    rv[j] = f ? val[pv[j]] : 0u;
-                }
-#pragma unroll
-                for (uint32_t j = 0; j < kXPer; ++j)
-                    if ((fin >> j) & 1u) val[t + kXT * j] = (uint8_t)rv[j];
-                if (fin) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                uint32_t done = fin;
+                uint32_t done = 0;
 #pragma unroll
                 for (uint32_t j = 0; j < kXPer; ++j) {
                     if ((pend >> j) & 1u) {
-                        pv[j] = (fin >> j) & 1u ? FIN : pp[j];
+                        const bool f = (pp[j] & LFIN) != 0;
+                        if (f) val[t + kXT * j] = (uint8_t)pp[j];
+                        pv[j] = f ? FIN : pp[j];
                         done |= ((pv[j] & LOUT) ? 1u : 0u) << j;
-                        ptr[t + kXT * j] = pv[j];
+                        ptr[t + kXT * j] = pp[j];
                     }
                 }
                 pend &= ~done;
-                if (pend) jflag[it % 3u] = 1u;
             }
+            if (pend) jflag[it % 3u] = 1u;
             if (t == 0) jflag[(it + 1u) % 3u] = 0u;
             __syncthreads();
             if (!jflag[it % 3u]) break;

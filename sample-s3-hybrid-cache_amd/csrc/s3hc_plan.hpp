@@ -111,6 +111,10 @@ constexpr uint32_t kLbwCapMax = 1u << 30; // spread execution: pointer-array pos
 constexpr uint32_t kLbwMaxBlocks = 16;        // ... and so do launches of more large blocks than this:
                                               // the step loop's one workgroup per block lets the reader's
                                               // queues overlap batches (config-4 A/B, §4b)
+#ifndef S3HC_LBW_MINLIMIT  // (diagnostic builds try other values)
+#define S3HC_LBW_MINLIMIT 65536
+#endif
+constexpr uint32_t kLbwMinLimit = S3HC_LBW_MINLIMIT;  // spread: blocks of frames allowing more than this
 constexpr uint32_t kLbwMaxOut = 96u << 20;     // launches whose large blocks may decode to more than
                                               // this run the step loop (k_lb_run): with a block per CU
                                               // it is as fast, and P stays small (measured, §4b)

@@ -349,7 +349,7 @@ struct LbCaps {
     void add_block(uint32_t csize, uint32_t out_bound, uint32_t limit) {
         ++lb;
         chunks += (csize + kLbChunk - 1) / kLbChunk;
-        if (limit > 65536u) {
+        if (limit > kLbwMinLimit) {
             ++nbig;
             outb += std::min<uint64_t>(out_bound, (uint64_t)kLbMaxSteps * kLbStep);
         }
