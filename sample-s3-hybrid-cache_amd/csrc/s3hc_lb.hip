@@ -16,17 +16,20 @@
 //                  (lz4_flex parse rules, exact for long runs), then pointer doubling in LDS:
 //                  each position learns where its token chain leaves the chunk.
 //   k_lb_entry     per block, serial over chunks: the true chain's entry into each chunk.
-//   k_lb_mark      per chunk: doubling again, marking the nodes reachable from the entry =
-//                  the block's real tokens; per-chunk sequence count and output bytes.
+//   k_lb_mark      per chunk: marks the nodes reachable from the entry (= the block's real
+//                  tokens) by sub-range exits, parses them one per thread and writes their
+//                  records; per-chunk sequence count and output bytes.
 //   (scans)        global sequence index and output offset of each chunk.
-//   k_lb_seq       per chunk: the sequence table (out, literal, ll, ml, offset) and the
-//                  lz4_flex bound checks in stream order (first failing sequence decides).
+//   k_lb_seq       per chunk: the sequence table (out, literal, ll, ml, offset) from the records
+//                  and the lz4_flex bound checks in stream order (first failing sequence decides).
 //   k_lb_fin       per block: size, status, first sequence.
-//   k_lb_run       one 1024-thread workgroup per block writes the output in 8 KiB steps: in
-//                  each step every byte gets its value (literal, or a match source before the
-//                  step: 64 KiB LDS ring of recent output) or a pointer to its source inside
-//                  the step (overlapping copies folded into the first period), and the
-//                  pointers are jumped in LDS until every byte is final.
+//   k_lb_run       (launches of many blocks) one 1024-thread workgroup per block writes the
+//                  output in 7.5 KiB steps: in each step every byte gets its value (literal, or a
+//                  match source before the step: 64 KiB LDS ring of recent output) or a pointer
+//                  to its source inside the step (overlapping copies folded into the first
+//                  period), and the pointers are jumped in LDS until every byte is final.
+//   k_lbw_*        (launches of few large blocks) spread execution: every 7.5 KiB tile of every
+//                  block at once, chains across tiles resolved by global pointer jumping.
 //
 // All of it is integer byte work (no MFMA); every kernel is bound by memory latency or LDS.
 #include <hip/hip_runtime.h>
