@@ -92,7 +92,8 @@ struct DecUnit {         // a run of blocks decoded in order by one wave
 // 1024-thread workgroup per block then writes the output in 7.5 KiB steps (15 waves, 8 bytes per
 // lane), resolving each step's match chains in LDS by pointer jumping against a 64 KiB ring of
 // recent output, while its 16th wave hashes the flushed output (the frame's content xxh32 when
-// the block is the whole frame).
+// the block is the whole frame). Launches of few such blocks decode every 7.5 KiB tile at once
+// instead (spread execution, k_lbw_*).
 #ifndef S3HC_LB_CHUNK  // (diagnostic builds try other sizes)
 #define S3HC_LB_CHUNK 8192  // A/B (tools_lbchunk_ab.sh): 1 MiB frame 0.98 -> 0.90 ms, 16 and 256 frames equal; 4096 loses at 256
 #endif
