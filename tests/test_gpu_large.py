@@ -327,3 +327,21 @@ def test_lb_spread_execution_is_taken(engine, oracle, capfd):
     assert _with_env("S3HC_LB_TRACE", "1", lambda: _step_path(lambda: engine.decompress_frames(frame))) == _data("log_1MiB")
     err = capfd.readouterr().err
     assert "spread tiles 0 " in err, err
+
+
+def test_lb_spread_and_step_in_one_launch_randomized(engine, oracle):
+    # one host call holding frames of both kinds (BD 0x40 blocks run the step loop, larger frames
+    # spread), random sizes and contents, compared with the oracle and with the step loop alone
+    rng = random.Random(77)
+    for case in range(6):
+        parts = []
+        for _ in range(rng.randrange(2, 9)):
+            size = rng.choice([1000, 65_536, 70_000, 300_000, MiB, 2 * MiB + 5])
+            kind = rng.randrange(3)
+            seed = rng.randrange(1 << 30)
+            p = synth.log_text(size, seed) if kind == 0 else (_deep_chain(size, seed) if kind == 1 else _runs(size, seed))
+            parts.append(p)
+        blob = b"".join(oracle.lz4flex_compress_frame(p) for p in parts)
+        want = b"".join(parts)
+        assert engine.decompress_frames(blob) == want, case
+        assert _step_path(lambda: engine.decompress_frames(blob)) == want, case
