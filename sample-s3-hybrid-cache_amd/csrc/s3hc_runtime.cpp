@@ -365,9 +365,11 @@ struct LbScratch {
         seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst, blk_hash, wbase, wtile0, wP, tpend, tinit;
     LbArgs a{};
     bool active = false;
+    bool all_lb = false;  // every unit of the launch is a taken large block (host walks know): no unit decoder launch
     // nunits: units of the launch; nblocks: its DecBlock count (block hashes are per DecBlock)
     hipError_t prepare(uint32_t nunits, uint32_t nblocks, const LbCaps& c) {
         active = c.lb > 0 && c.chunks > 0;
+        all_lb = active && c.exact && c.lb == nunits;  // (the caps equal the counts: every candidate is taken)
         if (!active) return hipSuccess;
         const size_t nch = c.chunks, nlb = c.lb;
         const size_t nseq = nch * kLbTokSlot;
@@ -429,7 +431,8 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
     if (blk_hash) *blk_hash = lb ? L->a.blk_hash : nullptr;
     hipError_t e;
     if (lb && (e = launch_lb_parse(L->a, src, blk, units, nunits, blk_out, blk_status, st)) != hipSuccess) return e;
-    if ((e = launch_decode_units(src, dst, blk, units, nunits, blk_out, blk_status, lb ? L->a.unit_lb : nullptr,
+    if (!(lb && L->all_lb) &&
+        (e = launch_decode_units(src, dst, blk, units, nunits, blk_out, blk_status, lb ? L->a.unit_lb : nullptr,
                                  st)) != hipSuccess)
         return e;
     if (lb && (e = launch_lb_exec(L->a, src, dst, st)) != hipSuccess) return e;
