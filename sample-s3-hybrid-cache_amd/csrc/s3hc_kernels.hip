@@ -1985,8 +1985,8 @@ __global__ void k_enc_frames(const uint32_t* __restrict__ frame_blk0, const uint
 }
 
 // Exclusive scan of u32 sizes into u64 offsets: single workgroup, chunked (n up to millions).
-__global__ __launch_bounds__(1024) void k_scan_u32_u64(const uint32_t* __restrict__ in, uint32_t n,
-                                                       uint64_t* __restrict__ out, uint64_t* __restrict__ total) {
+__device__ __forceinline__ void scan_u32_u64(const uint32_t* __restrict__ in, uint32_t n, uint64_t* __restrict__ out,
+                                             uint64_t* __restrict__ total) {
     __shared__ uint64_t wsum[16];
     __shared__ uint64_t carry_s;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -2023,6 +2023,17 @@ __global__ __launch_bounds__(1024) void k_scan_u32_u64(const uint32_t* __restric
         __syncthreads();
     }
     if (t == 0) *total = carry_s;
+}
+__global__ __launch_bounds__(1024) void k_scan_u32_u64(const uint32_t* __restrict__ in, uint32_t n,
+                                                       uint64_t* __restrict__ out, uint64_t* __restrict__ total) {
+    scan_u32_u64(in, n, out, total);
+}
+// two independent scans of n entries in one launch (one workgroup each)
+__global__ __launch_bounds__(1024) void k_scan2_u32_u64(const uint32_t* __restrict__ in0, const uint32_t* __restrict__ in1,
+                                                        uint32_t n, uint64_t* __restrict__ out0,
+                                                        uint64_t* __restrict__ out1, uint64_t* __restrict__ total) {
+    if (blockIdx.x == 0) scan_u32_u64(in0, n, out0, total);
+    else scan_u32_u64(in1, n, out1, total + 1);
 }
 
 // ============================================ device-side frame walk (decode)
@@ -2276,6 +2287,11 @@ hipError_t launch_enc_sizes(const EncBlock* blocks, uint32_t nblocks, const SegS
 }
 hipError_t launch_scan(const uint32_t* in, uint32_t n, uint64_t* out, uint64_t* total, hipStream_t st) {
     hipLaunchKernelGGL(k_scan_u32_u64, dim3(1), dim3(1024), 0, st, in, n, out, total);
+    return hipGetLastError();
+}
+hipError_t launch_scan2(const uint32_t* in0, const uint32_t* in1, uint32_t n, uint64_t* out0, uint64_t* out1,
+                        uint64_t* total, hipStream_t st) {
+    hipLaunchKernelGGL(k_scan2_u32_u64, dim3(2), dim3(1024), 0, st, in0, in1, n, out0, out1, total);
     return hipGetLastError();
 }
 hipError_t launch_enc_emit(const uint8_t* src, const EncBlock* blocks, const uint32_t* seg_block, uint32_t nseg,

@@ -1351,7 +1351,8 @@ __global__ __launch_bounds__(960) void k_lbw_gather(uint8_t* __restrict__ dst, L
 
 // ================================================================ launchers
 static inline uint32_t cdiv_lb(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
-hipError_t launch_scan(const uint32_t* in, uint32_t n, uint64_t* out, uint64_t* total, hipStream_t st);
+hipError_t launch_scan2(const uint32_t* in0, const uint32_t* in1, uint32_t n, uint64_t* out0, uint64_t* out1,
+                        uint64_t* total, hipStream_t st);
 
 // Parse stage: classify the units, tokenize, build the sequence table, statuses and sizes of
 // the taken blocks. Must precede k_decode_units (it reads unit_lb).
@@ -1362,9 +1363,7 @@ hipError_t launch_lb_parse(const LbArgs& A, const uint8_t* src, const DecBlock* 
     hipLaunchKernelGGL(k_lb_exit, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
     hipLaunchKernelGGL(k_lb_entry, dim3(cdiv_lb(A.lb_cap, 64)), dim3(64), 0, st, A);
     hipLaunchKernelGGL(k_lb_mark, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
-    hipError_t e = launch_scan(A.ntok, A.chunk_cap, A.tokbase, A.total, st);
-    if (e != hipSuccess) return e;
-    e = launch_scan(A.slsum, A.chunk_cap, A.outbase, A.total + 1, st);
+    hipError_t e = launch_scan2(A.ntok, A.slsum, A.chunk_cap, A.tokbase, A.outbase, A.total, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lb_seq, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
     hipLaunchKernelGGL(k_lb_fin, dim3(cdiv_lb(A.lb_cap, 256)), dim3(256), 0, st, A, blk_out, blk_status);
