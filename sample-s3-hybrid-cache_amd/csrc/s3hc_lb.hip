@@ -674,9 +674,9 @@ __global__ __launch_bounds__(1024) void k_lb_seq(const uint8_t* __restrict__ src
 }
 
 // ---------------------------------------------------------------- finish parse
-__global__ void k_lb_fin(LbArgs A, uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A.ctl->nlb) return;
+// size and status of LB block i (< nlb); returns the status, *size_out the decoded bytes (0 unless OK)
+__device__ __forceinline__ uint32_t lb_fin_block(const LbArgs& A, uint32_t i, uint32_t* __restrict__ blk_out,
+                                                 int32_t* __restrict__ blk_status, uint32_t* size_out) {
     const LbBlock B = A.lbt[i];
     const uint32_t cl = B.chunk0 + B.nchunks - 1;
     const uint64_t size = A.outbase[cl] + A.slsum[cl] - A.outbase[B.chunk0];
@@ -688,6 +688,13 @@ __global__ void k_lb_fin(LbArgs A, uint32_t* __restrict__ blk_out, int32_t* __re
     A.lb_ntok[i] = (uint32_t)(A.tokbase[cl] + A.ntok[cl] - A.tokbase[B.chunk0]);
     blk_out[B.blk] = stat == S3HC_OK ? (uint32_t)size : 0u;
     blk_status[B.blk] = (int32_t)stat;
+    *size_out = stat == S3HC_OK ? (uint32_t)size : 0u;
+    return stat;
+}
+__global__ void k_lb_fin(LbArgs A, uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t size;
+    if (i < A.ctl->nlb) (void)lb_fin_block(A, i, blk_out, blk_status, &size);
 }
 
 // ---------------------------------------------------------------- execute
@@ -1047,7 +1054,7 @@ constexpr uint32_t LOUT = 0x80000000u;  // k_lbw_init LDS pointer: source before
 constexpr uint32_t LFIN = 0x40000000u;  // k_lbw_init LDS entry of a final byte: LFIN | value
 }  // namespace lb
 
-__global__ __launch_bounds__(1024) void k_lbw_plan(LbArgs A) {
+__global__ __launch_bounds__(1024) void k_lbw_plan(LbArgs A, uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status) {
     using namespace lb;
     __shared__ uint64_t shs[16];
     __shared__ uint32_t sht[16];
@@ -1067,8 +1074,11 @@ __global__ __launch_bounds__(1024) void k_lbw_plan(LbArgs A) {
     const bool few = totbig <= kLbwMaxBlocks;
     for (uint32_t base = 0; base < nlb; base += 1024) {
         const uint32_t i = base + t;
-        const bool ok = few && i < nlb && A.lb_stat[i] == S3HC_OK && A.lb_size[i] > 0 && A.lbt[i].limit > kLbwMinLimit;
-        const uint32_t size = ok ? A.lb_size[i] : 0u;
+        // (k_lb_fin's work, done here when the spread execution runs)
+        uint32_t fsize = 0, fstat = S3HC_CORRUPT;
+        if (i < nlb) fstat = lb_fin_block(A, i, blk_out, blk_status, &fsize);
+        const bool ok = few && i < nlb && fstat == S3HC_OK && fsize > 0 && A.lbt[i].limit > kLbwMinLimit;
+        const uint32_t size = ok ? fsize : 0u;
         uint64_t tots;
         uint32_t tott;
         // positions grow with the block index, so the spread blocks are a prefix of the decodable ones
@@ -1366,15 +1376,17 @@ hipError_t launch_lb_parse(const LbArgs& A, const uint8_t* src, const DecBlock* 
     hipError_t e = launch_scan2(A.ntok, A.slsum, A.chunk_cap, A.tokbase, A.outbase, A.total, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lb_seq, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
-    hipLaunchKernelGGL(k_lb_fin, dim3(cdiv_lb(A.lb_cap, 256)), dim3(256), 0, st, A, blk_out, blk_status);
+    if (!A.wcap)  // (with the spread execution, k_lbw_plan does it)
+        hipLaunchKernelGGL(k_lb_fin, dim3(cdiv_lb(A.lb_cap, 256)), dim3(256), 0, st, A, blk_out, blk_status);
     return hipGetLastError();
 }
 
 // Execute stage: one workgroup per taken block.
-hipError_t launch_lb_exec(const LbArgs& A, const uint8_t* src, uint8_t* dst, hipStream_t st) {
+hipError_t launch_lb_exec(const LbArgs& A, const uint8_t* src, uint8_t* dst, uint32_t* blk_out, int32_t* blk_status,
+                          hipStream_t st) {
     if (A.wcap) {  // spread execution of the blocks that fit P, then the step loop for the rest
         const uint32_t tiles = A.tile_cap;
-        hipLaunchKernelGGL(k_lbw_plan, dim3(1), dim3(1024), 0, st, A);
+        hipLaunchKernelGGL(k_lbw_plan, dim3(1), dim3(1024), 0, st, A, blk_out, blk_status);
         hipLaunchKernelGGL(k_lbw_init, dim3(tiles < 512u ? tiles : 512u), dim3(lb::kXT), 0, st, src, dst, A);
         // S3HC_LBW_ROUNDS (tests): fewer launches, so k_lbw_gather walks long chains itself
         uint32_t rounds = kLbwRounds;

@@ -34,7 +34,7 @@ hipError_t launch_decode_units(const uint8_t*, uint8_t*, const DecBlock*, const 
                                int32_t*, const uint8_t*, hipStream_t);
 hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*, int32_t*,
                            hipStream_t);
-hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, hipStream_t);
+hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_enc_parse(const uint8_t*, const EncBlock*, const uint2*, uint32_t, const uint64_t*, const uint32_t*,
                             uint32_t, uint32_t*, uint2*, SegSummary*, hipStream_t);
 hipError_t launch_enc_sizes(const EncBlock*, uint32_t, const SegSummary*, SegPlace*, uint32_t*, uint32_t*,
@@ -435,7 +435,7 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
         (e = launch_decode_units(src, dst, blk, units, nunits, blk_out, blk_status, lb ? L->a.unit_lb : nullptr,
                                  st)) != hipSuccess)
         return e;
-    if (lb && (e = launch_lb_exec(L->a, src, dst, st)) != hipSuccess) return e;
+    if (lb && (e = launch_lb_exec(L->a, src, dst, blk_out, blk_status, st)) != hipSuccess) return e;
     if (lb && getenv("S3HC_LB_TRACE")) {  // diagnostics: blocks and chunks taken
         LbCtl c;
         if ((e = hipMemcpyAsync(&c, L->a.ctl, sizeof c, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
