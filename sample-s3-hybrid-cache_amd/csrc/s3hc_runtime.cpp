@@ -1151,7 +1151,8 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
     const uint32_t* bo = nullptr;
     const int32_t* bs = nullptr;
     const uint32_t *cs_got = nullptr, *flen = nullptr, *fhash = nullptr;
-    bool spec = false;  // the decoded slots [0, slot_total) are in hs.buf[0]
+    bool spec = false;  // the decoded slots [0, spec_bytes) are in hs.buf[0]
+    uint64_t spec_bytes = 0;
     if (stopped_out) *stopped_out = false;
     if (nb) {
         if (upload_in) {
@@ -1225,12 +1226,16 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         if (any_cs) HIPCHK(hipMemcpyAsync(rb + 2 * nb, ctx->d_hash.p, nb * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(rb + 3 * nb, ctx->d_flen.p, nf * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(rb + 3 * nb + nf, ctx->d_fhash.p, nf * 4, hipMemcpyDeviceToHost, st));
-        // small outputs: their slots come back in the same round trip (pageable destinations)
-        spec = W.slot_total <= kSpecBytes && (vout || !host_pinned(dst));
+        // small outputs: their slots come back in the same round trip (pageable destinations).
+        // Only a prefix of max(4 x input, 1 MiB) bytes: a BD 0x70 frame's slot is 4 MiB whatever it
+        // decodes to (lz4_flex writes no content size); output beyond the prefix (rare: ratios
+        // above 4) takes the second round trip below.
+        spec_bytes = std::min<uint64_t>(W.slot_total, std::max<uint64_t>(4 * (uint64_t)n, 1u << 20));
+        spec = spec_bytes <= kSpecBytes && (vout || !host_pinned(dst));
         if (spec) {
-            HIPCHK(hs.init(W.slot_total));
-            HIPCHK(hs.buf[0].ensure(W.slot_total + 16));
-            HIPCHK(hipMemcpyAsync(hs.buf[0].p, ctx->d_out.p, W.slot_total, hipMemcpyDeviceToHost, st));
+            HIPCHK(hs.init(spec_bytes));
+            HIPCHK(hs.buf[0].ensure(spec_bytes + 16));
+            HIPCHK(hipMemcpyAsync(hs.buf[0].p, ctx->d_out.p, spec_bytes, hipMemcpyDeviceToHost, st));
         }
         HTRACE("queued")
         HIPCHK(hipStreamSynchronize(st));
@@ -1356,6 +1361,7 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         if (!spans.empty() && spans.back().first + spans.back().second == fpos[f]) spans.back().second += fout[f];
         else spans.push_back({fpos[f], fout[f]});
     }
+    if (spec && !spans.empty() && spans.back().first + spans.back().second > spec_bytes) spec = false;
     if (spec) {
         uint64_t o = 0;
         for (auto& sp : spans) {
