@@ -66,9 +66,14 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def spawn_ranks(n: int, argv) -> int:
+def spawn_ranks(n: int, argv, timeout: float = 1800.0) -> int:
     """Run this script as n rank processes (fresh interpreters, never an exec of this one);
-    relay rank 0's stdout. Returns the exit code (first failing rank's, else 0)."""
+    relay rank 0's stdout. Returns the exit code (first failing rank's, else 0). All ranks are
+    polled together: as soon as one exits non-zero (or the overall timeout passes) the others are
+    killed, so a rank that dies before a collective cannot leave rank 0 blocked in gloo."""
+    import threading
+    import time
+
     port = _free_port()
     procs = []
     for r in range(n):
@@ -78,20 +83,30 @@ def spawn_ranks(n: int, argv) -> int:
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out0 = procs[0].communicate()[0]
-    rc = procs[0].returncode
-    for p in procs[1:]:
-        try:
-            p.wait(timeout=600)
-        except subprocess.TimeoutExpired:
+    chunks = []
+    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    deadline = time.monotonic() + timeout
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > deadline:
+            sys.stderr.write(f"bench.py: ranks still running after {timeout:g} s; killing them\n")
+            rc = 124
+            break
+        time.sleep(0.05)
+    for p in procs:
+        if p.poll() is None:
             p.kill()
-            p.wait()
-        rc = rc or p.returncode
-    if rc:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
-    sys.stdout.write(out0.decode())
+        p.wait()
+    reader.join(timeout=10)
+    sys.stdout.write(b"".join(c for c in chunks if c).decode())
     sys.stdout.flush()
     return rc
 
@@ -112,6 +127,9 @@ def launch_decision(args):
 def selftest(args):
     import shard
 
+    fail = os.environ.get("S3HC_SELFTEST_FAIL_RANK")  # launcher test: this rank dies before any collective
+    if fail is not None and int(fail) == int(os.environ.get("RANK", "0")):
+        sys.exit(3)
     g = shard.Group()
     total = args.total_blocks or args.blocks * g.world
     lo, hi = shard.shard_range(total, g.world, g.rank) if args.total_blocks else (g.rank * args.blocks, (g.rank + 1) * args.blocks)
@@ -168,26 +186,35 @@ def cpu_baseline(data_chunk: bytes, block: int, seconds: float):
         return done.value, wall.value, es.value, ds.value
 
     n1, w1, e1, d1 = run(1, seconds)
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    model, quota = host_cpu_info()
+    # effective cores: the CPUs this process may run on, capped by the cgroup CPU quota (a 16-CPU
+    # quota on a 256-thread host runs 16 threads' worth of work whatever the thread count)
+    threads = max(1, min(affinity, int(quota))) if quota else affinity
     runs = []
     for _ in range(5):
         n, w, _, _ = run(threads, seconds)
         runs.append(n * block / w / GiB)
-    model, quota = host_cpu_info()
+    over = None
+    if threads < affinity:  # the same run oversubscribed to every thread of the affinity mask
+        n, w, _, _ = run(affinity, seconds)
+        over = round(n * block / w / GiB, 4)
     return {
         "value": round(statistics.median(runs), 4),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
         "sample": f"64 KiB blocks of the bench's own log-text batch ({nb} distinct blocks, cycled), lz4_flex-faithful "
-                  f"frame encode + decompress_data per block (oracle/ C port, -O3), {threads} threads over contiguous "
-                  f"block ranges; median of 5 runs of >= {seconds:g} s wall",
+                  f"frame encode + decompress_data per block (oracle/ C port, -O3), {threads} threads (effective "
+                  f"cores = min(affinity {affinity}, cgroup quota {quota})) over contiguous block ranges; median of "
+                  f"5 runs of >= {seconds:g} s wall",
         "runs_gibps": [round(x, 4) for x in runs],
+        "oversubscribed_all_threads_gibps": over,
         "single_thread_gibps": round(n1 * block / w1 / GiB, 4),
         "single_thread_encode_gibps": round(n1 * block / e1 / GiB, 4),
         "single_thread_decode_gibps": round(n1 * block / d1 / GiB, 4),
         "host_nproc": os.cpu_count(),
-        "cpu_affinity": threads,
+        "cpu_affinity": affinity,
         "cgroup_cpu_quota": quota,
         "cpu_model": model,
     }

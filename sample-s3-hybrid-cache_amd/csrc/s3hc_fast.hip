@@ -1,0 +1,888 @@
+// s3hc_fast.hip — the 64 KiB-block LZ4 decode path.
+//
+// lz4_flex's FrameDecoder (compression.rs:479-480) decodes a block by one serial walk: token,
+// literal run, offset, match, next token. Here that walk is split in two kernels:
+//
+//   k_dtok   token index. One 256-thread workgroup per block stages the compressed block in LDS
+//            and cuts it into 256 segments. Every thread walks the token chain from the start of
+//            its segment as if a token began there (speculatively), marking the positions it
+//            visits in a bitmap; past its segment's end it keeps walking until it lands on a
+//            position another thread marked (LZ4 token chains merge after a few hops: a chain is
+//            a function of its position). The true chain is the first thread's walk, then the
+//            walk it merged into, and so on: those "merge into" links form a list over the
+//            segments that pointer doubling resolves in 8 steps. The true tokens are then
+//            counted (bitmap popcounts), scanned, validated against every lz4_flex bound (literal
+//            and match lengths against the block limit and the caller's capacity, offsets against
+//            the bytes produced) and their positions written to a pool.
+//   k_dexec  executor (one wave per block): 64 sequences at a time, one per lane.
+//
+// A block the fast path does not take (stored, larger than kFastMaxC compressed bytes, part of a
+// multi-block unit, or failing any check) is left to the per-unit decoder (k_decode_pe), which
+// also reports its exact status; the fast path only ever produces correct output for valid
+// blocks, so its results are the per-unit decoder's by construction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "s3hc_plan.hpp"
+#include "s3hc_lz4.h"
+
+// Phase timers of diagnostic builds only (S3HC_DIAG_LEVEL 10): per-wave s_memtime sums into
+// g_fprof, read back with s3hc_diag_fprof. Compiled out of the shipped library.
+#if defined(S3HC_DIAG_LEVEL) && S3HC_DIAG_LEVEL == 10
+#define FPROF 1
+#define FP_NOW() __builtin_amdgcn_s_memtime()
+#define FP_ADD(k, v) atomicAdd(&s3hc::g_fprof[k], (unsigned long long)(v))
+#else
+#define FP_NOW() 0ull
+#define FP_ADD(k, v) ((void)0)
+#endif
+
+namespace s3hc {
+#ifdef FPROF
+__device__ unsigned long long g_fprof[32];
+#endif
+namespace fst {
+constexpr uint32_t kMaxC = kFastMaxC;
+constexpr uint32_t kTT = 256;                  // k_dtok threads = speculative segments per block
+constexpr uint32_t kStage = kMaxC + 64;        // staged block: 16-B alignment slack + zero read-ahead
+constexpr uint32_t kBitW = kMaxC / 32;         // bitmap words, one bit per compressed position
+constexpr uint32_t END = 0xFFFFFFFEu;          // chain ended with the block's last sequence
+constexpr uint32_t DEAD = 0xFFFFFFFFu;         // malformed token (or a walk that gave up)
+constexpr uint32_t kOvfCap = 4096;             // hops a walk past its segment may take before giving up
+constexpr uint32_t kLv = 8;                    // doubling levels: chains over <= 256 segments
+constexpr uint32_t kTermEnd = kTT, kTermBad = kTT + 1;
+constexpr uint32_t kMEnd = 0xFFFEu, kMBad = 0xFFFFu;  // u16 merge codes (positions are < kMaxC)
+}  // namespace fst
+
+namespace {
+__device__ __forceinline__ uint32_t umin_(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t umax_(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+// 4 bytes at LDS byte offset i (two aligned dword reads + v_alignbyte)
+__device__ __forceinline__ uint32_t st32(const uint8_t* st, uint32_t i) {
+    const uint32_t* w = (const uint32_t*)(st + (i & ~3u));
+    return __builtin_amdgcn_alignbyte(w[1], w[0], i & 3u);
+}
+
+// Remainder of a length-extension run at block byte q (the inline decode already consumed two
+// bytes of 255): adds the run, advances q past it; q = C + 1 when the run reaches the end.
+__device__ uint32_t ext_tail(const uint8_t* st, uint32_t mis, uint32_t& q, uint32_t C) {
+    uint32_t acc = 0;
+    for (;;) {
+        if (q >= C) {
+            q = C + 1;
+            return acc;
+        }
+        const uint32_t e = st[q + mis];
+        ++q;
+        acc += e;
+        if (e != 255u) return acc;
+    }
+}
+
+struct Tok {
+    uint32_t nxt;  // next token position, END (this is the last sequence) or DEAD (malformed)
+    uint32_t ll, off, ml;
+};
+
+// One token of the staged block at position p (lz4_flex decompress_internal's parse: literal
+// length with 255-runs, literals, 2-byte offset, match length with 255-runs). A block must end
+// right after a literal run; a run, an offset or literals reaching past the end are malformed.
+__device__ __forceinline__ Tok hop(const uint8_t* st, uint32_t mis, uint32_t p, uint32_t C) {
+    Tok T;
+    T.off = 0;
+    T.ml = 0;
+    const uint32_t w0 = st32(st, p + mis);
+    const uint32_t t = w0 & 0xFFu;
+    uint32_t L = t >> 4, q = p + 1;
+    if (L == 15u) {
+        const uint32_t e1 = (w0 >> 8) & 0xFFu;
+        L += e1;
+        ++q;
+        if (e1 == 255u) {
+            const uint32_t e2 = (w0 >> 16) & 0xFFu;
+            L += e2;
+            ++q;
+            if (e2 == 255u) L += ext_tail(st, mis, q, C);
+        }
+    }
+    T.ll = L;
+    if (q > C || L > C - q) {  // run past the end / literals past the end
+        T.nxt = fst::DEAD;
+        return T;
+    }
+    const uint32_t mp = q + L;
+    if (mp == C) {  // last sequence: literals only
+        T.nxt = fst::END;
+        return T;
+    }
+    if (C - mp < 2) {
+        T.nxt = fst::DEAD;
+        return T;
+    }
+    const uint32_t w1 = st32(st, mp + mis);
+    T.off = w1 & 0xFFFFu;
+    uint32_t M = (t & 15u) + 4u, q2 = mp + 2;
+    if ((t & 15u) == 15u) {
+        const uint32_t f1 = (w1 >> 16) & 0xFFu;
+        M += f1;
+        ++q2;
+        if (f1 == 255u) {
+            const uint32_t f2 = w1 >> 24;
+            M += f2;
+            ++q2;
+            if (f2 == 255u) M += ext_tail(st, mis, q2, C);
+        }
+    }
+    T.ml = M;
+    T.nxt = q2 >= C ? fst::DEAD : q2;  // a run past the end, or no token after a match
+    return T;
+}
+
+// exclusive scan over the 256 threads of a workgroup (4 waves); *total = sum
+__device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) scratch[w] = x;
+    __syncthreads();
+    const uint32_t s0 = scratch[0], s1 = scratch[1], s2 = scratch[2], s3 = scratch[3];
+    const uint32_t before = (w > 0 ? s0 : 0u) + (w > 1 ? s1 : 0u) + (w > 2 ? s2 : 0u);
+    *total = s0 + s1 + s2 + s3;
+    __syncthreads();
+    return before + x - v;
+}
+}  // namespace
+
+// ------------------------------------------------------------------ k_dtok
+__global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ src, const DecBlock* __restrict__ blk,
+                                                   const DecUnit* __restrict__ units, uint32_t nunits,
+                                                   const uint8_t* __restrict__ unit_lb, FastArgs a) {
+    using namespace fst;
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kStage];
+    __shared__ uint32_t bits[kBitW];
+    __shared__ uint16_t smerge[kTT];   // per segment: where its walk merged (position, M_END or M_BAD)
+    __shared__ uint16_t svfrom[kTT];   // per segment on the true chain: its first true token (else M_BAD)
+    __shared__ uint16_t J[2][kTT + 2]; // succ^(2^k) per segment, ping-pong; kTT / kTT + 1 are terminals
+    __shared__ uint8_t reach[kTT + 2]; // segment is on the true chain
+    __shared__ uint32_t scr[8];
+    __shared__ uint32_t sflag[4];      // [0] terminal of the chain, [1] failure, [2] pool base
+    const uint32_t u = blockIdx.x, g = threadIdx.x;
+    if (u >= nunits) return;
+    const DecUnit U = units[u];
+    bool take = U.n == 1 && !(unit_lb && unit_lb[u]);
+    DecBlock B;
+    if (take) {
+        B = blk[U.first];
+        take = !(B.flags & DB_STORED) && B.csize >= 1u && B.csize <= kMaxC;
+    }
+    if (!take) {
+        if (g == 0) a.unit_fast[u] = 0;
+        return;
+    }
+    const uint32_t C = B.csize;
+    const uint64_t tp0 = FP_NOW();
+    // ---- stage the block: aligned 16-byte loads (never outside the 16-byte granules holding
+    // block bytes), four in flight per thread before their LDS stores
+    const uint8_t* in = src + B.src_off;
+    const uint32_t mis = (uint32_t)((uintptr_t)in & 15u);
+    {
+        // (mis + C + 15) / 16 <= 2050 granules: at most 9 per thread, all loads in flight at once
+        const uint4* gw = (const uint4*)(in - mis);
+        const uint32_t nv = (mis + C + 15u) >> 4;
+        static_assert((kMaxC + 30u) / 16u <= 9u * kTT, "staging covers the largest block");
+        uint4 v0, v1, v2, v3, v4, v5, v6, v7, v8;
+#define S3HC_LDG(i, v) if (g + (i) * kTT < nv) v = gw[g + (i) * kTT];
+#define S3HC_STS(i, v) if (g + (i) * kTT < nv) ((uint4*)stage)[g + (i) * kTT] = v;
+        S3HC_LDG(0, v0) S3HC_LDG(1, v1) S3HC_LDG(2, v2) S3HC_LDG(3, v3) S3HC_LDG(4, v4)
+        S3HC_LDG(5, v5) S3HC_LDG(6, v6) S3HC_LDG(7, v7) S3HC_LDG(8, v8)
+        S3HC_STS(0, v0) S3HC_STS(1, v1) S3HC_STS(2, v2) S3HC_STS(3, v3) S3HC_STS(4, v4)
+        S3HC_STS(5, v5) S3HC_STS(6, v6) S3HC_STS(7, v7) S3HC_STS(8, v8)
+#undef S3HC_LDG
+#undef S3HC_STS
+        for (uint32_t k = g; k < (C + 31u) / 32u; k += kTT) bits[k] = 0u;
+        reach[g] = g == 0 ? 1 : 0;
+        if (g == 0) {
+            sflag[0] = kTermBad;
+            sflag[1] = 0u;
+        }
+    }
+    __syncthreads();
+    if (g < 48u) stage[mis + C + g] = 0;  // read-ahead past the block reads zeros
+    __syncthreads();
+
+    const uint64_t tp1 = FP_NOW();
+    // ---- walk 1: from the start of my segment to its end, marking every position visited
+    const uint32_t segL = (C + kTT - 1u) / kTT;
+    const uint32_t s0 = umin_(g * segL, C), s1 = umin_(s0 + segL, C);
+    uint32_t p = s0;
+    while (p < s1) {
+        atomicOr(&bits[p >> 5], 1u << (p & 31u));
+        p = hop(stage, mis, p, C).nxt;
+    }
+    const uint32_t x = s0 < s1 ? p : DEAD;
+    __syncthreads();
+    const uint64_t tp2 = FP_NOW();
+    // ---- walk 2: past the segment until the chain lands on a marked position (merge)
+    uint32_t m = x, ovf = 0;
+    while (m < C) {
+        if ((bits[m >> 5] >> (m & 31u)) & 1u) break;
+        if (ovf == kOvfCap) {
+            m = DEAD;
+            break;
+        }
+        m = hop(stage, mis, m, C).nxt;
+        ++ovf;
+    }
+#ifdef FPROF
+    {
+        uint32_t mx = ovf;
+        for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+        if ((g & 63u) == 0) FP_ADD(10, mx);
+    }
+#endif
+    smerge[g] = (uint16_t)(m < C ? m : (m == END ? kMEnd : kMBad));
+    svfrom[g] = kMBad;
+    // successor segment of my walk: the segment of the merge point, or a terminal
+    J[0][g] = (uint16_t)(m < C ? m / segL : (m == END ? kTermEnd : kTermBad));
+    if (g < 2) {
+        J[0][kTT + g] = J[1][kTT + g] = (uint16_t)(kTT + g);
+        reach[kTT + g] = 0;
+    }
+    __syncthreads();
+    const uint64_t tp3 = FP_NOW();
+    // ---- the true chain: segment 0, then the segment its walk merged into, ... Reachability
+    // from segment 0 by doubling: after step k every segment within 2^(k+1) links is marked.
+#pragma unroll
+    for (uint32_t k = 0; k < kLv; ++k) {
+        const uint32_t h = J[k & 1][g];
+        if (reach[g]) reach[h] = 1;
+        J[(k + 1) & 1][g] = J[k & 1][h];
+        __syncthreads();
+    }
+    // a segment on the chain hands its merge point to its successor (that segment's first true
+    // token); the chain's last segment ends it: END, or a malformed / abandoned walk
+    if (reach[g]) {
+        const uint32_t sm = smerge[g];
+        if (sm < kMEnd) svfrom[sm / segL] = (uint16_t)sm;
+        else sflag[0] = sm == kMEnd ? kTermEnd : kTermBad;
+    }
+    if (g == 0) svfrom[0] = 0;
+    __syncthreads();
+    if (sflag[0] != kTermEnd) {
+        if (g == 0) a.unit_fast[u] = 0;
+        return;
+    }
+    const uint64_t tp4 = FP_NOW();
+    // ---- the true token bitmap: in a segment on the chain the marks before its first true
+    // token are speculative (cleared), a segment off the chain is cleared whole; the chain's
+    // walks past their segments (walk 2) then mark the tokens they passed
+    const uint32_t vf = svfrom[g];
+    const bool valid = vf != kMBad;
+    {
+        const uint32_t c1 = valid ? vf : s1;  // clear [s0, c1)
+        for (uint32_t q = s0; q < c1;) {
+            const uint32_t w = q >> 5, lo = q & 31u, hi = umin_(32u, c1 - (w << 5));
+            const uint32_t mk = (hi == 32u ? ~0u : (1u << hi) - 1u) & (~0u << lo);
+            atomicAnd(&bits[w], ~mk);
+            q = (w + 1) << 5;
+        }
+    }
+    __syncthreads();
+    const uint64_t tp5 = FP_NOW();
+    // ---- validate (lz4_flex bounds: output within the block limit and the caller's capacity,
+    // every offset non-zero and within the bytes produced before its match) while marking the
+    // tokens past my segment
+    uint32_t o = 0, ntok = 0;
+    int32_t minsl = 0x7FFFFFFF;
+    bool bad = false;
+    if (valid) {
+        p = vf;
+        while (p != m) {
+            if (p >= C) {  // END or DEAD before the merge point: not the walk 2 saw
+                bad = true;
+                break;
+            }
+            if (p >= s1) atomicOr(&bits[p >> 5], 1u << (p & 31u));
+            const Tok T = hop(stage, mis, p, C);
+            ++ntok;
+            if (T.nxt == DEAD) bad = true;
+            o += T.ll;
+            if (T.nxt != END) {
+                bad |= T.off == 0u;
+                minsl = min(minsl, (int32_t)o - (int32_t)T.off);
+                o += T.ml;
+            }
+            p = T.nxt;
+        }
+    }
+    const uint64_t tp6 = FP_NOW();
+    uint32_t Utot, N;
+    const uint32_t obase = wg_excl_scan(o, scr, &Utot);
+    (void)wg_excl_scan(ntok, scr, &N);
+    const bool fail = bad || (valid && (int64_t)obase + minsl < 0);
+    if (fail) sflag[1] = 1u;
+    __syncthreads();
+    const bool ok = !sflag[1] && Utot <= B.limit && Utot <= B.cap;
+    if (ok) {
+        uint32_t* gb = a.bmp + (size_t)u * kBitW;
+        for (uint32_t k = g; k < (C + 31u) / 32u; k += kTT) gb[k] = bits[k];
+    }
+    if (g == 0) {
+        if (ok) {
+            FastUnit F;
+            F.ntok = N;
+            F.U = Utot;
+            F.pad0 = F.pad1 = 0;
+            a.fu[u] = F;
+        }
+        a.unit_fast[u] = ok ? 1 : 0;
+    }
+#ifdef FPROF
+    if ((g & 63u) == 0) {
+        FP_ADD(0, tp1 - tp0);
+        FP_ADD(1, tp2 - tp1);
+        FP_ADD(2, tp3 - tp2);
+        FP_ADD(3, tp4 - tp3);
+        FP_ADD(4, tp5 - tp4);
+        FP_ADD(5, tp6 - tp5);
+        FP_ADD(6, FP_NOW() - tp0);
+        FP_ADD(7, 1);
+    }
+#endif
+}
+
+// ------------------------------------------------------------------ k_dexec
+// One wave per block. Windows of 64 tokens (one sequence per lane; token positions from k_dtok,
+// the token bytes and literals read straight from the compressed block in HBM/L2), executed in
+// batches of <= kWin output bytes into an LDS ring of the block's recent output:
+//   literals   every lane copies its literal run (16 bytes per step);
+//   matches    sources older than the ring come from the block's output in HBM (flushed windows
+//              ago), sources before the batch from the ring; sources inside the batch wait for
+//              the first unfinished sequence: each round, the lowest lane still pending and every
+//              pending lane whose source ends before that lane's match start copy (multi-round
+//              resolution; log text needs ~5 rounds per 64 sequences);
+//   flush      whole 1 KiB pieces of the ring to HBM.
+// A sequence longer than kWin runs alone, wave-wide, in 1 KiB pieces (overlapping matches by
+// growing multiples of their period).
+namespace fst {
+constexpr uint32_t kOR = 8192;       // output ring (bytes)
+constexpr uint32_t kORW = kOR / 4;
+constexpr uint32_t kORM = kOR - 1;
+constexpr uint32_t kWin = 2048;      // output bytes of one batch, at most
+constexpr uint32_t kFl = 1024;       // flush granule
+constexpr uint32_t kQ = 512;         // token queue entries (>= 4 windows + one 16-word refill)
+static_assert(2 * kWin + kFl <= kOR, "far sources of a batch must be flushed before it runs");
+}  // namespace fst
+
+namespace {
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint4 uint4u __attribute__((aligned(1)));
+typedef uint32_t u32u __attribute__((aligned(1)));
+
+// 16 bytes at any global address (hardware unaligned access)
+__device__ __forceinline__ uint4 gld16(const uint8_t* p) { return *(const uint4u*)p; }
+__device__ __forceinline__ uint32_t gld4(const uint8_t* p) { return *(const u32u*)p; }
+
+// 16 bytes at block byte p of a compressed block of C bytes: a block is always followed by at
+// least 4 bytes of its frame (next block word or EndMark), so loads ending by C + 4 stay inside
+// the frame; a load reaching further (the block's last literals) is done bytewise, zero-filled
+__device__ __forceinline__ uint4 gld16_blk(const uint8_t* in, uint32_t p, uint32_t C) {
+    if (p + 16u <= C + 4u) return gld16(in + p);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t k = 0; k < 16u && p + k < C; ++k) w[k >> 2] |= (uint32_t)in[p + k] << (8u * (k & 3u));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// 16 bytes of the ring at byte position y (any alignment, wraps)
+__device__ __forceinline__ uint4 rld16(const uint32_t* ring, uint32_t y) {
+    const uint32_t A = y & fst::kORM, dw = A >> 2, sh = A & 3u;
+    const uint32_t r0 = ring[dw], r1 = ring[(dw + 1) & (fst::kORW - 1)], r2 = ring[(dw + 2) & (fst::kORW - 1)];
+    const uint32_t r3 = ring[(dw + 3) & (fst::kORW - 1)], r4 = ring[(dw + 4) & (fst::kORW - 1)];
+    return make_uint4(__builtin_amdgcn_alignbyte(r1, r0, sh), __builtin_amdgcn_alignbyte(r2, r1, sh),
+                      __builtin_amdgcn_alignbyte(r3, r2, sh), __builtin_amdgcn_alignbyte(r4, r3, sh));
+}
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ void mskor(uint32_t* lds_dw, uint32_t mask, uint32_t data) {
+    const uint32_t addr = (uint32_t)(uintptr_t)(lds_u32*)lds_dw;  // LDS byte address
+    asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(addr), "v"(mask), "v"(data & mask) : "memory");
+}
+
+// the first n (<= 16) bytes of v to the ring at byte position y, exactly (other lanes may be
+// writing the neighbouring bytes of the first and last dword: masked atomic or-writes)
+__device__ __forceinline__ void rst(uint32_t* ring, uint32_t y, uint4 v, uint32_t n) {
+    if (n == 0) return;
+    const uint32_t a = y & 3u, db = (y & fst::kORM) >> 2;
+    const uint32_t s = 32u - 8u * a;  // v shifted up by a bytes: dword i = ({v_i, v_(i-1)} >> s)
+    const uint32_t o0 = (uint32_t)(((uint64_t)v.x << 32) >> s);
+    const uint32_t o1 = (uint32_t)((((uint64_t)v.y << 32) | v.x) >> s);
+    const uint32_t o2 = (uint32_t)((((uint64_t)v.z << 32) | v.y) >> s);
+    const uint32_t o3 = (uint32_t)((((uint64_t)v.w << 32) | v.z) >> s);
+    const uint32_t o4 = (uint32_t)((uint64_t)v.w >> s);
+    const uint32_t e = a + n;  // end byte in the 5-dword window (1..19)
+    auto tmask = [](int x) -> uint32_t {  // bytes below x (clamped to 0..4)
+        const uint32_t c = (uint32_t)min(max(x, 0), 4);
+        return ~(uint32_t)(0xFFFFFFFFull << (8u * c));
+    };
+    const uint32_t m0 = tmask((int)e) & (0xFFFFFFFFu << (8u * a));
+    const uint32_t m1 = tmask((int)e - 4), m2 = tmask((int)e - 8), m3 = tmask((int)e - 12), m4 = tmask((int)e - 16);
+    mskor(ring + db, m0, o0);
+    if (m1) mskor(ring + ((db + 1) & (fst::kORW - 1)), m1, o1);
+    if (m2) mskor(ring + ((db + 2) & (fst::kORW - 1)), m2, o2);
+    if (m3) mskor(ring + ((db + 3) & (fst::kORW - 1)), m3, o3);
+    if (m4) mskor(ring + ((db + 4) & (fst::kORW - 1)), m4, o4);
+}
+
+// ring [from, from + n) -> out + from, n <= kFl, the range contiguous in the ring
+__device__ __forceinline__ void flush_piece(const uint32_t* ring, uint8_t* out, uint32_t from, uint32_t n, uint32_t lane) {
+    const uint8_t* rb = (const uint8_t*)ring;
+    if (n == fst::kFl) {
+        const uint4 v = *(const uint4*)(rb + (from & fst::kORM) + 16u * lane);
+        *(uint4u*)(out + from + 16u * lane) = v;
+    } else {
+        for (uint32_t k = lane; k < n; k += 64) out[from + k] = rb[(from + k) & fst::kORM];
+    }
+}
+}  // namespace
+
+namespace {
+// Token decode of one window lane from its token dword w0 (token + 3 bytes at the token) and the
+// dword w1 at the offset (offset + 2 bytes); runs of three or more extension bytes (rare) are
+// read byte by byte. k_dtok validated the chain: every field is in bounds.
+struct SeqF {
+    uint32_t ll, lit, off, ml;
+};
+__device__ __forceinline__ uint32_t lit_len(const uint8_t* in, uint32_t pos, uint32_t w0, uint32_t& lit) {
+    const uint32_t t = w0 & 0xFFu;
+    uint32_t L = t >> 4, q = pos + 1;
+    if (L == 15u) {
+        uint32_t e = (w0 >> 8) & 0xFFu;
+        L += e;
+        ++q;
+        if (e == 255u) {
+            e = (w0 >> 16) & 0xFFu;
+            L += e;
+            ++q;
+            while (e == 255u) {
+                e = in[q++];
+                L += e;
+            }
+        }
+    }
+    lit = q;
+    return L;
+}
+__device__ __forceinline__ uint32_t match_len(const uint8_t* in, uint32_t mp, uint32_t t, uint32_t w1) {
+    uint32_t M = (t & 15u) + 4u;
+    if ((t & 15u) == 15u) {
+        uint32_t f = (w1 >> 16) & 0xFFu;
+        M += f;
+        if (f == 255u) {
+            f = w1 >> 24;
+            M += f;
+            uint32_t q2 = mp + 4;
+            while (f == 255u) {
+                f = in[q2++];
+                M += f;
+            }
+        }
+    }
+    return M;
+}
+__device__ __forceinline__ uint32_t incl_scan(uint32_t x, uint32_t lane) {
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+}  // namespace
+
+__global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                              const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+                                              uint32_t nunits, uint32_t* __restrict__ blk_out,
+                                              int32_t* __restrict__ blk_status, FastArgs a) {
+    using namespace fst;
+    __shared__ __attribute__((aligned(16))) uint32_t ring[kORW];
+    __shared__ uint16_t tq[kQ];              // token positions, queue entry t = token t
+    __shared__ uint32_t gmap[kWin / 16];     // per 16-byte granule of a window: lane owning its first byte
+    __shared__ uint16_t sdst[64];            // per lane: first output byte (window-relative)
+    const uint32_t u = blockIdx.x;
+    if (u >= nunits || !a.unit_fast[u]) return;
+    const uint32_t lane = threadIdx.x;
+    const DecUnit Un = units[u];
+    const DecBlock B = blk[Un.first];
+    const FastUnit F = a.fu[u];
+    const uint8_t* in = src + B.src_off;
+    uint8_t* out = dst + B.dst_off;
+    const uint32_t* bm = a.bmp + (size_t)u * kBitW;
+    const uint32_t N = F.ntok, C = B.csize, nbw = (C + 31u) >> 5;
+    uint32_t upos = 0, flushed = 0;
+    auto flush_full = [&]() {
+        while (upos - flushed >= kFl) {
+            flush_piece(ring, out, flushed, kFl, lane);
+            flushed += kFl;
+        }
+    };
+    // ---- token queue: the bitmap expanded 16 words at a time (the next 16 prefetched)
+    uint32_t qfill = 0, bw = 0;
+    uint32_t bword = lane < 16u && lane < nbw ? bm[lane] : 0u;
+    auto refill = [&](uint32_t want) {
+        while (qfill < want && bw < nbw) {
+            const uint32_t word = bword;
+            const uint32_t wbase = (bw + lane) << 5;
+            bw += 16;
+            bword = lane < 16u && bw + lane < nbw ? bm[bw + lane] : 0u;
+            const uint32_t pc = (uint32_t)__builtin_popcount(word);
+            const uint32_t incl = incl_scan(pc, lane);
+            uint32_t k = qfill + incl - pc, wv = word;
+            while (wv) {
+                const uint32_t b = (uint32_t)__builtin_ctz(wv);
+                tq[k & (kQ - 1)] = (uint16_t)(wbase + b);
+                ++k;
+                wv &= wv - 1u;
+            }
+            qfill += (uint32_t)__shfl((int)incl, 15, 64);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    const uint32_t nwin = (N + 63u) >> 6;
+    auto tpos = [&](uint32_t w) -> uint32_t {  // my token's position in window w (or C: none)
+        const uint32_t t = 64u * w + lane;
+        return t < N ? (uint32_t)tq[t & (kQ - 1)] : C;
+    };
+    auto ld_w0 = [&](uint32_t pos) -> uint32_t { return pos < C ? gld4(in + pos) : 0u; };
+    // ---- pipeline prologue: window 2's token dword, window 1's offset dword, window 0 decoded
+    refill(64u * 4u);
+    uint32_t w0_c = ld_w0(tpos(0));
+    uint32_t w0_n = ld_w0(tpos(1));
+    // window 0: token + offset dwords now
+    SeqF fc, fn;
+    uint32_t pos_n = tpos(1), mp_n = 0, w1_n = 0;
+    {
+        const uint32_t pos = tpos(0);
+        fc.ll = pos < C ? lit_len(in, pos, w0_c, fc.lit) : 0u;
+        const uint32_t mp = fc.lit + fc.ll;
+        fc.off = fc.ml = 0;
+        if (pos < C && mp < C) {
+            const uint32_t w1 = gld4(in + mp);
+            fc.off = w1 & 0xFFFFu;
+            fc.ml = match_len(in, mp, w0_c & 0xFFu, w1);
+        }
+        if (pos_n < C) {
+            uint32_t lit;
+            const uint32_t ll = lit_len(in, pos_n, w0_n, lit);
+            mp_n = lit + ll;
+            w1_n = mp_n < C ? gld4(in + mp_n) : 0u;
+        }
+    }
+    uint32_t pos_2 = tpos(2);
+    uint32_t w0_2 = ld_w0(pos_2);
+    uint32_t Sincl_c = incl_scan(fc.ll + fc.ml, lane);
+    uint32_t S_c = (uint32_t)__shfl((int)Sincl_c, 63, 64);
+    bool far_c = false, pf_c = false;  // window 0: nothing is far
+    uint4 lit0_c = make_uint4(0, 0, 0, 0), lit1_c = lit0_c, far0_c = lit0_c, far1_c = lit0_c;
+    if (S_c <= kWin) {
+        if (fc.ll) lit0_c = gld16_blk(in, fc.lit, C);
+        if (fc.ll > 16u) lit1_c = gld16_blk(in, fc.lit + 16u, C);
+        pf_c = true;
+    }
+    const uint64_t te0 = FP_NOW();
+    uint64_t tsum[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t nrounds = 0;
+    for (uint32_t w = 0; w < nwin; ++w) {
+        uint64_t tq0 = FP_NOW();
+        const uint32_t nact = umin_(64u, N - 64u * w);
+        const bool act = lane < nact;
+        // ---- stage A: window w+3's token dword
+        refill(64u * (w + 4u));
+        const uint32_t pos_3 = w + 3 < nwin ? tpos(w + 3) : C;
+        const uint32_t w0_3 = ld_w0(pos_3);
+        // ---- stage B: window w+2's offset dword
+        uint32_t mp_2 = 0, w1_2 = 0;
+        if (pos_2 < C) {
+            uint32_t lit;
+            const uint32_t ll = lit_len(in, pos_2, w0_2, lit);
+            mp_2 = lit + ll;
+            w1_2 = mp_2 < C ? gld4(in + mp_2) : 0u;
+        }
+        // ---- stage C: decode window w+1, prefetch its literals and far match sources
+        fn.ll = fn.lit = fn.off = fn.ml = 0;
+        if (pos_n < C) {
+            fn.ll = lit_len(in, pos_n, w0_n, fn.lit);
+            if (mp_n < C) {
+                fn.off = w1_n & 0xFFFFu;
+                fn.ml = match_len(in, mp_n, w0_n & 0xFFu, w1_n);
+            }
+        }
+        const uint32_t Sincl_n = incl_scan(fn.ll + fn.ml, lane);
+        const uint32_t S_n = (uint32_t)__shfl((int)Sincl_n, 63, 64);
+        const bool pf_n = S_c <= kWin && S_n <= kWin;
+        uint4 lit0_n = make_uint4(0, 0, 0, 0), lit1_n = lit0_n, far0_n = lit0_n, far1_n = lit0_n;
+        bool far_n = false;
+        if (S_n <= kWin) {
+            if (fn.ll) lit0_n = gld16_blk(in, fn.lit, C);
+            if (fn.ll > 16u) lit1_n = gld16_blk(in, fn.lit + 16u, C);
+        }
+        if (pf_n && fn.ml) {
+            const uint32_t upos_n = upos + S_c;
+            const uint32_t md = upos_n + Sincl_n - fn.ml, ms = md - fn.off;
+            far_n = ms + kOR < upos_n + S_n && ms < md;
+            if (far_n) {
+                far0_n = gld16(out + ms);
+                if (fn.ml > 16u) far1_n = gld16(out + ms + 16u);
+            }
+        }
+#ifdef FPROF
+        { const uint64_t tn = FP_NOW(); tsum[0] += tn - tq0; tq0 = tn; }
+#endif
+        // ---- execute window w
+        const uint32_t ll = act ? fc.ll : 0u, lit = fc.lit, off = fc.off, ml = act ? fc.ml : 0u;
+        const uint32_t len = ll + ml;
+        if (pf_c && S_c <= kWin) {
+            const uint32_t d0 = upos + Sincl_c - len;
+            // literals (first 32 bytes prefetched)
+            if (act && ll) rst(ring, d0, lit0_c, umin_(16u, ll));
+            if (act && ll > 16u) rst(ring, d0 + 16u, lit1_c, umin_(16u, ll - 16u));
+            for (uint32_t c = 32; __ballot(act && c < ll); c += 16u)
+                if (act && c < ll) rst(ring, d0 + c, gld16_blk(in, lit + c, C), umin_(16u, ll - c));
+#ifdef FPROF
+            __builtin_amdgcn_s_waitcnt(0);
+            { const uint64_t tn = FP_NOW(); tsum[1] += tn - tq0; tq0 = tn; }
+#endif
+            const uint32_t md = d0 + ll, ms = md - off;
+            const bool hasm = act && ml > 0;
+            const bool far = hasm && far_c;
+            bool pend = hasm && !far && ms + ml > upos;
+            const uint32_t step = off < 16u ? off : 16u;
+            // round 0: far sources (prefetched) and sources before the window
+            if (hasm && !pend) {
+                if (far) {
+                    rst(ring, md, far0_c, umin_(16u, ml));
+                    if (ml > 16u) rst(ring, md + 16u, far1_c, umin_(16u, ml - 16u));
+                }
+            }
+            for (uint32_t c = far ? 32u : 0u; __ballot(hasm && !pend && c < ml); c += far ? 16u : step) {
+                if (hasm && !pend && c < ml) {
+                    uint4 v;
+                    if (far) v = gld16(out + ms + c);
+                    else v = rld16(ring, ms + c);
+                    rst(ring, md + c, v, umin_(far ? 16u : step, ml - c));
+                }
+            }
+#ifdef FPROF
+            __builtin_amdgcn_s_waitcnt(0);
+            { const uint64_t tn = FP_NOW(); tsum[2] += tn - tq0; tq0 = tn; }
+#endif
+            // in-window sources: wait for exactly the lanes whose output the source overlaps
+            uint64_t notdone = __ballot(pend);
+            if (notdone) {
+                const uint32_t ex = Sincl_c - len;
+                sdst[lane] = (uint16_t)(act ? ex : 0xFFFFu);
+                if (lane < kWin / 32) ((uint2*)gmap)[lane] = make_uint2(0u, 0u);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t g0 = (ex + 15u) >> 4;
+                if (act && len && g0 < kWin / 16 && ex + len > (g0 << 4)) atomicMax(&gmap[g0], lane);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                {
+                    const uint2 pr = lane < kWin / 32 ? ((const uint2*)gmap)[lane] : make_uint2(0u, 0u);
+                    const uint32_t b = umax_(pr.x, pr.y);
+                    uint32_t x = b;  // inclusive max-scan over lanes
+#pragma unroll
+                    for (uint32_t d = 1; d < 64; d <<= 1) {
+                        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+                        if (lane >= d) x = umax_(x, y);
+                    }
+                    const uint32_t P = x == b ? (uint32_t)__shfl_up((int)x, 1, 64) : x;  // exclusive max
+                    const uint32_t Pex = lane ? umax_(P, 0u) : 0u;
+                    if (lane < kWin / 32) ((uint2*)gmap)[lane] = make_uint2(umax_(Pex, pr.x), umax_(Pex, b));
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                uint64_t dep = 0;
+                if (pend) {
+                    auto owner = [&](uint32_t xr) -> uint32_t {
+                        uint32_t k = gmap[xr >> 4];
+                        while (k + 1u < nact && sdst[k + 1u] <= xr) ++k;
+                        return k;
+                    };
+                    const uint32_t lo = owner((ms > upos ? ms : upos) - upos), hi = owner(ms + ml - 1u - upos);
+                    dep = (hi >= 63u ? ~0ull : ((2ull << hi) - 1ull)) & ~((1ull << lo) - 1ull) & ~(1ull << lane);
+                }
+                for (;;) {
+                    ++nrounds;
+                    const bool run = pend && (dep & notdone) == 0;
+                    for (uint32_t c = 0; __ballot(run && c < ml); c += step)
+                        if (run && c < ml) rst(ring, md + c, rld16(ring, ms + c), umin_(step, ml - c));
+                    notdone &= ~__ballot(run);
+                    pend = pend && !run;
+                    if (!notdone) break;
+                }
+            }
+#ifdef FPROF
+            __builtin_amdgcn_s_waitcnt(0);
+            { const uint64_t tn = FP_NOW(); tsum[3] += tn - tq0; tq0 = tn; }
+#endif
+            upos += S_c;
+            flush_full();
+        } else {
+            // ---- a window of more than kWin output bytes (or right after one): batches of
+            // <= kWin bytes in lane order, sources read at once; sequences longer than a batch run
+            // alone, wave-wide
+            uint32_t i0 = 0;
+            while (i0 < nact) {
+                const uint32_t base = i0 ? (uint32_t)__shfl((int)Sincl_c, (int)(i0 - 1), 64) : 0u;
+                const uint64_t fit = __ballot(act && lane >= i0 && Sincl_c - base <= kWin);
+                const uint32_t i1 = fit ? 64u - (uint32_t)__builtin_clzll(fit) : i0;
+                if (i1 <= i0) {
+                    const uint32_t sll = (uint32_t)__shfl((int)ll, (int)i0, 64), slit = (uint32_t)__shfl((int)lit, (int)i0, 64);
+                    const uint32_t soff = (uint32_t)__shfl((int)off, (int)i0, 64), sml = (uint32_t)__shfl((int)ml, (int)i0, 64);
+                    for (uint32_t k = 0; k < sll; k += kFl) {
+                        const uint32_t piece = umin_(kFl, sll - k);
+                        const uint32_t j = 16u * lane;
+                        if (j < piece) rst(ring, upos + j, gld16_blk(in, slit + k + j, C), umin_(16u, piece - j));
+                        upos += piece;
+                        flush_full();
+                    }
+                    const uint32_t mdst = upos;
+                    for (uint32_t k = 0; k < sml;) {
+                        uint32_t piece = umin_(kFl, sml - k), P = soff;
+                        if (soff < piece) {
+                            P = soff * ((piece + soff - 1) / soff);
+                            if (P > k + soff) P = soff * ((k + soff) / soff);
+                            piece = umin_(piece, P);
+                        }
+                        const uint32_t j = 16u * lane;
+                        if (j < piece) {
+                            const uint32_t y = mdst + k - P + j, n = umin_(16u, piece - j);
+                            uint4 v;
+                            if (y + kOR < upos + piece && y < upos) v = gld16(out + y);
+                            else v = rld16(ring, y);
+                            rst(ring, upos + j, v, n);
+                        }
+                        k += piece;
+                        upos += piece;
+                        flush_full();
+                    }
+                    i0 = i0 + 1;
+                    continue;
+                }
+                const bool inb = act && lane >= i0 && lane < i1;
+                const uint32_t Sb = (uint32_t)__shfl((int)Sincl_c, (int)(i1 - 1), 64) - base;
+                const uint32_t d0 = upos + Sincl_c - len - base;
+                for (uint32_t c = 0; __ballot(inb && c < ll); c += 16u)
+                    if (inb && c < ll) rst(ring, d0 + c, gld16_blk(in, lit + c, C), umin_(16u, ll - c));
+                const uint32_t md = d0 + ll, ms = md - off;
+                const bool hasm = inb && ml > 0;
+                const bool far = hasm && ms + kOR < upos + Sb && ms < md;
+                bool pend = hasm && !far && ms + ml > upos;
+                bool run = hasm && !pend;
+                const uint32_t step = off < 16u ? off : 16u;
+                for (;;) {
+                    for (uint32_t c = 0; __ballot(run && c < ml); c += step) {
+                        if (run && c < ml) {
+                            uint4 v;
+                            if (far) v = gld16(out + ms + c);
+                            else v = rld16(ring, ms + c);
+                            rst(ring, md + c, v, umin_(step, ml - c));
+                        }
+                    }
+                    const uint64_t pm = __ballot(pend);
+                    if (!pm) break;
+                    const uint32_t first = (uint32_t)__builtin_ctzll(pm);
+                    const uint32_t h = (uint32_t)__shfl((int)md, (int)first, 64);
+                    run = pend && (lane == first || (off >= ml && ms + ml <= h));
+                    pend = pend && !run;
+                }
+                upos += Sb;
+                flush_full();
+                i0 = i1;
+            }
+        }
+#ifdef FPROF
+        __builtin_amdgcn_s_waitcnt(0);
+        { const uint64_t tn = FP_NOW(); tsum[4] += tn - tq0; tq0 = tn; }
+#endif
+        // ---- rotate the pipeline
+        fc = fn;
+        Sincl_c = Sincl_n;
+        S_c = S_n;
+        pf_c = pf_n;
+        far_c = far_n;
+        lit0_c = lit0_n;
+        lit1_c = lit1_n;
+        far0_c = far0_n;
+        far1_c = far1_n;
+        pos_n = pos_2;
+        w0_n = w0_2;
+        mp_n = mp_2;
+        w1_n = w1_2;
+        pos_2 = pos_3;
+        w0_2 = w0_3;
+    }
+    // ---- the rest of the output (< kFl bytes)
+    if (upos > flushed) {
+        const uint32_t n = upos - flushed, first = kOR - (flushed & kORM);
+        if (n <= first) flush_piece(ring, out, flushed, n, lane);
+        else {
+            flush_piece(ring, out, flushed, first, lane);
+            flush_piece(ring, out, flushed + first, n - first, lane);
+        }
+    }
+    if (lane == 0) {
+        blk_out[Un.first] = upos;
+        blk_status[Un.first] = S3HC_OK;
+    }
+#ifdef FPROF
+    if (lane == 0) {
+        for (int k = 0; k < 5; ++k) FP_ADD(16 + k, tsum[k]);
+        FP_ADD(21, FP_NOW() - te0);
+        FP_ADD(22, nwin);
+        FP_ADD(23, nrounds);
+        FP_ADD(24, 1);
+    }
+#endif
+}
+
+// ================================================================ launchers
+static inline uint32_t fcdiv(uint64_t x, uint64_t y) { return (uint32_t)((x + y - 1) / y); }
+
+hipError_t launch_fast_tok(const uint8_t* src, const DecBlock* blk, const DecUnit* units, uint32_t nunits,
+                           const uint8_t* unit_lb, const FastArgs& a, hipStream_t st) {
+    if (!nunits) return hipSuccess;
+    hipLaunchKernelGGL(k_dtok, dim3(nunits), dim3(fst::kTT), 0, st, src, blk, units, nunits, unit_lb, a);
+    return hipGetLastError();
+}
+#ifdef FPROF
+extern "C" int s3hc_diag_fprof(unsigned long long* out, int n, int reset) {
+    if (n > 32) n = 32;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fprof), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_fprof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+hipError_t launch_fast_exec(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
+                            uint32_t nunits, uint32_t* blk_out, int32_t* blk_status, const FastArgs& a,
+                            hipStream_t st) {
+    if (!nunits) return hipSuccess;
+    hipLaunchKernelGGL(k_dexec, dim3(nunits), dim3(64), 0, st, src, dst, blk, units, nunits, blk_out, blk_status, a);
+    return hipGetLastError();
+}
+}  // namespace s3hc

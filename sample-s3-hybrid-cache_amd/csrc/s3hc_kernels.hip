@@ -910,7 +910,8 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
                                                       const DecUnit* __restrict__ units, uint32_t nunits,
                                                       uint32_t* __restrict__ blk_out,
                                                       int32_t* __restrict__ blk_status,
-                                                      const uint8_t* __restrict__ unit_lb) {
+                                                      const uint8_t* __restrict__ unit_lb,
+                                                      const uint8_t* __restrict__ unit_fast) {
 #ifndef S3HC_DEC_LDS_PAD
 #define S3HC_DEC_LDS_PAD 0  // diagnostic builds: extra LDS per workgroup to lower occupancy
 #endif
@@ -920,6 +921,7 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
     const uint32_t u = blockIdx.x * dec::kWaves + wv;
     if (u >= nunits) return;
     if (unit_lb && unit_lb[u]) return;  // decoded by the large-block path (s3hc_lb.hip)
+    if (unit_fast && unit_fast[u]) return;  // decoded by the 64 KiB-block path (s3hc_fast.hip)
     const DecUnit U = units[u];
     if (U.n == 0) return;
     DecWave w;
@@ -1010,13 +1012,14 @@ static_assert(kLds <= 10240, "16 units per CU (a 4096-block batch resident at on
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAVES_PER_EU, 8))) void k_decode_pe(
     const uint8_t* __restrict__ src, uint8_t* dst, const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
     uint32_t nunits, uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
-    const uint8_t* __restrict__ unit_lb) {
+    const uint8_t* __restrict__ unit_lb, const uint8_t* __restrict__ unit_fast) {
     using namespace dec;
     using dpe::Slot;
     __shared__ __attribute__((aligned(16))) uint8_t smem[dpe::kLds];
     const uint32_t u = blockIdx.x;
     if (u >= nunits) return;
     if (unit_lb && unit_lb[u]) return;  // decoded by the large-block path (s3hc_lb.hip)
+    if (unit_fast && unit_fast[u]) return;  // decoded by the 64 KiB-block path (s3hc_fast.hip)
     const DecUnit U = units[u];
     if (U.n == 0) return;
     const int lane = lane_id();
@@ -2257,16 +2260,16 @@ hipError_t launch_xxh32(const uint8_t* base, const uint64_t* off, const uint32_t
 }
 hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
                                uint32_t nunits, uint32_t* blk_out, int32_t* blk_status, const uint8_t* unit_lb,
-                               hipStream_t st) {
+                               const uint8_t* unit_fast, hipStream_t st) {
     if (!nunits) return hipSuccess;
     // S3HC_DEC_ONEWAVE=1 (comparisons): one wave per unit doing both halves (k_decode_units)
     const bool onewave = getenv("S3HC_DEC_ONEWAVE") != nullptr;  // read per launch (tests toggle it)
     if (onewave)
         hipLaunchKernelGGL(k_decode_units, dim3(cdiv(nunits, dec::kWaves)), dim3(64 * dec::kWaves), 0, st, src, dst,
-                           blk, units, nunits, blk_out, blk_status, unit_lb);
+                           blk, units, nunits, blk_out, blk_status, unit_lb, unit_fast);
     else
         hipLaunchKernelGGL(k_decode_pe, dim3(nunits), dim3(128), 0, st, src, dst, blk, units, nunits, blk_out,
-                           blk_status, unit_lb);
+                           blk_status, unit_lb, unit_fast);
     return hipGetLastError();
 }
 hipError_t launch_enc_parse(const uint8_t* src, const EncBlock* blocks, const uint2* groups, uint32_t ngroups,

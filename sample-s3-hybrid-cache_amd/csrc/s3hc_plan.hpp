@@ -177,5 +177,24 @@ struct LbArgs {
     uint8_t* tinit;        // per tile: some byte was left pending by k_lbw_init (needs the gather)
 };
 
+// ---- 64 KiB-block decode fast path ------------------------
+// k_dtok finds every token of a block (speculative segment walks over the LDS-staged block,
+// chains merged by pointer doubling) and validates the block against lz4_flex's bounds; it
+// hands the token positions to k_dexec, which executes 64 sequences at a time, one per lane.
+// Blocks it does not take (stored, > kFastMaxC compressed bytes, multi-block units, anything
+// malformed or out of bounds) go to the per-unit decoder, which also reports their exact status.
+constexpr uint32_t kFastMaxC = 32768;  // compressed bytes of a block the fast path takes
+
+struct FastUnit {        // 16 bytes, written by k_dtok for every unit it takes
+    uint32_t ntok;       // sequences (the last one has no match)
+    uint32_t U;          // decoded bytes
+    uint32_t pad0, pad1;
+};
+
+struct FastArgs {
+    uint32_t* bmp;       // per unit, kFastMaxC / 32 words: bit p = a token starts at block byte p
+    FastUnit* fu;        // per unit
+    uint8_t* unit_fast;  // per unit: 1 = decoded by the fast path
+};
 
 }  // namespace s3hc

@@ -31,7 +31,11 @@ hipError_t launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32
 hipError_t launch_compat_frames(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint8_t*, const uint64_t*,
                                 const uint32_t*, uint32_t*, uint32_t, hipStream_t);
 hipError_t launch_decode_units(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*,
-                               int32_t*, const uint8_t*, hipStream_t);
+                               int32_t*, const uint8_t*, const uint8_t*, hipStream_t);
+hipError_t launch_fast_tok(const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint8_t*, const FastArgs&,
+                           hipStream_t);
+hipError_t launch_fast_exec(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*, int32_t*,
+                            const FastArgs&, hipStream_t);
 hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*, int32_t*,
                            hipStream_t);
 hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, uint32_t*, int32_t*, hipStream_t);
@@ -364,6 +368,23 @@ struct LbScratch {
     DevBuf lbt, ctl, unit_lb, chunk_blk, nzg, E, J0, entry, trec, ntok, slsum, badrel, tokbase, outbase, total, seq4,
         seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst, blk_hash, wbase, wtile0, wP, tpend, tinit;
     LbArgs a{};
+    // 64 KiB-block fast path (s3hc_fast.hip): per-unit token bitmaps and results
+    DevBuf f_bmp, f_fu, f_unit_fast;
+    FastArgs fa{};
+    bool fast_ready = false;
+    hipError_t prepare_fast(uint32_t nunits) {
+        fast_ready = false;
+        if (!nunits) return hipSuccess;
+        hipError_t e;
+        if ((e = f_bmp.ensure((size_t)nunits * (kFastMaxC / 8) + 64)) != hipSuccess) return e;
+        if ((e = f_fu.ensure((size_t)nunits * sizeof(FastUnit) + 64)) != hipSuccess) return e;
+        if ((e = f_unit_fast.ensure((size_t)nunits + 64)) != hipSuccess) return e;
+        fa.bmp = f_bmp.as<uint32_t>();
+        fa.fu = f_fu.as<FastUnit>();
+        fa.unit_fast = f_unit_fast.as<uint8_t>();
+        fast_ready = true;
+        return hipSuccess;
+    }
     bool active = false;
     bool all_lb = false;  // every unit of the launch is a taken large block (host walks know): no unit decoder launch
     // nunits: units of the launch; nblocks: its DecBlock count (block hashes are per DecBlock)
@@ -420,6 +441,14 @@ struct LbScratch {
     }
 };
 
+// The 64 KiB-block fast path (s3hc_fast.hip) is opt-in while it is slower than the per-unit
+// decoder on config 2 (S3HC_FAST=1 enables it; S3HC_FAST_DISABLE=1 always wins).
+static bool fast_path_enabled() {
+    if (getenv("S3HC_FAST_DISABLE")) return false;
+    const char* e = getenv("S3HC_FAST");
+    return e && e[0] == '1';
+}
+
 // Block decode of a batch: large blocks by the large-block path (when L is active), the rest
 // one wave per unit. *blk_hash: the large-block path's per-block output hashes (single-block
 // units: 1 << 32 | xxh32, or 0), nullptr when the path did not run.
@@ -431,9 +460,28 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
     if (blk_hash) *blk_hash = lb ? L->a.blk_hash : nullptr;
     hipError_t e;
     if (lb && (e = launch_lb_parse(L->a, src, blk, units, nunits, blk_out, blk_status, st)) != hipSuccess) return e;
+    // 64 KiB blocks: token index + executor (S3HC_FAST_DISABLE=1: every block on the per-unit
+    // decoder, for comparisons); blocks the fast path leaves go to the per-unit decoder below
+    const bool fast = L && L->fast_ready && nunits && !(lb && L->all_lb) && fast_path_enabled();
+    if (fast) {
+        if ((e = launch_fast_tok(src, blk, units, nunits, lb ? L->a.unit_lb : nullptr, L->fa, st)) != hipSuccess) return e;
+        if ((e = launch_fast_exec(src, dst, blk, units, nunits, blk_out, blk_status, L->fa, st)) != hipSuccess) return e;
+        if (getenv("S3HC_FAST_TRACE")) {  // diagnostics: units the fast path took
+            std::vector<uint8_t> f(nunits);
+            std::vector<FastUnit> fu(nunits);
+            if ((e = hipMemcpyAsync(f.data(), L->fa.unit_fast, nunits, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+            if ((e = hipMemcpyAsync(fu.data(), L->fa.fu, nunits * sizeof(FastUnit), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+            uint32_t k = 0;
+            uint64_t ntok = 0;
+            for (uint32_t i = 0; i < nunits; ++i)
+                if (f[i]) { ++k; ntok += fu[i].ntok; }
+            fprintf(stderr, "[s3hc fast] units %u taken %u tokens %llu\n", nunits, k, (unsigned long long)ntok);
+        }
+    }
     if (!(lb && L->all_lb) &&
         (e = launch_decode_units(src, dst, blk, units, nunits, blk_out, blk_status, lb ? L->a.unit_lb : nullptr,
-                                 st)) != hipSuccess)
+                                 fast ? L->fa.unit_fast : nullptr, st)) != hipSuccess)
         return e;
     if (lb && (e = launch_lb_exec(L->a, src, dst, blk_out, blk_status, st)) != hipSuccess) return e;
     if (lb && getenv("S3HC_LB_TRACE")) {  // diagnostics: blocks and chunks taken
@@ -802,6 +850,7 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
             }
         }
         HIPCHK(P->lb.prepare(P->blk_cap, P->blk_cap, lc));
+        HIPCHK(P->lb.prepare_fast(P->blk_cap));
         HIPCHK(hipStreamSynchronize(st));
         *out = P.release();
         return S3HC_OK;
@@ -1151,8 +1200,8 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
     const uint32_t* bo = nullptr;
     const int32_t* bs = nullptr;
     const uint32_t *cs_got = nullptr, *flen = nullptr, *fhash = nullptr;
-    bool spec = false;  // the decoded slots [0, spec_bytes) are in hs.buf[0]
-    uint64_t spec_bytes = 0;
+    bool spec = false;  // each frame's slot prefix [out_off, out_off + spre[f]) is in hs.buf[0] at spos[f]
+    std::vector<uint64_t> spre, spos;
     if (stopped_out) *stopped_out = false;
     if (nb) {
         if (upload_in) {
@@ -1176,6 +1225,7 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         for (auto& U : units)
             if (lb_candidate(W.blocks[U.first], U.n == 1, lc.min_limit)) lc.add_block(W.blocks[U.first].csize, std::min(W.blocks[U.first].limit, W.blocks[U.first].cap), W.blocks[U.first].limit);
         HIPCHK(ctx->lb.prepare((uint32_t)units.size(), (uint32_t)nb, lc));
+        HIPCHK(ctx->lb.prepare_fast((uint32_t)units.size()));
         const uint64_t* bh = nullptr;
         HTRACE("launch")
         HIPCHK(decode_launch(&ctx->lb, ctx->d_in.as<uint8_t>(), ctx->d_out.as<uint8_t>(), ctx->d_blocks.as<DecBlock>(),
@@ -1227,15 +1277,39 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         HIPCHK(hipMemcpyAsync(rb + 3 * nb, ctx->d_flen.p, nf * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipMemcpyAsync(rb + 3 * nb + nf, ctx->d_fhash.p, nf * 4, hipMemcpyDeviceToHost, st));
         // small outputs: their slots come back in the same round trip (pageable destinations).
-        // Only a prefix of max(4 x input, 1 MiB) bytes: a BD 0x70 frame's slot is 4 MiB whatever it
-        // decodes to (lz4_flex writes no content size); output beyond the prefix (rare: ratios
-        // above 4) takes the second round trip below.
-        spec_bytes = std::min<uint64_t>(W.slot_total, std::max<uint64_t>(4 * (uint64_t)n, 1u << 20));
-        spec = spec_bytes <= kSpecBytes && (vout || !host_pinned(dst));
-        if (spec) {
-            HIPCHK(hs.init(spec_bytes));
-            HIPCHK(hs.buf[0].ensure(spec_bytes + 16));
-            HIPCHK(hipMemcpyAsync(hs.buf[0].p, ctx->d_out.p, spec_bytes, hipMemcpyDeviceToHost, st));
+        // Per frame only a prefix of its slot, min(slot, max(4 x the frame's compressed bytes,
+        // 1 MiB)): a BD 0x70 frame's slot is 4 MiB whatever it decodes to (lz4_flex writes no
+        // content size). The prefixes are packed in the staging buffer; adjacent ones (whole
+        // slots) are copied in one piece. A frame decoding past its prefix (ratios above 4) sends
+        // the delivery through the second round trip below.
+        {
+            spre.assign(nf, 0);
+            spos.assign(nf, 0);
+            uint64_t stot = 0;
+            for (size_t f = 0; f < nf; ++f) {
+                const HFrame& F = W.frames[f];
+                uint64_t slot = 0;
+                for (uint32_t k = 0; k < F.nblk; ++k) slot += W.blocks[F.blk0 + k].cap;
+                const uint64_t fc = (f + 1 < nf ? W.frames[f + 1].pos : n) - F.pos;
+                spre[f] = std::min<uint64_t>(slot, std::max<uint64_t>(4 * fc, 1u << 20));
+                spos[f] = stot;
+                stot += spre[f];
+            }
+            spec = stot <= kSpecBytes && (vout || !host_pinned(dst));
+            if (spec && stot) {
+                HIPCHK(hs.init(stot));
+                HIPCHK(hs.buf[0].ensure(stot + 16));
+                size_t f = 0;
+                while (f < nf) {  // one copy per run of frames whose device ranges abut
+                    size_t g = f + 1;
+                    while (g < nf && W.frames[g - 1].out_off + spre[g - 1] == W.frames[g].out_off) ++g;
+                    const uint64_t bytes = spos[g - 1] + spre[g - 1] - spos[f];
+                    if (bytes)
+                        HIPCHK(hipMemcpyAsync(hs.buf[0].p + spos[f], ctx->d_out.as<uint8_t>() + W.frames[f].out_off,
+                                              bytes, hipMemcpyDeviceToHost, st));
+                    f = g;
+                }
+            }
         }
         HTRACE("queued")
         HIPCHK(hipStreamSynchronize(st));
@@ -1361,12 +1435,22 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         if (!spans.empty() && spans.back().first + spans.back().second == fpos[f]) spans.back().second += fout[f];
         else spans.push_back({fpos[f], fout[f]});
     }
-    if (spec && !spans.empty() && spans.back().first + spans.back().second > spec_bytes) spec = false;
+    if (spec)
+        for (size_t f = 0; f < use_frames; ++f)
+            if (fout[f] > spre[f]) spec = false;  // decoded past the prefix read back early
     if (spec) {
+        // frames' bytes from their packed prefixes; adjacent frames whose prefixes are whole
+        // slots sit back to back in staging too, so runs stay one copy
         uint64_t o = 0;
-        for (auto& sp : spans) {
-            par_memcpy(hdst + o, hs.buf[0].p + sp.first, sp.second);
-            o += sp.second;
+        size_t f = 0;
+        while (f < use_frames) {
+            size_t g = f + 1;
+            while (g < use_frames && fout[g - 1] == spre[g - 1] && spos[g - 1] + spre[g - 1] == spos[g]) ++g;
+            uint64_t bytes = 0;
+            for (size_t k = f; k < g; ++k) bytes += fout[k];
+            if (bytes) par_memcpy(hdst + o, hs.buf[0].p + spos[f], bytes);
+            o += bytes;
+            f = g;
         }
     } else {
         for (auto& sp : spans) runs.push_back({dev_out + sp.first, sp.second});
@@ -1803,6 +1887,7 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
         for (auto& U : units)
             if (lb_candidate(mb[U.first], U.n == 1, lc.min_limit)) lc.add_block(mb[U.first].csize, std::min(mb[U.first].limit, mb[U.first].cap), mb[U.first].limit);
         HIPCHK(S.lb.prepare(nu, nbk, lc));
+        HIPCHK(S.lb.prepare_fast(nu));
     }
     HIPCHK(S.h_res.ensure(8ull * n));
     HIPCHK(hipMemcpyAsync(S.d_in.p, S.h_in.p, nin, hipMemcpyHostToDevice, st));

@@ -424,14 +424,35 @@ static int drain(s3hc_writer* w) {
     }
 }
 
+// Frees a writer when commit returns, however it returns: commit consumes the writer, so an
+// exception out of queue_batch / drain (caught by guarded()) must not leak it. On that path the
+// writer's queued batches are drained first (they reference it), as s3hc_writer_abort does.
+struct WriterReaper {
+    s3hc_writer* w;
+    ~WriterReaper() {
+        if (!w) return;
+        try {
+            {
+                std::lock_guard<std::mutex> g(w->agg->mu);
+                set_writer_error(w, S3HC_INVALID_ARG, "commit failed");
+            }
+            (void)drain(w);
+        } catch (...) {
+        }
+        delete w;
+    }
+};
+
 extern "C" int s3hc_writer_commit(s3hc_writer* w, double min_commit_ratio, uint64_t spec_out[4]) {
+    if (!w) return werr(S3HC_INVALID_ARG, "bad arguments");
+    WriterReaper reaper{w};
     return guarded([&]() -> int {
-        if (!w) return werr(S3HC_INVALID_ARG, "bad arguments");
         // finalize_incremental_range: residual batch first (disk_cache.rs:1981-1986)
         queue_batch(w);
         int rc = drain(w);
         if (!rc) rc = writer_error(w);
         if (rc) {
+            reaper.w = nullptr;
             delete w;  // the reference removes the .tmp file; the caller discards what its sink wrote
             return rc;
         }
@@ -445,6 +466,7 @@ extern "C" int s3hc_writer_commit(s3hc_writer* w, double min_commit_ratio, uint6
                 char m[160];
                 snprintf(m, sizeof m, "Incremental write size mismatch: expected %llu bytes, got %llu",
                          (unsigned long long)expected, (unsigned long long)w->bytes_written);
+                reaper.w = nullptr;
                 delete w;
                 return werr(S3HC_INVALID_ARG, m);
             }
@@ -457,6 +479,7 @@ extern "C" int s3hc_writer_commit(s3hc_writer* w, double min_commit_ratio, uint6
             spec_out[2] = w->compressed_bytes_written;
             spec_out[3] = w->bytes_written;
         }
+        reaper.w = nullptr;
         delete w;
         return S3HC_OK;
     });

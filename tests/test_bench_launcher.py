@@ -40,6 +40,13 @@ def test_config5_strong_split():
     assert d["n_gpus"] == 2 and d["blocks_total"] == 1048576 and d["scaling"] == "strong"
 
 
+def test_dead_rank_does_not_hang_the_launcher():
+    # rank 1 exits before the first collective: the launcher must kill rank 0 (blocked in gloo)
+    # and report rank 1's status instead of waiting for gloo's 30-minute timeout
+    r = _run(["--gpus", "2", "--selftest"], {"S3HC_SELFTEST_FAIL_RANK": "1"}, timeout=120)
+    assert r.returncode == 3
+
+
 def test_mismatched_world_size_is_refused():
     r = _run(["--gpus", "8", "--selftest"], {"WORLD_SIZE": "1", "RANK": "0"})
     assert r.returncode == 2

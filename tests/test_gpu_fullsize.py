@@ -11,6 +11,8 @@ config 4: one 8 GiB object of 64 KiB frames, and a 2 GiB object of the reference
           frames (what flush_batch writes, disk_cache.rs:1820-1870), through the range reader
           (stream_range_data, disk_cache.rs:3850-3935) in 256 KiB batches on 3 queues, 4 MiB
           file reads, 1 MiB chunks out; output equal to the input, total checked.
+config 5: one GPU's 131,072-block slice of the 1 M x 64 KiB batch (8 GiB), encode + decode,
+          every byte checked, a spread sample of frames through the oracle.
 """
 import numpy as np
 import pytest
@@ -130,3 +132,33 @@ def test_config4_object_through_reader_256k_batches(engine, item, size):
     if item == MiB:
         assert frames[4:7] == b"\x64\x70\xb9"  # BD 0x70: lz4_flex Auto for a 1 MiB batch
     _reader_roundtrip(engine, frames, data, 256 << 10)
+
+
+@pytest.mark.timeout(900)
+def test_config5_per_gpu_slice_131072_blocks(engine, oracle):
+    # config 5 (1 M x 64 KiB over 8 GPUs, no RCCL) gives each GPU a contiguous 131,072-block
+    # slice (8 GiB); this is one GPU's slice at full size: encode + decode in one batch each,
+    # every status and length checked, every decoded byte compared chunk by chunk, and a spread
+    # sample of frames decoded by the oracle (decompress_data, compression.rs:463-502).
+    n = 131072
+    chunk_blocks = 4096  # 256 MiB of distinct log text per chunk, regenerated for the checks
+    seeds = [synth.SEED_BASE + 5 + 7919 * c for c in range(n // chunk_blocks)]
+    d_src = engine.alloc(n * BLOCK)
+    for c, sd in enumerate(seeds):
+        d_src.write(synth.log_text(chunk_blocks * BLOCK, sd), c * chunk_blocks * BLOCK)
+    dst, fo, fl = _encode_items(engine, d_src, n, BLOCK)
+    del d_src
+    assert (fo[-1] + fl[-1]) / (n * BLOCK) < 0.45
+    out = _decode_all(engine, dst, fo, fl, n, BLOCK)
+    sample = set(list(range(0, n, 997)) + [n - 1])
+    for c, sd in enumerate(seeds):
+        want = synth.log_text(chunk_blocks * BLOCK, sd)
+        got = out.read(chunk_blocks * BLOCK, c * chunk_blocks * BLOCK)
+        assert got == want, f"decoded bytes differ in chunk {c}"
+        mv = memoryview(want)
+        for i in range(c * chunk_blocks, (c + 1) * chunk_blocks):
+            if i in sample:
+                k = i - c * chunk_blocks
+                f = dst.read(fl[i], fo[i])
+                assert f[:7] == b"\x04\x22\x4d\x18\x64\x40\xa7"
+                assert oracle.decompress_data(f) == mv[k * BLOCK:(k + 1) * BLOCK], f"frame {i}"

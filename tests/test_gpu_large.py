@@ -345,3 +345,29 @@ def test_lb_spread_and_step_in_one_launch_randomized(engine, oracle):
         want = b"".join(parts)
         assert engine.decompress_frames(blob) == want, case
         assert _step_path(lambda: engine.decompress_frames(blob)) == want, case
+
+
+# Host-buffer calls read back each frame's slot prefix, min(slot, max(4 x compressed, 1 MiB)),
+# in their first round trip: output past a frame's prefix must take the second trip.
+def test_hostcall_single_frame_past_its_prefix(engine, oracle):
+    # one BD 0x70 frame (4 MiB slot) of very compressible data: ~2.5 MiB decoded from a frame far
+    # below 1/4 of that, so the decoded bytes run past the early prefix
+    data = (b"abcdefgh" * 7 + b"\n") * (2_500_000 // 57)
+    frame = engine.compress_frame(data)
+    assert frame[5] == 0x70 and len(frame) * 4 < len(data) - (1 << 20)
+    assert engine.decompress_frames(frame) == data
+    assert engine.decompress_frames(oracle.lz4flex_compress_frame(data)) == data
+
+
+@pytest.mark.parametrize("nframes", [2, 3, 4])
+def test_hostcall_reference_multi_frame_files(engine, oracle, nframes):
+    # a reference cache file: ~1 MiB frames (BD 0x70, 4 MiB slots) written back to back
+    parts = [synth.log_text(MiB - 1000 * k, 40 + k) for k in range(nframes)]
+    blob = b"".join(oracle.lz4flex_compress_frame(p) for p in parts)
+    want = b"".join(parts)
+    assert oracle.decompress_data(blob) == want
+    assert engine.decompress_frames(blob) == want
+    # a compressible frame after a text frame: the second one decodes past its own prefix
+    big = bytes(3 * MiB)
+    blob2 = oracle.lz4flex_compress_frame(parts[0]) + oracle.lz4flex_compress_frame(big)
+    assert engine.decompress_frames(blob2) == parts[0] + big
