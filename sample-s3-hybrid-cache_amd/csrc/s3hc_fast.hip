@@ -375,7 +375,9 @@ constexpr uint32_t kORW = kOR / 4;
 constexpr uint32_t kORM = kOR - 1;
 constexpr uint32_t kWin = 2048;      // output bytes of one batch, at most
 constexpr uint32_t kFl = 1024;       // flush granule
-constexpr uint32_t kQ = 512;         // token queue entries (>= 4 windows + one 16-word refill)
+constexpr uint32_t kQ = 256;         // token queue entries (window w+3 plus one 16-word refill)
+constexpr uint32_t kGD = 4;          // pending-match dwords per lane held in registers
+constexpr uint32_t kGW = 64 * kGD;
 static_assert(2 * kWin + kFl <= kOR, "far sources of a batch must be flushed before it runs");
 }  // namespace fst
 
@@ -494,15 +496,69 @@ __device__ __forceinline__ uint32_t match_len(const uint8_t* in, uint32_t mp, ui
     }
     return M;
 }
-__device__ __forceinline__ uint32_t incl_scan(uint32_t x, uint32_t lane) {
+// DPP lane moves (row_shr / row_bcast; lanes without a source read 0) and wave-wide inclusive
+// scans on them (no LDS round trip)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t fdpp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, 0xF, false);
+}
+__device__ __forceinline__ uint32_t incl_scan(uint32_t x, uint32_t) {
+    x += fdpp<0x111, 0xF>(x);
+    x += fdpp<0x112, 0xF>(x);
+    x += fdpp<0x114, 0xF>(x);
+    x += fdpp<0x118, 0xF>(x);
+    x += fdpp<0x142, 0xA>(x);
+    x += fdpp<0x143, 0xC>(x);
+    return x;
+}
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// v shifted down by sh bytes (0..15), zeros shifted in
+__device__ __forceinline__ uint4 shr16(uint4 v, uint32_t sh) {
+    uint32_t w[8] = {v.x, v.y, v.z, v.w, 0u, 0u, 0u, 0u};
+    const uint32_t k = sh >> 2, r = sh & 3u;
+    uint32_t o[4];
 #pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-        if (lane >= d) x += y;
+    for (uint32_t i = 0; i < 4; ++i) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+            lo = k == t ? w[i + t] : lo;
+            hi = k == t ? w[i + t + 1] : hi;
+        }
+        o[i] = __builtin_amdgcn_alignbyte(hi, lo, r);
     }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+__device__ __forceinline__ uint32_t incl_max(uint32_t x) {
+    x = umax_(x, fdpp<0x111, 0xF>(x));
+    x = umax_(x, fdpp<0x112, 0xF>(x));
+    x = umax_(x, fdpp<0x114, 0xF>(x));
+    x = umax_(x, fdpp<0x118, 0xF>(x));
+    x = umax_(x, fdpp<0x142, 0xA>(x));
+    x = umax_(x, fdpp<0x143, 0xC>(x));
     return x;
 }
 }  // namespace
+
+// One output dword (ring dword index d, bytes of mask m) of an overlapping match (P = md, ms,
+// ml | off << 16): byte b copies the byte ((b - md) mod off) into the match's first period.
+__device__ uint32_t periodic_dword(const uint32_t* ring, uint4 P, uint32_t d, uint32_t m) {
+    const uint32_t md = P.x, ms = P.y, off = P.z >> 16;
+    const uint8_t* rb = (const uint8_t*)ring;
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        if ((m >> (8u * j)) & 0xFFu) {
+            const uint32_t e = 4u * d + j - md;
+            v |= (uint32_t)rb[(ms + e % off) & fst::kORM] << (8u * j);
+        }
+    }
+    return v;
+}
 
 __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                               const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
@@ -511,8 +567,8 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
     using namespace fst;
     __shared__ __attribute__((aligned(16))) uint32_t ring[kORW];
     __shared__ uint16_t tq[kQ];              // token positions, queue entry t = token t
-    __shared__ uint32_t gmap[kWin / 16];     // per 16-byte granule of a window: lane owning its first byte
-    __shared__ uint16_t sdst[64];            // per lane: first output byte (window-relative)
+    __shared__ uint4 pinfo[64];              // pending matches: md, ms, ml | off << 16, first dword - rank
+    __shared__ uint8_t gmk[kGW];             // pending dwords: rank of each lane's first dword -> lane + 1
     const uint32_t u = blockIdx.x;
     if (u >= nunits || !a.unit_fast[u]) return;
     const uint32_t lane = threadIdx.x;
@@ -559,16 +615,23 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
         const uint32_t t = 64u * w + lane;
         return t < N ? (uint32_t)tq[t & (kQ - 1)] : C;
     };
-    auto ld_w0 = [&](uint32_t pos) -> uint32_t { return pos < C ? gld4(in + pos) : 0u; };
+    auto ld_w0 = [&](uint32_t pos) -> uint32_t { return gld4(in + umin_(pos, C)); };
     // ---- pipeline prologue: window 2's token dword, window 1's offset dword, window 0 decoded
-    refill(64u * 4u);
-    uint32_t w0_c = ld_w0(tpos(0));
-    uint32_t w0_n = ld_w0(tpos(1));
+    // (the queue holds one window plus one refill: windows 0..2 are read as they arrive)
+    refill(64u);
+    const uint32_t pos_0 = tpos(0);
+    uint32_t w0_c = ld_w0(pos_0);
+    refill(128u);
+    uint32_t pos_n = tpos(1);
+    uint32_t w0_n = ld_w0(pos_n);
+    refill(192u);
+    uint32_t pos_2 = tpos(2);
+    uint32_t w0_2 = ld_w0(pos_2);
     // window 0: token + offset dwords now
     SeqF fc, fn;
-    uint32_t pos_n = tpos(1), mp_n = 0, w1_n = 0;
+    uint32_t mp_n = 0, w1_n = 0;
     {
-        const uint32_t pos = tpos(0);
+        const uint32_t pos = pos_0;
         fc.ll = pos < C ? lit_len(in, pos, w0_c, fc.lit) : 0u;
         const uint32_t mp = fc.lit + fc.ll;
         fc.off = fc.ml = 0;
@@ -577,23 +640,27 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
             fc.off = w1 & 0xFFFFu;
             fc.ml = match_len(in, mp, w0_c & 0xFFu, w1);
         }
+        mp_n = C;
         if (pos_n < C) {
             uint32_t lit;
             const uint32_t ll = lit_len(in, pos_n, w0_n, lit);
-            mp_n = lit + ll;
-            w1_n = mp_n < C ? gld4(in + mp_n) : 0u;
+            mp_n = umin_(lit + ll, C);
         }
+        w1_n = gld4(in + mp_n);
     }
-    uint32_t pos_2 = tpos(2);
-    uint32_t w0_2 = ld_w0(pos_2);
+
     uint32_t Sincl_c = incl_scan(fc.ll + fc.ml, lane);
     uint32_t S_c = (uint32_t)__shfl((int)Sincl_c, 63, 64);
-    bool far_c = false, pf_c = false;  // window 0: nothing is far
-    uint4 lit0_c = make_uint4(0, 0, 0, 0), lit1_c = lit0_c, far0_c = lit0_c, far1_c = lit0_c;
-    if (S_c <= kWin) {
-        if (fc.ll) lit0_c = gld16_blk(in, fc.lit, C);
-        if (fc.ll > 16u) lit1_c = gld16_blk(in, fc.lit + 16u, C);
-        pf_c = true;
+    bool far_c = false, pf_c = S_c <= kWin;  // window 0: nothing is far
+    uint4 lit0_c, lit1_c, far0_c = make_uint4(0, 0, 0, 0), far1_c = far0_c;
+    uint32_t lsh_c;
+    {
+        const int32_t lim = (int32_t)C + 4 - 16;
+        const uint32_t lit = fc.ll ? fc.lit : C;
+        const int32_t q0 = min((int32_t)lit, max(lim, -11)), q1 = min((int32_t)lit + 16, max(lim, -11));
+        lit0_c = gld16(in + q0);
+        lit1_c = gld16(in + q1);
+        lsh_c = (lit - (uint32_t)q0) | ((lit + 16u - (uint32_t)q1) << 8);
     }
     const uint64_t te0 = FP_NOW();
     uint64_t tsum[6] = {0, 0, 0, 0, 0, 0};
@@ -602,20 +669,23 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
         uint64_t tq0 = FP_NOW();
         const uint32_t nact = umin_(64u, N - 64u * w);
         const bool act = lane < nact;
-        // ---- stage A: window w+3's token dword
+        // ---- stage A: window w+3's token dword (loads are unconditional: a lane without a
+        // token reads a harmless in-frame address, so no branch forces an early wait)
         refill(64u * (w + 4u));
         const uint32_t pos_3 = w + 3 < nwin ? tpos(w + 3) : C;
-        const uint32_t w0_3 = ld_w0(pos_3);
+        const uint32_t w0_3 = gld4(in + pos_3);
         // ---- stage B: window w+2's offset dword
-        uint32_t mp_2 = 0, w1_2 = 0;
-        if (pos_2 < C) {
+        uint32_t mp_2;
+        {
             uint32_t lit;
-            const uint32_t ll = lit_len(in, pos_2, w0_2, lit);
-            mp_2 = lit + ll;
-            w1_2 = mp_2 < C ? gld4(in + mp_2) : 0u;
+            const uint32_t ll = pos_2 < C ? lit_len(in, pos_2, w0_2, lit) : 0u;
+            mp_2 = pos_2 < C ? umin_(lit + ll, C) : C;
         }
+        const uint32_t w1_2 = gld4(in + mp_2);
         // ---- stage C: decode window w+1, prefetch its literals and far match sources
-        fn.ll = fn.lit = fn.off = fn.ml = 0;
+        fn.ll = 0;
+        fn.lit = C;
+        fn.off = fn.ml = 0;
         if (pos_n < C) {
             fn.ll = lit_len(in, pos_n, w0_n, fn.lit);
             if (mp_n < C) {
@@ -626,21 +696,21 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
         const uint32_t Sincl_n = incl_scan(fn.ll + fn.ml, lane);
         const uint32_t S_n = (uint32_t)__shfl((int)Sincl_n, 63, 64);
         const bool pf_n = S_c <= kWin && S_n <= kWin;
-        uint4 lit0_n = make_uint4(0, 0, 0, 0), lit1_n = lit0_n, far0_n = lit0_n, far1_n = lit0_n;
+        // literal chunks at clamped in-frame addresses (a frame holds >= 11 bytes before a block's
+        // payload and >= 4 after it); the shift back to the literal start is applied at use
+        const int32_t lim = (int32_t)C + 4 - 16;
+        const int32_t q0 = min((int32_t)fn.lit, max(lim, -11)), q1 = min((int32_t)fn.lit + 16, max(lim, -11));
+        const uint4 lit0_n = gld16(in + q0), lit1_n = gld16(in + q1);
+        const uint32_t lsh_n = (fn.lit - (uint32_t)q0) | ((fn.lit + 16u - (uint32_t)q1) << 8);
         bool far_n = false;
-        if (S_n <= kWin) {
-            if (fn.ll) lit0_n = gld16_blk(in, fn.lit, C);
-            if (fn.ll > 16u) lit1_n = gld16_blk(in, fn.lit + 16u, C);
-        }
+        const uint8_t* fa0 = in - 11;
         if (pf_n && fn.ml) {
             const uint32_t upos_n = upos + S_c;
             const uint32_t md = upos_n + Sincl_n - fn.ml, ms = md - fn.off;
             far_n = ms + kOR < upos_n + S_n && ms < md;
-            if (far_n) {
-                far0_n = gld16(out + ms);
-                if (fn.ml > 16u) far1_n = gld16(out + ms + 16u);
-            }
+            if (far_n) fa0 = out + ms;
         }
+        const uint4 far0_n = gld16(fa0), far1_n = gld16(far_n ? fa0 + 16 : fa0);
 #ifdef FPROF
         { const uint64_t tn = FP_NOW(); tsum[0] += tn - tq0; tq0 = tn; }
 #endif
@@ -649,7 +719,12 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
         const uint32_t len = ll + ml;
         if (pf_c && S_c <= kWin) {
             const uint32_t d0 = upos + Sincl_c - len;
-            // literals (first 32 bytes prefetched)
+            // literals (first 32 bytes prefetched; near the block's end they were loaded from a
+            // clamped address: shift them back)
+            if (__ballot(act && ll && (lsh_c & 0xFFFFu))) {
+                if (lsh_c & 0xFFu) lit0_c = shr16(lit0_c, lsh_c & 0xFFu);
+                if (lsh_c & 0xFF00u) lit1_c = shr16(lit1_c, (lsh_c >> 8) & 0xFFu);
+            }
             if (act && ll) rst(ring, d0, lit0_c, umin_(16u, ll));
             if (act && ll > 16u) rst(ring, d0 + 16u, lit1_c, umin_(16u, ll - 16u));
             for (uint32_t c = 32; __ballot(act && c < ll); c += 16u)
@@ -662,74 +737,98 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
             const bool hasm = act && ml > 0;
             const bool far = hasm && far_c;
             bool pend = hasm && !far && ms + ml > upos;
-            const uint32_t step = off < 16u ? off : 16u;
-            // round 0: far sources (prefetched) and sources before the window
+            // round 0: far sources (prefetched) and sources before the window (an overlapping
+            // match is always pending: its source reaches its own output)
             if (hasm && !pend) {
                 if (far) {
                     rst(ring, md, far0_c, umin_(16u, ml));
                     if (ml > 16u) rst(ring, md + 16u, far1_c, umin_(16u, ml - 16u));
                 }
             }
-            for (uint32_t c = far ? 32u : 0u; __ballot(hasm && !pend && c < ml); c += far ? 16u : step) {
+            for (uint32_t c = far ? 32u : 0u; __ballot(hasm && !pend && c < ml); c += 16u) {
                 if (hasm && !pend && c < ml) {
                     uint4 v;
                     if (far) v = gld16(out + ms + c);
                     else v = rld16(ring, ms + c);
-                    rst(ring, md + c, v, umin_(far ? 16u : step, ml - c));
+                    rst(ring, md + c, v, umin_(16u, ml - c));
                 }
             }
 #ifdef FPROF
             __builtin_amdgcn_s_waitcnt(0);
             { const uint64_t tn = FP_NOW(); tsum[2] += tn - tq0; tq0 = tn; }
 #endif
-            // in-window sources: wait for exactly the lanes whose output the source overlaps
-            uint64_t notdone = __ballot(pend);
-            if (notdone) {
-                const uint32_t ex = Sincl_c - len;
-                sdst[lane] = (uint16_t)(act ? ex : 0xFFFFu);
-                if (lane < kWin / 32) ((uint2*)gmap)[lane] = make_uint2(0u, 0u);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const uint32_t g0 = (ex + 15u) >> 4;
-                if (act && len && g0 < kWin / 16 && ex + len > (g0 << 4)) atomicMax(&gmap[g0], lane);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                {
-                    const uint2 pr = lane < kWin / 32 ? ((const uint2*)gmap)[lane] : make_uint2(0u, 0u);
-                    const uint32_t b = umax_(pr.x, pr.y);
-                    uint32_t x = b;  // inclusive max-scan over lanes
+            // in-window sources: every output dword of a pending match is given to one lane
+            // (packed over the lanes), and each such dword is re-gathered from its sources until a
+            // whole sweep changes nothing: at that fixed point every byte equals its source, whose
+            // chain ends in a final byte, so every byte is final (sweeps ~ chain depth + 1)
+            if (__ballot(pend)) {
+                const uint32_t df = md >> 2, cnt = pend ? ((md + ml - 1u) >> 2) - df + 1u : 0u;
+                const uint32_t cincl = incl_scan(cnt, lane);
+                const uint32_t T = (uint32_t)__shfl((int)cincl, 63, 64);
+                if (T <= 64u * kGD) {
+                    pinfo[lane] = make_uint4(md, ms, ml | (off << 16), df - (cincl - cnt));
+                    ((uint32_t*)gmk)[lane] = 0u;  // kGW = 256 mark bytes
+                    wsync();
+                    if (cnt) gmk[cincl - cnt] = (uint8_t)(lane + 1u);
+                    wsync();
+                    uint32_t gd[kGD], gm[kGD], ga[kGD], go[kGD];
+                    uint32_t carry = 0;
 #pragma unroll
-                    for (uint32_t d = 1; d < 64; d <<= 1) {
-                        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-                        if (lane >= d) x = umax_(x, y);
+                    for (uint32_t i = 0; i < kGD; ++i) {
+                        const uint32_t j = lane + 64u * i;
+                        const uint32_t own = umax_(incl_max(j < T ? (uint32_t)gmk[j] : 0u), carry);
+                        carry = (uint32_t)__shfl((int)own, 63, 64);
+                        gd[i] = 0xFFFFFFFFu;
+                        gm[i] = ga[i] = go[i] = 0;
+                        if (j < T && own) {
+                            const uint4 P = pinfo[own - 1u];
+                            const uint32_t d = P.w + j, b0 = d << 2, pmd = P.x, pml = P.z & 0xFFFFu;
+                            const uint32_t lo = pmd > b0 ? pmd - b0 : 0u, hi = umin_(4u, pmd + pml - b0);
+                            gd[i] = d;
+                            gm[i] = (hi >= 4u ? ~0u : (1u << (8u * hi)) - 1u) & (~0u << (8u * lo));
+                            ga[i] = P.y + b0 - pmd;  // source of the dword's byte 0 (non-overlapping)
+                            go[i] = (P.z >> 16) < pml ? own : 0u;  // overlapping: periodic sources
+                        }
                     }
-                    const uint32_t P = x == b ? (uint32_t)__shfl_up((int)x, 1, 64) : x;  // exclusive max
-                    const uint32_t Pex = lane ? umax_(P, 0u) : 0u;
-                    if (lane < kWin / 32) ((uint2*)gmap)[lane] = make_uint2(umax_(Pex, pr.x), umax_(Pex, b));
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                uint64_t dep = 0;
-                if (pend) {
-                    auto owner = [&](uint32_t xr) -> uint32_t {
-                        uint32_t k = gmap[xr >> 4];
-                        while (k + 1u < nact && sdst[k + 1u] <= xr) ++k;
-                        return k;
-                    };
-                    const uint32_t lo = owner((ms > upos ? ms : upos) - upos), hi = owner(ms + ml - 1u - upos);
-                    dep = (hi >= 63u ? ~0ull : ((2ull << hi) - 1ull)) & ~((1ull << lo) - 1ull) & ~(1ull << lane);
-                }
-                for (;;) {
-                    ++nrounds;
-                    const bool run = pend && (dep & notdone) == 0;
-                    for (uint32_t c = 0; __ballot(run && c < ml); c += step)
-                        if (run && c < ml) rst(ring, md + c, rld16(ring, ms + c), umin_(step, ml - c));
-                    notdone &= ~__ballot(run);
-                    pend = pend && !run;
-                    if (!notdone) break;
+                    uint32_t sweeps = 0;
+                    for (;;) {
+                        bool chg = false;
+#pragma unroll
+                        for (uint32_t i = 0; i < kGD; ++i) {
+                            if (gd[i] == 0xFFFFFFFFu) continue;
+                            uint32_t* rd = ring + (gd[i] & (kORW - 1));
+                            const uint32_t cur = *rd;
+                            uint32_t v;
+                            if (!go[i]) {
+                                const uint32_t A = ga[i];
+                                v = __builtin_amdgcn_alignbyte(ring[((A >> 2) + 1u) & (kORW - 1)],
+                                                               ring[(A >> 2) & (kORW - 1)], A & 3u);
+                            } else {
+                                v = periodic_dword(ring, pinfo[go[i] - 1u], gd[i], gm[i]);
+                            }
+                            if (((cur ^ v) & gm[i]) != 0u) {
+                                chg = true;
+                                mskor(rd, gm[i], v);
+                            }
+                        }
+                        ++nrounds;
+                        if (!__ballot(chg) || ++sweeps > 8192u) break;  // (a bound, never reached)
+                    }
+                } else {
+                    // (more pending output than the registers hold: multi-round resolution, the
+                    // lowest pending lane and every pending lane whose source ends before it)
+                    for (;;) {
+                        const uint64_t pm = __ballot(pend);
+                        if (!pm) break;
+                        const uint32_t first = (uint32_t)__builtin_ctzll(pm);
+                        const uint32_t h = (uint32_t)__shfl((int)md, (int)first, 64);
+                        const bool run = pend && (lane == first || (off >= ml && ms + ml <= h));
+                        const uint32_t step = off < 16u ? off : 16u;
+                        for (uint32_t c = 0; __ballot(run && c < ml); c += step)
+                            if (run && c < ml) rst(ring, md + c, rld16(ring, ms + c), umin_(step, ml - c));
+                        pend = pend && !run;
+                        ++nrounds;
+                    }
                 }
             }
 #ifdef FPROF
@@ -824,6 +923,7 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
         far_c = far_n;
         lit0_c = lit0_n;
         lit1_c = lit1_n;
+        lsh_c = lsh_n;
         far0_c = far0_n;
         far1_c = far1_n;
         pos_n = pos_2;
