@@ -369,6 +369,12 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
 //   flush      whole 1 KiB pieces of the ring to HBM.
 // A sequence longer than kWin runs alone, wave-wide, in 1 KiB pieces (overlapping matches by
 // growing multiples of their period).
+#ifndef S3HC_FXOR  // 1: a window's output range is cleared, then or-written (0: masked writes)
+#define S3HC_FXOR 0
+#endif
+#ifndef S3HC_FXSKIP  // diagnostic builds: phases of k_dexec left out (timing only; output wrong)
+#define S3HC_FXSKIP 0
+#endif
 namespace fst {
 constexpr uint32_t kOR = 8192;       // output ring (bytes)
 constexpr uint32_t kORW = kOR / 4;
@@ -438,6 +444,73 @@ __device__ __forceinline__ void rst(uint32_t* ring, uint32_t y, uint4 v, uint32_
     if (m2) mskor(ring + ((db + 2) & (fst::kORW - 1)), m2, o2);
     if (m3) mskor(ring + ((db + 3) & (fst::kORW - 1)), m3, o3);
     if (m4) mskor(ring + ((db + 4) & (fst::kORW - 1)), m4, o4);
+}
+
+// the same into ring bytes known to be zero (the window's output range is cleared before it
+// runs): plain or-writes, no per-dword masks. v's bytes at and after n are dropped first; the
+// five output dwords come from byte permutes of neighbouring source dwords.
+__device__ __forceinline__ uint32_t keep_below(int x) {  // bytes below x (clamped to 0..4)
+    const uint32_t c = (uint32_t)min(max(x, 0), 4);
+    return ~(uint32_t)(0xFFFFFFFFull << (8u * c));
+}
+__device__ __forceinline__ void ds_or(uint32_t* lds_dw, uint32_t data) {
+    __hip_atomic_fetch_or(lds_dw, data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+__device__ __forceinline__ void rst_or(uint32_t* ring, uint32_t y, uint4 v, uint32_t n) {
+    const int ni = (int)n;
+    v.x &= keep_below(ni);
+    v.y &= keep_below(ni - 4);
+    v.z &= keep_below(ni - 8);
+    v.w &= keep_below(ni - 12);
+    const uint32_t a = y & 3u, db = (y & fst::kORM) >> 2;
+    // output byte j of dword i = source byte 4i + j - a: selector byte (j + 4 - a) picks from
+    // {hi = v_i, lo = v_(i-1)}
+    const uint32_t sel = 0x03020100u + (4u - a) * 0x01010101u;
+    const uint32_t o0 = __builtin_amdgcn_perm(v.x, 0u, sel), o1 = __builtin_amdgcn_perm(v.y, v.x, sel);
+    const uint32_t o2 = __builtin_amdgcn_perm(v.z, v.y, sel), o3 = __builtin_amdgcn_perm(v.w, v.z, sel);
+    const uint32_t o4 = __builtin_amdgcn_perm(0u, v.w, sel);
+    if (db + 4u < fst::kORW) {
+        ds_or(ring + db, o0);
+        ds_or(ring + db + 1, o1);
+        ds_or(ring + db + 2, o2);
+        ds_or(ring + db + 3, o3);
+        if (o4) ds_or(ring + db + 4, o4);
+    } else {
+        ds_or(ring + db, o0);
+        ds_or(ring + ((db + 1) & (fst::kORW - 1)), o1);
+        ds_or(ring + ((db + 2) & (fst::kORW - 1)), o2);
+        ds_or(ring + ((db + 3) & (fst::kORW - 1)), o3);
+        if (o4) ds_or(ring + ((db + 4) & (fst::kORW - 1)), o4);
+    }
+}
+
+// ring [from, from + n) -> 0 (wave-wide; n <= kOR): aligned 16-byte pieces plus masked edges
+__device__ __forceinline__ void ring_clear(uint32_t* ring, uint32_t from, uint32_t n, uint32_t lane) {
+    if (n == 0) return;
+    const uint32_t to = from + n;
+    const uint32_t a16 = (from + 15u) & ~15u, b16 = to & ~15u;
+    if (a16 < b16) {
+        for (uint32_t q = a16 + 16u * lane; q < b16; q += 1024u)
+            *(uint4*)((uint8_t*)ring + (q & fst::kORM)) = make_uint4(0, 0, 0, 0);
+    }
+    // edges: the dwords of [from, min(a16, to)) and [max(b16, a16), to), lanes 0..3 and 4..7
+    const uint32_t e0 = umin_(a16, to), s1 = umax_(b16, e0);
+    const uint32_t d = lane < 4u ? (from & ~3u) + 4u * lane : s1 + 4u * (lane - 4u);
+    const uint32_t lo = lane < 4u ? umax_(d, from) : d, hi = umin_(d + 4u, lane < 4u ? e0 : to);
+    if (lane < 8u && lo < hi) {
+        const uint32_t m = (0xFFFFFFFFu << (8u * (lo - d))) & keep_below((int)(hi - d));
+        uint32_t* p = ring + ((d & fst::kORM) >> 2);
+        if (m == 0xFFFFFFFFu) *p = 0u;
+        else mskor(p, m, 0u);
+    }
+}
+
+__device__ __forceinline__ void wr16(uint32_t* ring, uint32_t y, uint4 v, uint32_t n) {
+#if S3HC_FXOR
+    rst_or(ring, y, v, n);
+#else
+    rst(ring, y, v, n);
+#endif
 }
 
 // ring [from, from + n) -> out + from, n <= kFl, the range contiguous in the ring
@@ -544,6 +617,11 @@ __device__ __forceinline__ uint32_t incl_max(uint32_t x) {
 }
 }  // namespace
 
+// lane l's value of x (l wave-uniform): v_readlane, no LDS round trip (unlike __shfl's ds_bpermute)
+__device__ __forceinline__ uint32_t rdlane(uint32_t x, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
+}
+
 // One output dword (ring dword index d, bytes of mask m) of an overlapping match (P = md, ms,
 // ml | off << 16): byte b copies the byte ((b - md) mod off) into the match's first period.
 __device__ uint32_t periodic_dword(const uint32_t* ring, uint4 P, uint32_t d, uint32_t m) {
@@ -582,7 +660,7 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
     uint32_t upos = 0, flushed = 0;
     auto flush_full = [&]() {
         while (upos - flushed >= kFl) {
-            flush_piece(ring, out, flushed, kFl, lane);
+            if (!(S3HC_FXSKIP & 16)) flush_piece(ring, out, flushed, kFl, lane);
             flushed += kFl;
         }
     };
@@ -604,7 +682,7 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
                 ++k;
                 wv &= wv - 1u;
             }
-            qfill += (uint32_t)__shfl((int)incl, 15, 64);
+            qfill += rdlane(incl, 15);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -650,7 +728,7 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
     }
 
     uint32_t Sincl_c = incl_scan(fc.ll + fc.ml, lane);
-    uint32_t S_c = (uint32_t)__shfl((int)Sincl_c, 63, 64);
+    uint32_t S_c = rdlane(Sincl_c, 63);
     bool far_c = false, pf_c = S_c <= kWin;  // window 0: nothing is far
     uint4 lit0_c, lit1_c, far0_c = make_uint4(0, 0, 0, 0), far1_c = far0_c;
     uint32_t lsh_c;
@@ -694,7 +772,7 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
             }
         }
         const uint32_t Sincl_n = incl_scan(fn.ll + fn.ml, lane);
-        const uint32_t S_n = (uint32_t)__shfl((int)Sincl_n, 63, 64);
+        const uint32_t S_n = rdlane(Sincl_n, 63);
         const bool pf_n = S_c <= kWin && S_n <= kWin;
         // literal chunks at clamped in-frame addresses (a frame holds >= 11 bytes before a block's
         // payload and >= 4 after it); the shift back to the literal start is applied at use
@@ -725,10 +803,12 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
                 if (lsh_c & 0xFFu) lit0_c = shr16(lit0_c, lsh_c & 0xFFu);
                 if (lsh_c & 0xFF00u) lit1_c = shr16(lit1_c, (lsh_c >> 8) & 0xFFu);
             }
-            if (act && ll) rst(ring, d0, lit0_c, umin_(16u, ll));
-            if (act && ll > 16u) rst(ring, d0 + 16u, lit1_c, umin_(16u, ll - 16u));
+            if (S3HC_FXOR && !(S3HC_FXSKIP & 8)) ring_clear(ring, upos, S_c, lane);
+            wsync();
+            if (!(S3HC_FXSKIP & 2) && act && ll) wr16(ring, d0, lit0_c, umin_(16u, ll));
+            if (!(S3HC_FXSKIP & 2) && act && ll > 16u) wr16(ring, d0 + 16u, lit1_c, umin_(16u, ll - 16u));
             for (uint32_t c = 32; __ballot(act && c < ll); c += 16u)
-                if (act && c < ll) rst(ring, d0 + c, gld16_blk(in, lit + c, C), umin_(16u, ll - c));
+                if (act && c < ll) wr16(ring, d0 + c, gld16_blk(in, lit + c, C), umin_(16u, ll - c));
 #ifdef FPROF
             __builtin_amdgcn_s_waitcnt(0);
             { const uint64_t tn = FP_NOW(); tsum[1] += tn - tq0; tq0 = tn; }
@@ -739,18 +819,42 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
             bool pend = hasm && !far && ms + ml > upos;
             // round 0: far sources (prefetched) and sources before the window (an overlapping
             // match is always pending: its source reaches its own output)
-            if (hasm && !pend) {
+            if (!(S3HC_FXSKIP & 4) && hasm && !pend) {
                 if (far) {
-                    rst(ring, md, far0_c, umin_(16u, ml));
-                    if (ml > 16u) rst(ring, md + 16u, far1_c, umin_(16u, ml - 16u));
+                    wr16(ring, md, far0_c, umin_(16u, ml));
+                    if (ml > 16u) wr16(ring, md + 16u, far1_c, umin_(16u, ml - 16u));
                 }
             }
-            for (uint32_t c = far ? 32u : 0u; __ballot(hasm && !pend && c < ml); c += 16u) {
-                if (hasm && !pend && c < ml) {
-                    uint4 v;
-                    if (far) v = gld16(out + ms + c);
-                    else v = rld16(ring, ms + c);
-                    rst(ring, md + c, v, umin_(16u, ml - c));
+            // the rest of round 0 load-balanced over the lanes: every 16-byte chunk of every such
+            // match (a far match's first 32 bytes came prefetched) is one work item, items are
+            // dealt out 64 at a time (the owner of item j: start marks + max-scan); a window's
+            // <= kWin bytes make <= 192 items
+            {
+                const uint32_t c0 = far ? 32u : 0u;
+                const uint32_t nch = !(S3HC_FXSKIP & 4) && hasm && !pend && ml > c0 ? (ml - c0 + 15u) >> 4 : 0u;
+                const uint32_t chincl = incl_scan(nch, lane);
+                const uint32_t T0 = rdlane(chincl, 63);
+                if (T0) {
+                    pinfo[lane] = make_uint4(md + c0, ms + c0, (ml - c0) | (far ? 0x10000u : 0u), chincl - nch);
+                    ((uint32_t*)gmk)[lane] = 0u;
+                    wsync();
+                    if (nch) gmk[chincl - nch] = (uint8_t)(lane + 1u);
+                    wsync();
+                    uint32_t carry = 0;
+                    for (uint32_t j0 = 0; j0 < T0; j0 += 64u) {
+                        const uint32_t j = j0 + lane;
+                        const uint32_t own = umax_(incl_max(j < T0 ? (uint32_t)gmk[j] : 0u), carry);
+                        carry = rdlane(own, 63);
+                        if (j < T0) {
+                            const uint4 P = pinfo[own - 1u];
+                            const uint32_t c = 16u * (j - P.w), rem = P.z & 0xFFFFu;
+                            uint4 v;
+                            if (P.z >> 16) v = gld16(out + P.y + c);
+                            else v = rld16(ring, P.y + c);
+                            wr16(ring, P.x + c, v, umin_(16u, rem - c));
+                        }
+                    }
+                    wsync();
                 }
             }
 #ifdef FPROF
@@ -761,10 +865,10 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
             // (packed over the lanes), and each such dword is re-gathered from its sources until a
             // whole sweep changes nothing: at that fixed point every byte equals its source, whose
             // chain ends in a final byte, so every byte is final (sweeps ~ chain depth + 1)
-            if (__ballot(pend)) {
+            if (!(S3HC_FXSKIP & 1) && __ballot(pend)) {
                 const uint32_t df = md >> 2, cnt = pend ? ((md + ml - 1u) >> 2) - df + 1u : 0u;
                 const uint32_t cincl = incl_scan(cnt, lane);
-                const uint32_t T = (uint32_t)__shfl((int)cincl, 63, 64);
+                const uint32_t T = rdlane(cincl, 63);
                 if (T <= 64u * kGD) {
                     pinfo[lane] = make_uint4(md, ms, ml | (off << 16), df - (cincl - cnt));
                     ((uint32_t*)gmk)[lane] = 0u;  // kGW = 256 mark bytes
@@ -775,9 +879,10 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
                     uint32_t carry = 0;
 #pragma unroll
                     for (uint32_t i = 0; i < kGD; ++i) {
+                        if (64u * i >= T) break;
                         const uint32_t j = lane + 64u * i;
                         const uint32_t own = umax_(incl_max(j < T ? (uint32_t)gmk[j] : 0u), carry);
-                        carry = (uint32_t)__shfl((int)own, 63, 64);
+                        carry = rdlane(own, 63);
                         gd[i] = 0xFFFFFFFFu;
                         gm[i] = ga[i] = go[i] = 0;
                         if (j < T && own) {
@@ -790,12 +895,16 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
                             go[i] = (P.z >> 16) < pml ? own : 0u;  // overlapping: periodic sources
                         }
                     }
-                    uint32_t sweeps = 0;
-                    for (;;) {
-                        bool chg = false;
+                    // slot by slot: a slot's dwords only read lower addresses (earlier slots, already
+                    // final, or lower dwords of the same slot), so each slot is swept to its own
+                    // fixed point once the slots before it are final
 #pragma unroll
-                        for (uint32_t i = 0; i < kGD; ++i) {
-                            if (gd[i] == 0xFFFFFFFFu) continue;
+                    for (uint32_t i = 0; i < kGD; ++i) {
+                        if (64u * i >= T) break;
+                        for (uint32_t sweeps = 0;; ++sweeps) {
+                            bool chg = false;
+                            if (gd[i] == 0xFFFFFFFFu) goto next_sweep;
+                            {
                             uint32_t* rd = ring + (gd[i] & (kORW - 1));
                             const uint32_t cur = *rd;
                             uint32_t v;
@@ -810,9 +919,11 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
                                 chg = true;
                                 mskor(rd, gm[i], v);
                             }
+                            }
+                        next_sweep:
+                            ++nrounds;
+                            if (!__ballot(chg) || sweeps > 8192u) break;  // (a bound, never reached)
                         }
-                        ++nrounds;
-                        if (!__ballot(chg) || ++sweeps > 8192u) break;  // (a bound, never reached)
                     }
                 } else {
                     // (more pending output than the registers hold: multi-round resolution, the
@@ -821,7 +932,7 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
                         const uint64_t pm = __ballot(pend);
                         if (!pm) break;
                         const uint32_t first = (uint32_t)__builtin_ctzll(pm);
-                        const uint32_t h = (uint32_t)__shfl((int)md, (int)first, 64);
+                        const uint32_t h = rdlane(md, (int)first);
                         const bool run = pend && (lane == first || (off >= ml && ms + ml <= h));
                         const uint32_t step = off < 16u ? off : 16u;
                         for (uint32_t c = 0; __ballot(run && c < ml); c += step)
@@ -843,12 +954,12 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
             // alone, wave-wide
             uint32_t i0 = 0;
             while (i0 < nact) {
-                const uint32_t base = i0 ? (uint32_t)__shfl((int)Sincl_c, (int)(i0 - 1), 64) : 0u;
+                const uint32_t base = i0 ? rdlane(Sincl_c, (int)(i0 - 1)) : 0u;
                 const uint64_t fit = __ballot(act && lane >= i0 && Sincl_c - base <= kWin);
                 const uint32_t i1 = fit ? 64u - (uint32_t)__builtin_clzll(fit) : i0;
                 if (i1 <= i0) {
-                    const uint32_t sll = (uint32_t)__shfl((int)ll, (int)i0, 64), slit = (uint32_t)__shfl((int)lit, (int)i0, 64);
-                    const uint32_t soff = (uint32_t)__shfl((int)off, (int)i0, 64), sml = (uint32_t)__shfl((int)ml, (int)i0, 64);
+                    const uint32_t sll = rdlane(ll, (int)i0), slit = rdlane(lit, (int)i0);
+                    const uint32_t soff = rdlane(off, (int)i0), sml = rdlane(ml, (int)i0);
                     for (uint32_t k = 0; k < sll; k += kFl) {
                         const uint32_t piece = umin_(kFl, sll - k);
                         const uint32_t j = 16u * lane;
@@ -880,7 +991,7 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
                     continue;
                 }
                 const bool inb = act && lane >= i0 && lane < i1;
-                const uint32_t Sb = (uint32_t)__shfl((int)Sincl_c, (int)(i1 - 1), 64) - base;
+                const uint32_t Sb = rdlane(Sincl_c, (int)(i1 - 1)) - base;
                 const uint32_t d0 = upos + Sincl_c - len - base;
                 for (uint32_t c = 0; __ballot(inb && c < ll); c += 16u)
                     if (inb && c < ll) rst(ring, d0 + c, gld16_blk(in, lit + c, C), umin_(16u, ll - c));
@@ -902,7 +1013,7 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
                     const uint64_t pm = __ballot(pend);
                     if (!pm) break;
                     const uint32_t first = (uint32_t)__builtin_ctzll(pm);
-                    const uint32_t h = (uint32_t)__shfl((int)md, (int)first, 64);
+                    const uint32_t h = rdlane(md, (int)first);
                     run = pend && (lane == first || (off >= ml && ms + ml <= h));
                     pend = pend && !run;
                 }
