@@ -221,9 +221,13 @@ def cpu_baseline(data_chunk: bytes, block: int, seconds: float):
 
 
 # ------------------------------------------------------------------ the GPU bench (one rank)
-# decode: the parser + executor kernel (k_decode_pe); S3HC_DEC_ONEWAVE=1 selects the one-wave kernel
+# decode: the fast path's token index + executor (k_dtok + k_dexec; k_decode_pe then only exits for
+# the units they took), or with S3HC_FAST=0 / S3HC_FAST_DISABLE the parser + executor kernel
+# (k_decode_pe; S3HC_DEC_ONEWAVE=1 selects the one-wave kernel)
+_FAST_OFF = bool(os.environ.get("S3HC_FAST_DISABLE")) or os.environ.get("S3HC_FAST", "") == "0"
 KERNEL_SYMBOL = {"enc_parse": "k_enc_parse", "enc_emit": "k_enc_emit",
-                 "decode": "k_decode_units" if os.environ.get("S3HC_DEC_ONEWAVE") else "k_decode_pe",
+                 "decode": ("k_decode_units" if os.environ.get("S3HC_DEC_ONEWAVE") else "k_decode_pe") if _FAST_OFF
+                 else "k_dtok+k_dexec+k_decode_pe",
                  "dec_close": "k_dframe_close"}
 
 
@@ -237,10 +241,13 @@ def pmc_traffic(kernel):
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    k = d.get(KERNEL_SYMBOL.get(kernel, kernel), {})
-    if "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
-        return None, None
-    return int((2 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024), os.path.relpath(files[-1], ROOT)
+    total = 0.0
+    for part in KERNEL_SYMBOL.get(kernel, kernel).split("+"):  # a phase of several kernels: their sum
+        k = d.get(part, {})
+        if "FETCH_SIZE" not in k or "WRITE_SIZE" not in k:
+            return None, None
+        total += 2 * k["FETCH_SIZE"] + k["WRITE_SIZE"]
+    return int(total * 1024), os.path.relpath(files[-1], ROOT)
 
 
 def roofline_obj(kt, name, alg_bytes, profiled_shape: bool):

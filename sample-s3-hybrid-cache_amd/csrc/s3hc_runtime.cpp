@@ -443,10 +443,12 @@ struct LbScratch {
 
 // The 64 KiB-block fast path (s3hc_fast.hip) is opt-in while it is slower than the per-unit
 // decoder on config 2 (S3HC_FAST=1 enables it; S3HC_FAST_DISABLE=1 always wins).
+// The 64 KiB-block fast path (k_dtok + k_dexec) is on by default; S3HC_FAST=0 or
+// S3HC_FAST_DISABLE leave every unit to the per-unit decoder (A/B runs, parity tests).
 static bool fast_path_enabled() {
     if (getenv("S3HC_FAST_DISABLE")) return false;
     const char* e = getenv("S3HC_FAST");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
 }
 
 // Block decode of a batch: large blocks by the large-block path (when L is active), the rest

@@ -38,6 +38,9 @@ for _ in range(5):
 print(round(best * 1e3, 4))
 ''' % ROOT
 
+if os.environ.get("FX_INPROC"):  # one library, in this process (for rocprofv3 --pmc)
+    exec(CHILD)
+    sys.exit(0)
 res = {}
 for lib in sys.argv[1:]:
     env = dict(os.environ, S3HC_LIB_PATH=lib, S3HC_FAST="1")
