@@ -43,13 +43,17 @@ __device__ unsigned long long g_fprof[32];
 #endif
 namespace fst {
 constexpr uint32_t kMaxC = kFastMaxC;
-constexpr uint32_t kTT = 256;                  // k_dtok threads = speculative segments per block
+#ifndef S3HC_DTOK_TT
+#define S3HC_DTOK_TT 256
+#endif
+constexpr uint32_t kTT = S3HC_DTOK_TT;         // k_dtok threads = speculative segments per block
 constexpr uint32_t kStage = kMaxC + 64;        // staged block: 16-B alignment slack + zero read-ahead
 constexpr uint32_t kBitW = kMaxC / 32;         // bitmap words, one bit per compressed position
 constexpr uint32_t END = 0xFFFFFFFEu;          // chain ended with the block's last sequence
 constexpr uint32_t DEAD = 0xFFFFFFFFu;         // malformed token (or a walk that gave up)
 constexpr uint32_t kOvfCap = 4096;             // hops a walk past its segment may take before giving up
-constexpr uint32_t kLv = 8;                    // doubling levels: chains over <= 256 segments
+constexpr uint32_t kLv = kTT == 512 ? 9 : 8;   // doubling levels: chains over <= kTT segments
+static_assert(kTT == 256 || kTT == 512, "k_dtok: 4 or 8 waves");
 constexpr uint32_t kTermEnd = kTT, kTermBad = kTT + 1;
 constexpr uint32_t kMEnd = 0xFFFEu, kMBad = 0xFFFFu;  // u16 merge codes (positions are < kMaxC)
 }  // namespace fst
@@ -139,7 +143,8 @@ __device__ __forceinline__ Tok hop(const uint8_t* st, uint32_t mis, uint32_t p, 
     return T;
 }
 
-// exclusive scan over the 256 threads of a workgroup (4 waves); *total = sum
+// exclusive scan over the NW waves of a workgroup; *total = sum
+template <uint32_t NW>
 __device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     uint32_t x = v;
@@ -150,9 +155,14 @@ __device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* scratch, 
     }
     if (lane == 63) scratch[w] = x;
     __syncthreads();
-    const uint32_t s0 = scratch[0], s1 = scratch[1], s2 = scratch[2], s3 = scratch[3];
-    const uint32_t before = (w > 0 ? s0 : 0u) + (w > 1 ? s1 : 0u) + (w > 2 ? s2 : 0u);
-    *total = s0 + s1 + s2 + s3;
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NW; ++k) {
+        const uint32_t sk = scratch[k];
+        before += k < w ? sk : 0u;
+        all += sk;
+    }
+    *total = all;
     __syncthreads();
     return before + x - v;
 }
@@ -165,7 +175,6 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
     using namespace fst;
     __shared__ __attribute__((aligned(16))) uint8_t stage[kStage];
     __shared__ uint32_t bits[kBitW];
-    __shared__ uint16_t smerge[kTT];   // per segment: where its walk merged (position, M_END or M_BAD)
     __shared__ uint16_t svfrom[kTT];   // per segment on the true chain: its first true token (else M_BAD)
     __shared__ uint16_t J[2][kTT + 2]; // succ^(2^k) per segment, ping-pong; kTT / kTT + 1 are terminals
     __shared__ uint8_t reach[kTT + 2]; // segment is on the true chain
@@ -191,17 +200,18 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
     const uint8_t* in = src + B.src_off;
     const uint32_t mis = (uint32_t)((uintptr_t)in & 15u);
     {
-        // (mis + C + 15) / 16 <= 2050 granules: at most 9 per thread, all loads in flight at once
+        // (mis + C + 15) / 16 <= 2050 granules: at most 9 (256 threads) or 5 (512) per thread,
+        // all loads in flight at once
         const uint4* gw = (const uint4*)(in - mis);
         const uint32_t nv = (mis + C + 15u) >> 4;
-        static_assert((kMaxC + 30u) / 16u <= 9u * kTT, "staging covers the largest block");
+        static_assert((kMaxC + 30u) / 16u <= (kTT == 512 ? 5u : 9u) * kTT, "staging covers the largest block");
         uint4 v0, v1, v2, v3, v4, v5, v6, v7, v8;
 #define S3HC_LDG(i, v) if (g + (i) * kTT < nv) v = gw[g + (i) * kTT];
 #define S3HC_STS(i, v) if (g + (i) * kTT < nv) ((uint4*)stage)[g + (i) * kTT] = v;
         S3HC_LDG(0, v0) S3HC_LDG(1, v1) S3HC_LDG(2, v2) S3HC_LDG(3, v3) S3HC_LDG(4, v4)
-        S3HC_LDG(5, v5) S3HC_LDG(6, v6) S3HC_LDG(7, v7) S3HC_LDG(8, v8)
+        if (kTT == 256) { S3HC_LDG(5, v5) S3HC_LDG(6, v6) S3HC_LDG(7, v7) S3HC_LDG(8, v8) }
         S3HC_STS(0, v0) S3HC_STS(1, v1) S3HC_STS(2, v2) S3HC_STS(3, v3) S3HC_STS(4, v4)
-        S3HC_STS(5, v5) S3HC_STS(6, v6) S3HC_STS(7, v7) S3HC_STS(8, v8)
+        if (kTT == 256) { S3HC_STS(5, v5) S3HC_STS(6, v6) S3HC_STS(7, v7) S3HC_STS(8, v8) }
 #undef S3HC_LDG
 #undef S3HC_STS
         for (uint32_t k = g; k < (C + 31u) / 32u; k += kTT) bits[k] = 0u;
@@ -245,7 +255,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
         if ((g & 63u) == 0) FP_ADD(10, mx);
     }
 #endif
-    smerge[g] = (uint16_t)(m < C ? m : (m == END ? kMEnd : kMBad));
+    const uint32_t smerge = m < C ? m : (m == END ? kMEnd : kMBad);  // where my walk merged
     svfrom[g] = kMBad;
     // successor segment of my walk: the segment of the merge point, or a terminal
     J[0][g] = (uint16_t)(m < C ? m / segL : (m == END ? kTermEnd : kTermBad));
@@ -267,7 +277,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
     // a segment on the chain hands its merge point to its successor (that segment's first true
     // token); the chain's last segment ends it: END, or a malformed / abandoned walk
     if (reach[g]) {
-        const uint32_t sm = smerge[g];
+        const uint32_t sm = smerge;
         if (sm < kMEnd) svfrom[sm / segL] = (uint16_t)sm;
         else sflag[0] = sm == kMEnd ? kTermEnd : kTermBad;
     }
@@ -322,8 +332,8 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
     }
     const uint64_t tp6 = FP_NOW();
     uint32_t Utot, N;
-    const uint32_t obase = wg_excl_scan(o, scr, &Utot);
-    (void)wg_excl_scan(ntok, scr, &N);
+    const uint32_t obase = wg_excl_scan<kTT / 64>(o, scr, &Utot);
+    (void)wg_excl_scan<kTT / 64>(ntok, scr, &N);
     const bool fail = bad || (valid && (int64_t)obase + minsl < 0);
     if (fail) sflag[1] = 1u;
     __syncthreads();

@@ -1398,6 +1398,16 @@ constexpr uint32_t kTbl = 1u << kHashLog;
 #endif
 constexpr uint32_t kSteps = S3HC_STEPS;                     // 64-position steps per sub-block
 constexpr uint32_t kStash = 64 * kSteps / 4;                // hops per sub-block (a hop covers >= 4 bytes)
+#ifndef S3HC_PSTRIDE
+#define S3HC_PSTRIDE 1
+#endif
+constexpr uint32_t kPS = S3HC_PSTRIDE;                      // positions per lane and step: every position is
+                                                            // inserted into the table, the first of a lane's
+                                                            // kPS is probed (a match starting at one of the
+                                                            // others is found by the backward extension)
+constexpr uint32_t kStepPos = 64 * kPS;                     // positions of one step
+constexpr uint32_t kPSteps = kSteps / kPS;                  // steps of a sub-block (its 64 x kSteps positions)
+static_assert(kPS == 1 || kPS == 2, "probe stride 1 or 2");
 #ifndef S3HC_FWD_DW
 #define S3HC_FWD_DW 5
 #endif
@@ -1584,10 +1594,10 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
         const uint64_t tc0 = PROF_NOW();
         PROF_ADD(epr, 6, 1);
         // ---- A: table pass
-        uint32_t vv[kSteps], vm[kSteps], vm8[kSteps], cc[kSteps];
+        uint32_t vv[kPSteps], vm[kPSteps], vm8[kPSteps], cc[kPSteps];
 #pragma unroll
-        for (uint32_t q = 0; q < kSteps; ++q) {
-            const uint32_t P = sb + 64 * q + lane;
+        for (uint32_t q = 0; q < kPSteps; ++q) {
+            const uint32_t P = sb + kStepPos * q + kPS * lane;
             const uint32_t i = P - pw_lo;
             const uint32_t a = i >> 2, sh = i & 3;
             const uint32_t w0 = dw[a], w1 = dw[a + 1], wp = dw[(int)a - 1], wpp = dw[(int)a - 2];
@@ -1597,14 +1607,18 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             const uint32_t h = hash4(vv[q]);
             cc[q] = tbl[h];
             tbl[P < sb_end ? h : kTbl] = (uint16_t)i;
+            if (kPS == 2) {  // (i even: sh + 1 <= 3) the lane's second position, inserted after the first
+                const uint32_t h1 = hash4(__builtin_amdgcn_alignbyte(w1, w0, sh + 1));
+                tbl[P + 1 < sb_end ? h1 : kTbl] = (uint16_t)(i + 1);
+            }
         }
         // ---- B: verify + measure both candidates (table: one LDS round trip; distance 1..4:
         // from the position's own bytes, no reads)
-        uint32_t word[kSteps], flen[kSteps];
-        uint64_t mm[kSteps];
+        uint32_t word[kPSteps], flen[kPSteps];
+        uint64_t mm[kPSteps];
 #pragma unroll
-        for (uint32_t q = 0; q < kSteps; ++q) {
-            const uint32_t P = sb + 64 * q + lane;
+        for (uint32_t q = 0; q < kPSteps; ++q) {
+            const uint32_t P = sb + kStepPos * q + kPS * lane;
             const bool valid = P < sb_end;
             const uint32_t i = P - pw_lo;
             const uint32_t v = vv[q], vm4 = vm[q];
@@ -1680,25 +1694,28 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
         const uint32_t ns_sb = nseq, le_sb = last_end;
         WALK_PRIO_ON();
 #pragma unroll
-        for (uint32_t q = 0; q < kSteps; ++q) {
-            const uint32_t base = sb + 64 * q;
-            if (x >= base + 64 || !mm[q]) continue;
+        for (uint32_t q = 0; q < kPSteps; ++q) {
+            const uint32_t base = sb + kStepPos * q;
+            if (x >= base + kStepPos || !mm[q]) continue;
             uint64_t hm = 0;
             // per lane: greedy position after taking this lane's match (chunk-relative);
-            // 0x100 marks a match that reached kFwd and needs the wave-wide extension
-            const uint32_t nxr = (uint32_t)lane + flen[q] + (flen[q] == kFwd ? 0x100u : 0u);
+            // 0x1000 marks a match that reached kFwd and needs the wave-wide extension
+            const uint32_t nxr = kPS * (uint32_t)lane + flen[q] + (flen[q] == kFwd ? 0x1000u : 0u);
             uint32_t r = x > base ? x - base : 0u, rend = 0;
-            while (r < 64u) {
-                const uint64_t av = mm[q] & (~0ull << r);
+            while (r < kStepPos) {
+                // the first probed position at or after r (a probe after r reaches back to it)
+                const uint32_t j0 = (r + kPS - 1u) / kPS;
+                if (j0 >= 64u) break;
+                const uint64_t av = mm[q] & (~0ull << j0);
                 if (!av) break;
                 const uint32_t j = (uint32_t)__builtin_ctzll(av);
                 hm |= 1ull << j;
                 r = rdl(nxr, j);
-                if (r & 0x100u) {  // long match: wave-wide forward extension
+                if (r & 0x1000u) {  // long match: wave-wide forward extension
                     const uint64_t tx0 = PROF_NOW();
                     PROF_ADD(epr, 8, 1);
                     const uint32_t wj = rdl(word[q], j);
-                    const uint32_t P = base + j;
+                    const uint32_t P = base + kPS * j;
                     const uint32_t maxf = end_lim - P;
                     const uint32_t c = P - (wj & 0xFFFFu);
                     uint32_t lenf = kFwd;
@@ -1721,7 +1738,7 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
                         break;
                     }
                     flen[q] = (uint32_t)lane == j ? lenf : flen[q];
-                    r = j + lenf;
+                    r = kPS * j + lenf;
                     PROF_ADD(epr, 2, PROF_NOW() - tx0);
                 }
                 rend = r;
@@ -1731,7 +1748,7 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
                 const uint32_t rank =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0));
                 const uint32_t hidx = (hm >> lane) & 1ull ? nseq - ns_sb + rank : kStash + ((uint32_t)lane & 7u);
-                stash[hidx] = make_uint2((base + lane - seg_lo) | (flen[q] << 16), word[q]);
+                stash[hidx] = make_uint2((base + kPS * lane - seg_lo) | (flen[q] << 16), word[q]);
                 last_end = base + rend;
                 nseq += (uint32_t)__builtin_popcountll(hm);
             }
