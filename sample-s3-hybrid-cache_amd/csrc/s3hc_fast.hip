@@ -169,9 +169,9 @@ __device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* scratch, 
 }  // namespace
 
 // ------------------------------------------------------------------ k_dtok
-__global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ src, const DecBlock* __restrict__ blk,
-                                                   const DecUnit* __restrict__ units, uint32_t nunits,
-                                                   const uint8_t* __restrict__ unit_lb, FastArgs a) {
+__device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __restrict__ src,
+                                          const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+                                          const uint8_t* __restrict__ unit_lb, const FastArgs& a) {
     using namespace fst;
     __shared__ __attribute__((aligned(16))) uint8_t stage[kStage];
     __shared__ uint32_t bits[kBitW];
@@ -180,8 +180,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
     __shared__ uint8_t reach[kTT + 2]; // segment is on the true chain
     __shared__ uint32_t scr[8];
     __shared__ uint32_t sflag[4];      // [0] terminal of the chain, [1] failure, [2] pool base
-    const uint32_t u = blockIdx.x, g = threadIdx.x;
-    if (u >= nunits) return;
+    const uint32_t g = threadIdx.x;
     const DecUnit U = units[u];
     bool take = U.n == 1 && !(unit_lb && unit_lb[u]);
     DecBlock B;
@@ -194,7 +193,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
         return;
     }
     const uint32_t C = B.csize;
-    const uint64_t tp0 = FP_NOW();
+    [[maybe_unused]] const uint64_t tp0 = FP_NOW();
     // ---- stage the block: aligned 16-byte loads (never outside the 16-byte granules holding
     // block bytes), four in flight per thread before their LDS stores
     const uint8_t* in = src + B.src_off;
@@ -225,7 +224,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
     if (g < 48u) stage[mis + C + g] = 0;  // read-ahead past the block reads zeros
     __syncthreads();
 
-    const uint64_t tp1 = FP_NOW();
+    [[maybe_unused]] const uint64_t tp1 = FP_NOW();
     // ---- walk 1: from the start of my segment to its end, marking every position visited
     const uint32_t segL = (C + kTT - 1u) / kTT;
     const uint32_t s0 = umin_(g * segL, C), s1 = umin_(s0 + segL, C);
@@ -236,7 +235,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
     }
     const uint32_t x = s0 < s1 ? p : DEAD;
     __syncthreads();
-    const uint64_t tp2 = FP_NOW();
+    [[maybe_unused]] const uint64_t tp2 = FP_NOW();
     // ---- walk 2: past the segment until the chain lands on a marked position (merge)
     uint32_t m = x, ovf = 0;
     while (m < C) {
@@ -264,7 +263,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
         reach[kTT + g] = 0;
     }
     __syncthreads();
-    const uint64_t tp3 = FP_NOW();
+    [[maybe_unused]] const uint64_t tp3 = FP_NOW();
     // ---- the true chain: segment 0, then the segment its walk merged into, ... Reachability
     // from segment 0 by doubling: after step k every segment within 2^(k+1) links is marked.
 #pragma unroll
@@ -287,7 +286,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
         if (g == 0) a.unit_fast[u] = 0;
         return;
     }
-    const uint64_t tp4 = FP_NOW();
+    [[maybe_unused]] const uint64_t tp4 = FP_NOW();
     // ---- the true token bitmap: in a segment on the chain the marks before its first true
     // token are speculative (cleared), a segment off the chain is cleared whole; the chain's
     // walks past their segments (walk 2) then mark the tokens they passed
@@ -303,7 +302,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
         }
     }
     __syncthreads();
-    const uint64_t tp5 = FP_NOW();
+    [[maybe_unused]] const uint64_t tp5 = FP_NOW();
     // ---- validate (lz4_flex bounds: output within the block limit and the caller's capacity,
     // every offset non-zero and within the bytes produced before its match) while marking the
     // tokens past my segment
@@ -330,7 +329,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
             p = T.nxt;
         }
     }
-    const uint64_t tp6 = FP_NOW();
+    [[maybe_unused]] const uint64_t tp6 = FP_NOW();
     uint32_t Utot, N;
     const uint32_t obase = wg_excl_scan<kTT / 64>(o, scr, &Utot);
     (void)wg_excl_scan<kTT / 64>(ntok, scr, &N);
@@ -364,6 +363,23 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
         FP_ADD(7, 1);
     }
 #endif
+}
+
+// units [0, count) of a plan, count read on the device (a device-built plan: the frame walk's
+// block total) or the launch's cap; the grid strides over them
+__device__ __forceinline__ uint32_t unit_count(const uint64_t* ucount, uint32_t cap) {
+    return ucount ? (uint32_t)min<uint64_t>(*ucount, (uint64_t)cap) : cap;
+}
+
+__global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ src, const DecBlock* __restrict__ blk,
+                                                   const DecUnit* __restrict__ units, uint32_t nunits,
+                                                   const uint64_t* __restrict__ ucount,
+                                                   const uint8_t* __restrict__ unit_lb, FastArgs a) {
+    const uint32_t nu = unit_count(ucount, nunits);
+    for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
+        dtok_unit(u, src, blk, units, unit_lb, a);
+        __syncthreads();  // (the next unit reuses the LDS)
+    }
 }
 
 // ------------------------------------------------------------------ k_dexec
@@ -648,17 +664,16 @@ __device__ uint32_t periodic_dword(const uint32_t* ring, uint4 P, uint32_t d, ui
     return v;
 }
 
-__global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                              const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
-                                              uint32_t nunits, uint32_t* __restrict__ blk_out,
-                                              int32_t* __restrict__ blk_status, FastArgs a) {
+__device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                           const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+                                           uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
+                                           const FastArgs& a) {
     using namespace fst;
     __shared__ __attribute__((aligned(16))) uint32_t ring[kORW];
     __shared__ uint16_t tq[kQ];              // token positions, queue entry t = token t
     __shared__ uint4 pinfo[64];              // pending matches: md, ms, ml | off << 16, first dword - rank
     __shared__ uint8_t gmk[kGW];             // pending dwords: rank of each lane's first dword -> lane + 1
-    const uint32_t u = blockIdx.x;
-    if (u >= nunits || !a.unit_fast[u]) return;
+    if (!a.unit_fast[u]) return;
     const uint32_t lane = threadIdx.x;
     const DecUnit Un = units[u];
     const DecBlock B = blk[Un.first];
@@ -750,11 +765,11 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
         lit1_c = gld16(in + q1);
         lsh_c = (lit - (uint32_t)q0) | ((lit + 16u - (uint32_t)q1) << 8);
     }
-    const uint64_t te0 = FP_NOW();
-    uint64_t tsum[6] = {0, 0, 0, 0, 0, 0};
+    [[maybe_unused]] const uint64_t te0 = FP_NOW();
+    [[maybe_unused]] uint64_t tsum[6] = {0, 0, 0, 0, 0, 0};
     uint32_t nrounds = 0;
     for (uint32_t w = 0; w < nwin; ++w) {
-        uint64_t tq0 = FP_NOW();
+        [[maybe_unused]] uint64_t tq0 = FP_NOW();
         const uint32_t nact = umin_(64u, N - 64u * w);
         const bool act = lane < nact;
         // ---- stage A: window w+3's token dword (loads are unconditional: a lane without a
@@ -1078,13 +1093,27 @@ __global__ __launch_bounds__(64) void k_dexec(const uint8_t* __restrict__ src, u
 #endif
 }
 
+// (<= 128 VGPRs: 4 waves per SIMD, a 4096-block batch resident at once)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_dexec(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                              const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+                                              uint32_t nunits, const uint64_t* __restrict__ ucount,
+                                              uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
+                                              FastArgs a) {
+    const uint32_t nu = unit_count(ucount, nunits);
+    for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
+        dexec_unit(u, src, dst, blk, units, blk_out, blk_status, a);
+        wsync();
+    }
+}
+
 // ================================================================ launchers
 static inline uint32_t fcdiv(uint64_t x, uint64_t y) { return (uint32_t)((x + y - 1) / y); }
 
 hipError_t launch_fast_tok(const uint8_t* src, const DecBlock* blk, const DecUnit* units, uint32_t nunits,
-                           const uint8_t* unit_lb, const FastArgs& a, hipStream_t st) {
-    if (!nunits) return hipSuccess;
-    hipLaunchKernelGGL(k_dtok, dim3(nunits), dim3(fst::kTT), 0, st, src, blk, units, nunits, unit_lb, a);
+                           const uint64_t* ucount, uint32_t grid, const uint8_t* unit_lb, const FastArgs& a,
+                           hipStream_t st) {
+    if (!nunits || !grid) return hipSuccess;
+    hipLaunchKernelGGL(k_dtok, dim3(grid), dim3(fst::kTT), 0, st, src, blk, units, nunits, ucount, unit_lb, a);
     return hipGetLastError();
 }
 #ifdef FPROF
@@ -1100,10 +1129,11 @@ extern "C" int s3hc_diag_fprof(unsigned long long* out, int n, int reset) {
 }
 #endif
 hipError_t launch_fast_exec(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
-                            uint32_t nunits, uint32_t* blk_out, int32_t* blk_status, const FastArgs& a,
-                            hipStream_t st) {
-    if (!nunits) return hipSuccess;
-    hipLaunchKernelGGL(k_dexec, dim3(nunits), dim3(64), 0, st, src, dst, blk, units, nunits, blk_out, blk_status, a);
+                            uint32_t nunits, const uint64_t* ucount, uint32_t grid, uint32_t* blk_out,
+                            int32_t* blk_status, const FastArgs& a, hipStream_t st) {
+    if (!nunits || !grid) return hipSuccess;
+    hipLaunchKernelGGL(k_dexec, dim3(grid), dim3(64), 0, st, src, dst, blk, units, nunits, ucount, blk_out,
+                       blk_status, a);
     return hipGetLastError();
 }
 }  // namespace s3hc

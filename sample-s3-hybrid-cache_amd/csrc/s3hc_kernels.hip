@@ -905,21 +905,22 @@ __device__ int dec_block(DecWave& w, const uint8_t* in, uint32_t C, uint32_t lim
     }
 }
 
-__global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict__ src, uint8_t* dst,
-                                                      const DecBlock* __restrict__ blk,
-                                                      const DecUnit* __restrict__ units, uint32_t nunits,
-                                                      uint32_t* __restrict__ blk_out,
-                                                      int32_t* __restrict__ blk_status,
-                                                      const uint8_t* __restrict__ unit_lb,
-                                                      const uint8_t* __restrict__ unit_fast) {
+// units [0, count) of a plan: count read on the device (a device-built plan: the frame walk's
+// block total) or the launch's cap; grids stride over them
+__device__ __forceinline__ uint32_t unit_count(const uint64_t* ucount, uint32_t cap) {
+    return ucount ? (uint32_t)min<uint64_t>(*ucount, (uint64_t)cap) : cap;
+}
+
 #ifndef S3HC_DEC_LDS_PAD
 #define S3HC_DEC_LDS_PAD 0  // diagnostic builds: extra LDS per workgroup to lower occupancy
 #endif
-    __shared__ __attribute__((aligned(16))) uint8_t smem[dec::kWaves * dec::kWaveLds + S3HC_DEC_LDS_PAD];
+__device__ __forceinline__ void decode_unit_wave(const uint32_t u, uint8_t* smem, const uint8_t* __restrict__ src,
+                                                 uint8_t* dst, const DecBlock* __restrict__ blk,
+                                                 const DecUnit* __restrict__ units, uint32_t* __restrict__ blk_out,
+                                                 int32_t* __restrict__ blk_status, const uint8_t* __restrict__ unit_lb,
+                                                 const uint8_t* __restrict__ unit_fast) {
     const int lane = lane_id();
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t u = blockIdx.x * dec::kWaves + wv;
-    if (u >= nunits) return;
     if (unit_lb && unit_lb[u]) return;  // decoded by the large-block path (s3hc_lb.hip)
     if (unit_fast && unit_fast[u]) return;  // decoded by the 64 KiB-block path (s3hc_fast.hip)
     const DecUnit U = units[u];
@@ -974,6 +975,23 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
 #endif
 }
 
+__global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict__ src, uint8_t* dst,
+                                                      const DecBlock* __restrict__ blk,
+                                                      const DecUnit* __restrict__ units, uint32_t nunits,
+                                                      const uint64_t* __restrict__ ucount,
+                                                      uint32_t* __restrict__ blk_out,
+                                                      int32_t* __restrict__ blk_status,
+                                                      const uint8_t* __restrict__ unit_lb,
+                                                      const uint8_t* __restrict__ unit_fast) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[dec::kWaves * dec::kWaveLds + S3HC_DEC_LDS_PAD];
+    const uint32_t nu = unit_count(ucount, nunits);
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (uint32_t ub = blockIdx.x; ub * dec::kWaves < nu; ub += gridDim.x) {  // (each wave on its own LDS)
+        const uint32_t u = ub * dec::kWaves + wv;
+        if (u < nu) decode_unit_wave(u, smem, src, dst, blk, units, blk_out, blk_status, unit_lb, unit_fast);
+    }
+}
+
 // ====================================================== decode, parser + executor waves
 // k_decode_pe: the same decoder with the two halves of a window on two waves of one 128-thread
 // workgroup per unit. Wave P walks the token chain (staging, next-token steps, the serial
@@ -1009,15 +1027,12 @@ static_assert(kLds <= 10240, "16 units per CU (a 4096-block batch resident at on
 #ifndef S3HC_PE_WAVES_PER_EU
 #define S3HC_PE_WAVES_PER_EU 8
 #endif
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAVES_PER_EU, 8))) void k_decode_pe(
-    const uint8_t* __restrict__ src, uint8_t* dst, const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
-    uint32_t nunits, uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
+__device__ __forceinline__ void decode_unit_pe(
+    const uint32_t u, uint8_t* smem, const uint8_t* __restrict__ src, uint8_t* dst, const DecBlock* __restrict__ blk,
+    const DecUnit* __restrict__ units, uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
     const uint8_t* __restrict__ unit_lb, const uint8_t* __restrict__ unit_fast) {
     using namespace dec;
     using dpe::Slot;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[dpe::kLds];
-    const uint32_t u = blockIdx.x;
-    if (u >= nunits) return;
     if (unit_lb && unit_lb[u]) return;  // decoded by the large-block path (s3hc_lb.hip)
     if (unit_fast && unit_fast[u]) return;  // decoded by the 64 KiB-block path (s3hc_fast.hip)
     const DecUnit U = units[u];
@@ -1381,6 +1396,18 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAV
         }
         __syncthreads();
         if (*done) break;
+    }
+}
+
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(S3HC_PE_WAVES_PER_EU, 8))) void k_decode_pe(
+    const uint8_t* __restrict__ src, uint8_t* dst, const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+    uint32_t nunits, const uint64_t* __restrict__ ucount, uint32_t* __restrict__ blk_out,
+    int32_t* __restrict__ blk_status, const uint8_t* __restrict__ unit_lb, const uint8_t* __restrict__ unit_fast) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[dpe::kLds];
+    const uint32_t nu = unit_count(ucount, nunits);
+    for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
+        decode_unit_pe(u, smem, src, dst, blk, units, blk_out, blk_status, unit_lb, unit_fast);
+        __syncthreads();  // (the next unit reuses the LDS)
     }
 }
 
@@ -2276,16 +2303,16 @@ hipError_t launch_xxh32(const uint8_t* base, const uint64_t* off, const uint32_t
     return hipGetLastError();
 }
 hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
-                               uint32_t nunits, uint32_t* blk_out, int32_t* blk_status, const uint8_t* unit_lb,
-                               const uint8_t* unit_fast, hipStream_t st) {
-    if (!nunits) return hipSuccess;
+                               uint32_t nunits, const uint64_t* ucount, uint32_t grid, uint32_t* blk_out,
+                               int32_t* blk_status, const uint8_t* unit_lb, const uint8_t* unit_fast, hipStream_t st) {
+    if (!nunits || !grid) return hipSuccess;
     // S3HC_DEC_ONEWAVE=1 (comparisons): one wave per unit doing both halves (k_decode_units)
     const bool onewave = getenv("S3HC_DEC_ONEWAVE") != nullptr;  // read per launch (tests toggle it)
     if (onewave)
-        hipLaunchKernelGGL(k_decode_units, dim3(cdiv(nunits, dec::kWaves)), dim3(64 * dec::kWaves), 0, st, src, dst,
-                           blk, units, nunits, blk_out, blk_status, unit_lb, unit_fast);
+        hipLaunchKernelGGL(k_decode_units, dim3(cdiv(grid, dec::kWaves)), dim3(64 * dec::kWaves), 0, st, src, dst,
+                           blk, units, nunits, ucount, blk_out, blk_status, unit_lb, unit_fast);
     else
-        hipLaunchKernelGGL(k_decode_pe, dim3(nunits), dim3(128), 0, st, src, dst, blk, units, nunits, blk_out,
+        hipLaunchKernelGGL(k_decode_pe, dim3(grid), dim3(128), 0, st, src, dst, blk, units, nunits, ucount, blk_out,
                            blk_status, unit_lb, unit_fast);
     return hipGetLastError();
 }

@@ -280,7 +280,8 @@ __device__ __forceinline__ LbView lb_view(const uint8_t* src, const LbBlock& B, 
 
 // ---------------------------------------------------------------- classify
 __global__ __launch_bounds__(1024) void k_lb_classify(const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
-                                                      uint32_t nunits, LbArgs A) {
+                                                      uint32_t nunits, const uint64_t* __restrict__ ucount, LbArgs A) {
+    if (ucount) nunits = (uint32_t)min<uint64_t>(*ucount, (uint64_t)nunits);  // a device-built plan's units
     __shared__ uint32_t sh[3][16];
     __shared__ uint32_t carry[3];
     __shared__ uint32_t ntaken;
@@ -1367,8 +1368,9 @@ hipError_t launch_scan2(const uint32_t* in0, const uint32_t* in1, uint32_t n, ui
 // Parse stage: classify the units, tokenize, build the sequence table, statuses and sizes of
 // the taken blocks. Must precede k_decode_units (it reads unit_lb).
 hipError_t launch_lb_parse(const LbArgs& A, const uint8_t* src, const DecBlock* blk, const DecUnit* units,
-                           uint32_t nunits, uint32_t* blk_out, int32_t* blk_status, hipStream_t st) {
-    hipLaunchKernelGGL(k_lb_classify, dim3(1), dim3(1024), 0, st, blk, units, nunits, A);
+                           uint32_t nunits, const uint64_t* ucount, uint32_t* blk_out, int32_t* blk_status,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(k_lb_classify, dim3(1), dim3(1024), 0, st, blk, units, nunits, ucount, A);
     hipLaunchKernelGGL(k_lb_gran, dim3(A.chunk_cap), dim3(lb::kGpc), 0, st, src, A);
     hipLaunchKernelGGL(k_lb_exit, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
     hipLaunchKernelGGL(k_lb_entry, dim3(cdiv_lb(A.lb_cap, 64)), dim3(64), 0, st, A);

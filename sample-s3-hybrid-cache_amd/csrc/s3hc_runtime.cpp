@@ -30,14 +30,16 @@ namespace s3hc {
 hipError_t launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*, hipStream_t);
 hipError_t launch_compat_frames(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint8_t*, const uint64_t*,
                                 const uint32_t*, uint32_t*, uint32_t, hipStream_t);
-hipError_t launch_decode_units(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*,
-                               int32_t*, const uint8_t*, const uint8_t*, hipStream_t);
-hipError_t launch_fast_tok(const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint8_t*, const FastArgs&,
-                           hipStream_t);
-hipError_t launch_fast_exec(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*, int32_t*,
-                            const FastArgs&, hipStream_t);
-hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, uint32_t*, int32_t*,
-                           hipStream_t);
+// per-unit launches: units [0, *ucount) when ucount is set (a device-built plan), else [0, nunits);
+// `grid` workgroups stride over them
+hipError_t launch_decode_units(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*,
+                               uint32_t, uint32_t*, int32_t*, const uint8_t*, const uint8_t*, hipStream_t);
+hipError_t launch_fast_tok(const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*, uint32_t,
+                           const uint8_t*, const FastArgs&, hipStream_t);
+hipError_t launch_fast_exec(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*,
+                            uint32_t, uint32_t*, int32_t*, const FastArgs&, hipStream_t);
+hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*,
+                           uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_enc_parse(const uint8_t*, const EncBlock*, const uint2*, uint32_t, const uint64_t*, const uint32_t*,
                             uint32_t, uint32_t*, uint2*, SegSummary*, hipStream_t);
@@ -454,36 +456,49 @@ static bool fast_path_enabled() {
 // Block decode of a batch: large blocks by the large-block path (when L is active), the rest
 // one wave per unit. *blk_hash: the large-block path's per-block output hashes (single-block
 // units: 1 << 32 | xxh32, or 0), nullptr when the path did not run.
+// Plans walked on the device pass ucount (the frame walk's block total: the units' count) and
+// size the per-unit grids to their frames; host-walked plans know their units exactly.
 static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, const DecBlock* blk,
                                 const DecUnit* units, uint32_t nunits, uint32_t* blk_out, int32_t* blk_status,
-                                hipStream_t st, const uint64_t** blk_hash = nullptr) {
+                                hipStream_t st, const uint64_t** blk_hash = nullptr, const uint64_t* ucount = nullptr,
+                                uint32_t grid = 0) {
+    if (!grid || grid > nunits) grid = nunits;
     // S3HC_LB_DISABLE (tests, comparisons): every block goes to the one-wave decoder
     const bool lb = L && L->active && nunits && !getenv("S3HC_LB_DISABLE");
     if (blk_hash) *blk_hash = lb ? L->a.blk_hash : nullptr;
     hipError_t e;
-    if (lb && (e = launch_lb_parse(L->a, src, blk, units, nunits, blk_out, blk_status, st)) != hipSuccess) return e;
+    if (lb && (e = launch_lb_parse(L->a, src, blk, units, nunits, ucount, blk_out, blk_status, st)) != hipSuccess) return e;
     // 64 KiB blocks: token index + executor (S3HC_FAST_DISABLE=1: every block on the per-unit
     // decoder, for comparisons); blocks the fast path leaves go to the per-unit decoder below
     const bool fast = L && L->fast_ready && nunits && !(lb && L->all_lb) && fast_path_enabled();
     if (fast) {
-        if ((e = launch_fast_tok(src, blk, units, nunits, lb ? L->a.unit_lb : nullptr, L->fa, st)) != hipSuccess) return e;
-        if ((e = launch_fast_exec(src, dst, blk, units, nunits, blk_out, blk_status, L->fa, st)) != hipSuccess) return e;
+        if ((e = launch_fast_tok(src, blk, units, nunits, ucount, grid, lb ? L->a.unit_lb : nullptr, L->fa, st)) !=
+            hipSuccess)
+            return e;
+        if ((e = launch_fast_exec(src, dst, blk, units, nunits, ucount, grid, blk_out, blk_status, L->fa, st)) !=
+            hipSuccess)
+            return e;
         if (getenv("S3HC_FAST_TRACE")) {  // diagnostics: units the fast path took
-            std::vector<uint8_t> f(nunits);
-            std::vector<FastUnit> fu(nunits);
-            if ((e = hipMemcpyAsync(f.data(), L->fa.unit_fast, nunits, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-            if ((e = hipMemcpyAsync(fu.data(), L->fa.fu, nunits * sizeof(FastUnit), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+            uint64_t nu = nunits;
+            if (ucount && (e = hipMemcpyAsync(&nu, ucount, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+            nu = std::min<uint64_t>(nu, nunits);
+            std::vector<uint8_t> f(nu + 1);
+            std::vector<FastUnit> fu(nu + 1);
+            if ((e = hipMemcpyAsync(f.data(), L->fa.unit_fast, nu, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+            if ((e = hipMemcpyAsync(fu.data(), L->fa.fu, nu * sizeof(FastUnit), hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
             if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
             uint32_t k = 0;
             uint64_t ntok = 0;
-            for (uint32_t i = 0; i < nunits; ++i)
+            for (uint64_t i = 0; i < nu; ++i)
                 if (f[i]) { ++k; ntok += fu[i].ntok; }
-            fprintf(stderr, "[s3hc fast] units %u taken %u tokens %llu\n", nunits, k, (unsigned long long)ntok);
+            fprintf(stderr, "[s3hc fast] units %llu taken %u tokens %llu grid %u\n", (unsigned long long)nu, k,
+                    (unsigned long long)ntok, grid);
         }
     }
     if (!(lb && L->all_lb) &&
-        (e = launch_decode_units(src, dst, blk, units, nunits, blk_out, blk_status, lb ? L->a.unit_lb : nullptr,
-                                 fast ? L->fa.unit_fast : nullptr, st)) != hipSuccess)
+        (e = launch_decode_units(src, dst, blk, units, nunits, ucount, grid, blk_out, blk_status,
+                                 lb ? L->a.unit_lb : nullptr, fast ? L->fa.unit_fast : nullptr, st)) != hipSuccess)
         return e;
     if (lb && (e = launch_lb_exec(L->a, src, dst, blk_out, blk_status, st)) != hipSuccess) return e;
     if (lb && getenv("S3HC_LB_TRACE")) {  // diagnostics: blocks and chunks taken
@@ -873,7 +888,7 @@ extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src
         HIPCHK(launch_dframe_count(d_src, P->d_frame_off.as<uint64_t>(), P->d_frame_len.as<uint32_t>(),
                                    P->d_dst_cap.as<uint32_t>(), n, P->d_nblk.as<uint32_t>(), d_status, st));
         HIPCHK(launch_scan(P->d_nblk.as<uint32_t>(), n, P->d_blk_base.as<uint64_t>(), P->d_total.as<uint64_t>(), st));
-        HIPCHK(hipMemsetAsync(P->d_units.p, 0, (size_t)P->blk_cap * sizeof(DecUnit), st));
+        // (no clearing of the unit table: the per-unit kernels stop at the walk's block total)
         HIPCHK(launch_dframe_fill(d_src, P->d_frame_off.as<uint64_t>(), P->d_frame_len.as<uint32_t>(), n,
                                   P->d_dst_off.as<uint64_t>(), P->d_dst_cap.as<uint32_t>(), P->d_blk_base.as<uint64_t>(),
                                   d_status, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(),
@@ -881,8 +896,11 @@ extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src
         T.end();
         T.begin("decode");
         const uint64_t* bh = nullptr;
+        // one workgroup per frame (the common one block per frame: the exact unit count); frames of
+        // several independent blocks have their extra units taken by a stride of the grid
         HIPCHK(decode_launch(&P->lb, d_src, d_dst, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(), P->blk_cap,
-                             P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st, &bh));
+                             P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st, &bh,
+                             P->d_total.as<uint64_t>(), std::max<uint32_t>(1u, std::min(n, P->blk_cap))));
         T.end();
         // frame results, content xxh32 and EndMark checks (one launch)
         T.begin("dec_close");
