@@ -233,7 +233,7 @@ KERNEL_SYMBOL = {"enc_parse": "k_enc_parse", "enc_emit": "k_enc_emit",
 
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/rNN/traffic.json, made by tools_traffic.sh from this same bench command:
+    (profiles/rNN/traffic.json, made by tools/traffic.sh from this same bench command:
     FETCH_SIZE and WRITE_SIZE in separate --pmc passes, per-dispatch averages in KB).
     FETCH_SIZE is doubled: on gfx950 it counts half the bytes of 16-B/lane streaming reads."""
     import glob
@@ -397,6 +397,9 @@ def run_rank(args):
                              else f"config2: {nb} x 64 KiB log-text blocks per GPU") + ", LZ4 frame encode + decode, device-resident",
                 "blocks_per_gpu": nb, "block_bytes": block, "frame": "FLG 0x64 BD 0x40 (lz4_flex Auto), xxh32 content checksum",
                 "compression_ratio": round(comp_bytes / (nb * block), 4), "parallelism": f"shard{world}",
+                "decode_plan": "built before timing from the frame offsets/lengths the encoder wrote (read back once: "
+                               "they are the same every step); the plan's frame walk (headers, block table, units) "
+                               "runs on the device inside every timed step",
             },
             "per_gpu_gibps": [round(x, 3) for x in rates],
             "blocks_checked": int(checked_all),
