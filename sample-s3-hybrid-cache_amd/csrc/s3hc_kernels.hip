@@ -1632,11 +1632,24 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             vm[q] = __builtin_amdgcn_alignbyte(w0, wp, sh);    // bytes [P-4, P)
             vm8[q] = __builtin_amdgcn_alignbyte(wp, wpp, sh);  // bytes [P-8, P-4)
             const uint32_t h = hash4(vv[q]);
-            cc[q] = tbl[h];
-            tbl[P < sb_end ? h : kTbl] = (uint16_t)i;
-            if (kPS == 2) {  // (i even: sh + 1 <= 3) the lane's second position, inserted after the first
+            if (kPS == 1) {
+                cc[q] = tbl[h];
+                tbl[P < sb_end ? h : kTbl] = (uint16_t)i;
+            } else {
+                // (i even: sh + 1 <= 3) the lane's second position is inserted after the first; the
+                // two half-waves (64 positions each) read and insert one after the other, so a
+                // probe sees every position before its own 64 (as with one position per lane)
                 const uint32_t h1 = hash4(__builtin_amdgcn_alignbyte(w1, w0, sh + 1));
-                tbl[P + 1 < sb_end ? h1 : kTbl] = (uint16_t)(i + 1);
+                const uint32_t t0 = P < sb_end ? h : kTbl, t1 = P + 1 < sb_end ? h1 : kTbl;
+#pragma unroll
+                for (uint32_t half = 0; half < 2; ++half) {
+                    if (((uint32_t)lane >> 5) == half) {
+                        cc[q] = tbl[h];
+                        tbl[t0] = (uint16_t)i;
+                        tbl[t1] = (uint16_t)(i + 1);
+                    }
+                    wave_sync();
+                }
             }
         }
         // ---- B: verify + measure both candidates (table: one LDS round trip; distance 1..4:
