@@ -11,7 +11,7 @@ CHILD = r'''
 import os, sys, time
 sys.path[:0] = [os.path.join(%r, "sample-s3-hybrid-cache_amd")]
 import s3hc_lz4 as S, synth
-nb, block = 4096, 65536
+nb, block = int(os.environ.get("FX_BLOCKS", "4096")), 65536
 eng = S.Engine(0)
 data = synth.log_text(nb * block, synth.SEED_BASE + 1)
 offs = [i * block for i in range(nb)]
