@@ -54,6 +54,7 @@ constexpr uint32_t DEAD = 0xFFFFFFFFu;         // malformed token (or a walk tha
 constexpr uint32_t kOvfCap = 4096;             // hops a walk past its segment may take before giving up
 constexpr uint32_t kLv = kTT == 512 ? 9 : 8;   // doubling levels: chains over <= kTT segments
 static_assert(kTT == 256 || kTT == 512, "k_dtok: 4 or 8 waves");
+static_assert(kBitW <= 4 * 256, "k_dtok: four bitmap words per thread cover the block");
 constexpr uint32_t kTermEnd = kTT, kTermBad = kTT + 1;
 constexpr uint32_t kMEnd = 0xFFFEu, kMBad = 0xFFFFu;  // u16 merge codes (positions are < kMaxC)
 }  // namespace fst
@@ -338,8 +339,28 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
     __syncthreads();
     const bool ok = !sflag[1] && Utot <= B.limit && Utot <= B.cap;
     if (ok) {
-        uint32_t* gb = a.bmp + (size_t)u * kBitW;
-        for (uint32_t k = g; k < (C + 31u) / 32u; k += kTT) gb[k] = bits[k];
+        // the token positions in order (k_dexec reads 64 per window): each thread expands four
+        // consecutive bitmap words at its scanned rank
+        const uint32_t nbw = (C + 31u) / 32u;
+        uint32_t wv[4], cnt = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t k = 4u * g + j;
+            wv[j] = k < nbw ? bits[k] : 0u;
+            cnt += (uint32_t)__builtin_popcount(wv[j]);
+        }
+        uint32_t tot;
+        uint32_t r = wg_excl_scan<kTT / 64>(cnt, scr, &tot);
+        uint16_t* tk = a.tok + (size_t)u * kFastMaxTok;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            uint32_t x = wv[j];
+            const uint32_t wb = (4u * g + j) << 5;
+            while (x) {
+                tk[r++] = (uint16_t)(wb + (uint32_t)__builtin_ctz(x));
+                x &= x - 1u;
+            }
+        }
     }
     if (g == 0) {
         if (ok) {
@@ -407,7 +428,6 @@ constexpr uint32_t kORW = kOR / 4;
 constexpr uint32_t kORM = kOR - 1;
 constexpr uint32_t kWin = 2048;      // output bytes of one batch, at most
 constexpr uint32_t kFl = 1024;       // flush granule
-constexpr uint32_t kQ = 256;         // token queue entries (window w+3 plus one 16-word refill)
 constexpr uint32_t kGD = 4;          // pending-match dwords per lane held in registers
 constexpr uint32_t kGW = 64 * kGD;
 static_assert(2 * kWin + kFl <= kOR, "far sources of a batch must be flushed before it runs");
@@ -670,7 +690,6 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                                            const FastArgs& a) {
     using namespace fst;
     __shared__ __attribute__((aligned(16))) uint32_t ring[kORW];
-    __shared__ uint16_t tq[kQ];              // token positions, queue entry t = token t
     __shared__ uint4 pinfo[64];              // pending matches: md, ms, ml | off << 16, first dword - rank
     __shared__ uint8_t gmk[kGW];             // pending dwords: rank of each lane's first dword -> lane + 1
     if (!a.unit_fast[u]) return;
@@ -680,8 +699,8 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
     const FastUnit F = a.fu[u];
     const uint8_t* in = src + B.src_off;
     uint8_t* out = dst + B.dst_off;
-    const uint32_t* bm = a.bmp + (size_t)u * kBitW;
-    const uint32_t N = F.ntok, C = B.csize, nbw = (C + 31u) >> 5;
+    const uint16_t* tk = a.tok + (size_t)u * kFastMaxTok;
+    const uint32_t N = F.ntok, C = B.csize;
     uint32_t upos = 0, flushed = 0;
     auto flush_full = [&]() {
         while (upos - flushed >= kFl) {
@@ -689,46 +708,20 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
             flushed += kFl;
         }
     };
-    // ---- token queue: the bitmap expanded 16 words at a time (the next 16 prefetched)
-    uint32_t qfill = 0, bw = 0;
-    uint32_t bword = lane < 16u && lane < nbw ? bm[lane] : 0u;
-    auto refill = [&](uint32_t want) {
-        while (qfill < want && bw < nbw) {
-            const uint32_t word = bword;
-            const uint32_t wbase = (bw + lane) << 5;
-            bw += 16;
-            bword = lane < 16u && bw + lane < nbw ? bm[bw + lane] : 0u;
-            const uint32_t pc = (uint32_t)__builtin_popcount(word);
-            const uint32_t incl = incl_scan(pc, lane);
-            uint32_t k = qfill + incl - pc, wv = word;
-            while (wv) {
-                const uint32_t b = (uint32_t)__builtin_ctz(wv);
-                tq[k & (kQ - 1)] = (uint16_t)(wbase + b);
-                ++k;
-                wv &= wv - 1u;
-            }
-            qfill += rdlane(incl, 15);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
     const uint32_t nwin = (N + 63u) >> 6;
     auto tpos = [&](uint32_t w) -> uint32_t {  // my token's position in window w (or C: none)
         const uint32_t t = 64u * w + lane;
-        return t < N ? (uint32_t)tq[t & (kQ - 1)] : C;
+        const uint32_t v = tk[t < N ? t : N - 1u];  // (unconditional load)
+        return t < N ? v : C;
     };
     auto ld_w0 = [&](uint32_t pos) -> uint32_t { return gld4(in + umin_(pos, C)); };
     // ---- pipeline prologue: window 2's token dword, window 1's offset dword, window 0 decoded
-    // (the queue holds one window plus one refill: windows 0..2 are read as they arrive)
-    refill(64u);
     const uint32_t pos_0 = tpos(0);
-    uint32_t w0_c = ld_w0(pos_0);
-    refill(128u);
     uint32_t pos_n = tpos(1);
-    uint32_t w0_n = ld_w0(pos_n);
-    refill(192u);
     uint32_t pos_2 = tpos(2);
+    uint32_t pos_3r = tpos(3);  // window w + 3's positions, read one window ahead of their use
+    uint32_t w0_c = ld_w0(pos_0);
+    uint32_t w0_n = ld_w0(pos_n);
     uint32_t w0_2 = ld_w0(pos_2);
     // window 0: token + offset dwords now
     SeqF fc, fn;
@@ -773,9 +766,10 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
         const uint32_t nact = umin_(64u, N - 64u * w);
         const bool act = lane < nact;
         // ---- stage A: window w+3's token dword (loads are unconditional: a lane without a
-        // token reads a harmless in-frame address, so no branch forces an early wait)
-        refill(64u * (w + 4u));
-        const uint32_t pos_3 = w + 3 < nwin ? tpos(w + 3) : C;
+        // token reads a harmless in-frame address, so no branch forces an early wait) and
+        // window w+4's token positions
+        const uint32_t pos_3 = pos_3r;
+        pos_3r = tpos(w + 4);
         const uint32_t w0_3 = gld4(in + pos_3);
         // ---- stage B: window w+2's offset dword
         uint32_t mp_2;

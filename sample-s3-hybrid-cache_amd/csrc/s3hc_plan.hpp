@@ -184,6 +184,9 @@ struct LbArgs {
 // Blocks it does not take (stored, > kFastMaxC compressed bytes, multi-block units, anything
 // malformed or out of bounds) go to the per-unit decoder, which also reports their exact status.
 constexpr uint32_t kFastMaxC = 32768;  // compressed bytes of a block the fast path takes
+// tokens of such a block: every sequence but the last has a token and a 2-byte offset, the last
+// a token and >= 1 literal, so N <= (C - 1) / 3 + 1 (rounded up to whole 64-token windows)
+constexpr uint32_t kFastMaxTok = ((kFastMaxC - 1) / 3 + 1 + 63) / 64 * 64;
 
 struct FastUnit {        // 16 bytes, written by k_dtok for every unit it takes
     uint32_t ntok;       // sequences (the last one has no match)
@@ -192,7 +195,7 @@ struct FastUnit {        // 16 bytes, written by k_dtok for every unit it takes
 };
 
 struct FastArgs {
-    uint32_t* bmp;       // per unit, kFastMaxC / 32 words: bit p = a token starts at block byte p
+    uint16_t* tok;       // per unit, kFastMaxTok entries: the block's token positions in order
     FastUnit* fu;        // per unit
     uint8_t* unit_fast;  // per unit: 1 = decoded by the fast path
 };

@@ -371,17 +371,17 @@ struct LbScratch {
         seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst, blk_hash, wbase, wtile0, wP, tpend, tinit;
     LbArgs a{};
     // 64 KiB-block fast path (s3hc_fast.hip): per-unit token bitmaps and results
-    DevBuf f_bmp, f_fu, f_unit_fast;
+    DevBuf f_bmp, f_fu, f_unit_fast;  // (f_bmp: token positions)
     FastArgs fa{};
     bool fast_ready = false;
     hipError_t prepare_fast(uint32_t nunits) {
         fast_ready = false;
         if (!nunits) return hipSuccess;
         hipError_t e;
-        if ((e = f_bmp.ensure((size_t)nunits * (kFastMaxC / 8) + 64)) != hipSuccess) return e;
+        if ((e = f_bmp.ensure((size_t)nunits * kFastMaxTok * sizeof(uint16_t) + 64)) != hipSuccess) return e;
         if ((e = f_fu.ensure((size_t)nunits * sizeof(FastUnit) + 64)) != hipSuccess) return e;
         if ((e = f_unit_fast.ensure((size_t)nunits + 64)) != hipSuccess) return e;
-        fa.bmp = f_bmp.as<uint32_t>();
+        fa.tok = f_bmp.as<uint16_t>();
         fa.fu = f_fu.as<FastUnit>();
         fa.unit_fast = f_unit_fast.as<uint8_t>();
         fast_ready = true;
