@@ -277,3 +277,54 @@ def test_fast_path_device_batch_corruption(engine, oracle):
         assert ost[i] == want_st, i
         if want_st == 0:
             assert out.read(BLOCK, i * BLOCK) == want
+
+
+def _raw_frame(block: bytes, out: bytes) -> bytes:
+    # one independent BD 0x40 block, content checksum (lz4_flex's frame layout, compression.rs:539-557)
+    import xxhash
+
+    hdr = bytes([0x64, 0x40])
+    hc = (xxhash.xxh32(hdr, seed=0).intdigest() >> 8) & 0xFF
+    return (b"\x04\x22\x4d\x18" + hdr + bytes([hc]) + len(block).to_bytes(4, "little") + block +
+            b"\x00\x00\x00\x00" + xxhash.xxh32(out, seed=0).intdigest().to_bytes(4, "little"))
+
+
+def _densest_block(c_target: int, lit: int = 5):
+    # as many sequences as a block of c_target bytes can hold: after one literal, every sequence is
+    # a bare token + offset 1 (3 bytes, 4 output bytes), then a literal-only last sequence
+    n = (c_target - 2 - 1 - (1 + lit)) // 3
+    blk = bytearray(b"\x10a")  # token: 1 literal, match 4; literal 'a'
+    blk += b"\x01\x00"         # offset 1
+    blk += b"\x00\x01\x00" * n
+    blk += bytes([lit << 4]) + b"b" * lit
+    out = b"a" * (1 + 4 * (n + 1)) + b"b" * lit
+    return bytes(blk), out, n + 2
+
+
+def test_fast_path_densest_token_blocks(engine, oracle):
+    # the token-position list at its bound (kFastMaxTok: N <= (C - 1) / 3 + 1 for C <= 32 KiB),
+    # through the fast path and the per-unit decoder, single calls and one batch
+    items = []
+    for c in (32768, 32767, 32766, 32000, 4096, 100, 12):
+        blk, out, ntok = _densest_block(c)
+        assert len(blk) <= 32768 and ntok <= (len(blk) - 1) // 3 + 1
+        f = _raw_frame(blk, out)
+        assert oracle.decompress_data(f) == out
+        assert _fast(lambda: engine.decompress_frames(f)) == out
+        assert _slow(lambda: engine.decompress_frames(f)) == out
+        items.append((f, out))
+    blob = b"".join(f for f, _ in items)
+    fo, fl, offs, caps = [], [], [], []
+    p = o = 0
+    for f, d in items:
+        fo.append(p)
+        fl.append(len(f))
+        offs.append(o)
+        caps.append(BLOCK)
+        p += len(f)
+        o += BLOCK
+    d_blob = engine.upload(blob)
+    out, olen, ost = _decode_batch(engine, d_blob, fo, fl, offs, caps)
+    for i, (f, d) in enumerate(items):
+        assert ost[i] == 0 and olen[i] == len(d), i
+        assert out.read(len(d), offs[i]) == d, i
