@@ -49,11 +49,14 @@ def run(eng, frames_h, ctot, total_u, out_h, bb, depth, bmax=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, default=512)
+    ap.add_argument("--only", default="")
     a = ap.parse_args()
     eng = S.Engine(0)
     data = synth.log_text(a.mib << 20, 7)
     res = {}
     for name, item, pol in (("64KiB_frames", 65536, 0), ("ref_1MiB_frames", 1 << 20, 0)):
+        if a.only and a.only not in name:
+            continue
         fr = b"".join(eng.compress_frame(data[i:i + item], pol) for i in range(0, len(data), item))
         h_fr = eng.host_alloc(len(fr))
         h_fr.view()[:] = np.frombuffer(fr, dtype=np.uint8)
