@@ -824,7 +824,26 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
             }
             if (S3HC_FXOR && !(S3HC_FXSKIP & 8)) ring_clear(ring, upos, S_c, lane);
             wsync();
-            if (!(S3HC_FXSKIP & 2) && act && ll) wr16(ring, d0, lit0_c, umin_(16u, ll));
+            if (!(S3HC_FXSKIP & 2)) {
+                // first literal chunk as 16 plain byte stores, last byte first: bytes past a
+                // lane's literals land in its own match or in later lanes' bytes, which are
+                // all stored after them (later lanes' first chunks by a later store of this
+                // sequence; matches and further chunks after it); lanes whose chunk would wrap
+                // the ring or pass the window's end take the masked write
+                const uint32_t A0 = d0 & kORM;
+                const bool bytew = !S3HC_FXOR && act && ll && A0 + 16u <= kOR && d0 + 16u <= upos + S_c;
+                if (bytew) {
+                    uint8_t* rb = (uint8_t*)ring + A0;
+                    const uint32_t x[4] = {lit0_c.x, lit0_c.y, lit0_c.z, lit0_c.w};
+#pragma unroll
+                    for (int k = 15; k >= 0; --k) {
+                        rb[k] = (uint8_t)(x[k >> 2] >> (8 * (k & 3)));
+                        __builtin_amdgcn_sched_barrier(0);  // (the stores' order is the contract)
+                    }
+                }
+                asm volatile("" ::: "memory");
+                if (act && ll && !bytew) wr16(ring, d0, lit0_c, umin_(16u, ll));
+            }
             if (!(S3HC_FXSKIP & 2) && act && ll > 16u) wr16(ring, d0 + 16u, lit1_c, umin_(16u, ll - 16u));
             for (uint32_t c = 32; __ballot(act && c < ll); c += 16u)
                 if (act && c < ll) wr16(ring, d0 + c, gld16_blk(in, lit + c, C), umin_(16u, ll - c));
