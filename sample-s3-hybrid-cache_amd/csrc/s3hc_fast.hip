@@ -668,22 +668,6 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t x, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
 }
 
-// One output dword (ring dword index d, bytes of mask m) of an overlapping match (P = md, ms,
-// ml | off << 16): byte b copies the byte ((b - md) mod off) into the match's first period.
-__device__ uint32_t periodic_dword(const uint32_t* ring, uint4 P, uint32_t d, uint32_t m) {
-    const uint32_t md = P.x, ms = P.y, off = P.z >> 16;
-    const uint8_t* rb = (const uint8_t*)ring;
-    uint32_t v = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) {
-        if ((m >> (8u * j)) & 0xFFu) {
-            const uint32_t e = 4u * d + j - md;
-            v |= (uint32_t)rb[(ms + e % off) & fst::kORM] << (8u * j);
-        }
-    }
-    return v;
-}
-
 __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                            const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
                                            uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
@@ -930,7 +914,27 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                             gd[i] = d;
                             gm[i] = (hi >= 4u ? ~0u : (1u << (8u * hi)) - 1u) & (~0u << (8u * lo));
                             ga[i] = P.y + b0 - pmd;  // source of the dword's byte 0 (non-overlapping)
-                            go[i] = (P.z >> 16) < pml ? own : 0u;  // overlapping: periodic sources
+                            const uint32_t poff = P.z >> 16;
+                            if (poff < pml) {
+                                // overlapping: byte b copies the byte (b - md) mod off into the
+                                // match's first period; the four ring indices, found once here
+                                // (one division) instead of in every sweep
+                                const int32_t e0 = (int32_t)b0 - (int32_t)pmd;
+                                const uint32_t base = e0 > 0 ? (uint32_t)e0 : 0u;
+                                const uint32_t rr = base % poff;
+                                uint32_t sx[4];
+#pragma unroll
+                                for (uint32_t q = 0; q < 4u; ++q) {
+                                    const int32_t e = e0 + (int32_t)q;
+                                    uint32_t x = e > 0 ? rr + ((uint32_t)e - base) : 0u;
+                                    x = poff == 1u ? 0u : x;
+                                    x -= x >= poff ? poff : 0u;
+                                    x -= x >= poff ? poff : 0u;
+                                    sx[q] = (P.y + x) & kORM;
+                                }
+                                ga[i] = sx[0] | (sx[1] << 16);
+                                go[i] = sx[2] | (sx[3] << 16) | 0x80000000u;  // (ring indices < 2^13)
+                            }
                         }
                     }
                     // slot by slot: a slot's dwords only read lower addresses (earlier slots, already
@@ -951,7 +955,10 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                                 v = __builtin_amdgcn_alignbyte(ring[((A >> 2) + 1u) & (kORW - 1)],
                                                                ring[(A >> 2) & (kORW - 1)], A & 3u);
                             } else {
-                                v = periodic_dword(ring, pinfo[go[i] - 1u], gd[i], gm[i]);
+                                const uint8_t* rb = (const uint8_t*)ring;
+                                const uint32_t A = ga[i], Bq = go[i];
+                                v = (uint32_t)rb[A & 0xFFFFu] | ((uint32_t)rb[A >> 16] << 8) |
+                                    ((uint32_t)rb[Bq & 0x7FFFu] << 16) | ((uint32_t)rb[(Bq >> 16) & 0x7FFFu] << 24);
                             }
                             if (((cur ^ v) & gm[i]) != 0u) {
                                 chg = true;
