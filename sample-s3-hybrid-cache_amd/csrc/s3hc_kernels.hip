@@ -1982,6 +1982,31 @@ __global__ __launch_bounds__(256) void k_enc_emit(const uint8_t* __restrict__ sr
             const uint32_t ipos = in_pos + wave_excl_scan(act ? ll + ml : 0u, lane);
             const uint32_t tot = rdl(opos + sz, 63) - ob_len;                 // this group's bytes
             const uint32_t itot = rdl(ipos + (act ? ll + ml : 0u), 63) - in_pos;
+            // literal runs of <= 48 bytes first, as 16-byte chunks of plain byte stores: last
+            // chunk first, last byte first, so bytes past a lane's run (its offset and length
+            // bytes, or later lanes' bytes) are always stored again after them (the record
+            // bytes below; a later lane's chunk by a later store); longer runs are copied
+            // wave-wide after the records
+            const uint32_t lw = opos + hsz;  // my literals' position in ob
+            const uint32_t nck = act && ll <= 48 ? (ll + 15u) >> 4 : 0u;
+#pragma unroll
+            for (int kc = 2; kc >= 0; --kc) {
+                if (!__ballot(nck > (uint32_t)kc)) continue;
+                if (nck > (uint32_t)kc) {
+                    const uint32_t si = ipos + 16u * (uint32_t)kc, sa = si >> 2, sh = si & 3u;
+                    const uint32_t* iw = (const uint32_t*)ib;
+                    const uint32_t d0 = iw[sa], d1 = iw[sa + 1], d2 = iw[sa + 2], d3 = iw[sa + 3], d4 = iw[sa + 4];
+                    const uint32_t x[4] = {__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                                           __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh)};
+                    uint8_t* dp = ob + lw + 16u * (uint32_t)kc;
+#pragma unroll
+                    for (int k = 15; k >= 0; --k) {
+                        dp[k] = (uint8_t)(x[k >> 2] >> (8 * (k & 3)));
+                        __builtin_amdgcn_sched_barrier(0);  // (the stores' order is the contract)
+                    }
+                }
+            }
+            wave_sync();
             if (act) {
                 uint32_t w = opos;
                 if (j != 0) {
@@ -1992,9 +2017,6 @@ __global__ __launch_bounds__(256) void k_enc_emit(const uint8_t* __restrict__ sr
                         while (x >= 255) { ob[w++] = 255; x -= 255; }
                         ob[w++] = (uint8_t)x;
                     }
-                }
-                if (ll <= 48) {
-                    for (uint32_t t = 0; t < ll; ++t) ob[w + t] = ib[ipos + t];
                 }
                 w += ll;
                 ob[w++] = (uint8_t)off;
