@@ -808,6 +808,23 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
             }
             if (S3HC_FXOR && !(S3HC_FXSKIP & 8)) ring_clear(ring, upos, S_c, lane);
             wsync();
+            if (!(S3HC_FXSKIP & 2) && __ballot(act && ll > 16u)) {
+                // second chunk first (same rule as the first chunk below: its bytes past the
+                // run land in this lane's match or in later lanes' bytes, stored after them)
+                const uint32_t A1 = (d0 + 16u) & kORM;
+                const bool bytew2 = !S3HC_FXOR && act && ll > 16u && A1 + 16u <= kOR && d0 + 32u <= upos + S_c;
+                if (bytew2) {
+                    uint8_t* rb = (uint8_t*)ring + A1;
+                    const uint32_t x[4] = {lit1_c.x, lit1_c.y, lit1_c.z, lit1_c.w};
+#pragma unroll
+                    for (int k = 15; k >= 0; --k) {
+                        rb[k] = (uint8_t)(x[k >> 2] >> (8 * (k & 3)));
+                        __builtin_amdgcn_sched_barrier(0);  // (the stores' order is the contract)
+                    }
+                }
+                asm volatile("" ::: "memory");
+                if (act && ll > 16u && !bytew2) wr16(ring, d0 + 16u, lit1_c, umin_(16u, ll - 16u));
+            }
             if (!(S3HC_FXSKIP & 2)) {
                 // first literal chunk as 16 plain byte stores, last byte first: bytes past a
                 // lane's literals land in its own match or in later lanes' bytes, which are
@@ -828,7 +845,6 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                 asm volatile("" ::: "memory");
                 if (act && ll && !bytew) wr16(ring, d0, lit0_c, umin_(16u, ll));
             }
-            if (!(S3HC_FXSKIP & 2) && act && ll > 16u) wr16(ring, d0 + 16u, lit1_c, umin_(16u, ll - 16u));
             for (uint32_t c = 32; __ballot(act && c < ll); c += 16u)
                 if (act && c < ll) wr16(ring, d0 + c, gld16_blk(in, lit + c, C), umin_(16u, ll - c));
 #ifdef FPROF
