@@ -167,6 +167,40 @@ __device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* scratch, 
     __syncthreads();
     return before + x - v;
 }
+// two exclusive scans over the workgroup at once (one scratch exchange, two barriers)
+template <uint32_t NW>
+__device__ __forceinline__ void wg_excl_scan2(uint32_t v, uint32_t u, uint32_t* scratch, uint32_t* ev, uint32_t* eu,
+                                              uint32_t* tv, uint32_t* tu) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    uint32_t x = v, y = u;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t a = (uint32_t)__shfl_up((int)x, d, 64), b = (uint32_t)__shfl_up((int)y, d, 64);
+        if (lane >= d) {
+            x += a;
+            y += b;
+        }
+    }
+    if (lane == 63) {
+        scratch[2 * w] = x;
+        scratch[2 * w + 1] = y;
+    }
+    __syncthreads();
+    uint32_t bx = 0, by = 0, ax = 0, ay = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NW; ++k) {
+        const uint32_t sx = scratch[2 * k], sy = scratch[2 * k + 1];
+        bx += k < w ? sx : 0u;
+        by += k < w ? sy : 0u;
+        ax += sx;
+        ay += sy;
+    }
+    *tv = ax;
+    *tu = ay;
+    *ev = bx + x - v;
+    *eu = by + y - u;
+    __syncthreads();
+}
 }  // namespace
 
 // ------------------------------------------------------------------ k_dtok
@@ -179,7 +213,7 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
     __shared__ uint16_t svfrom[kTT];   // per segment on the true chain: its first true token (else M_BAD)
     __shared__ uint16_t J[2][kTT + 2]; // succ^(2^k) per segment, ping-pong; kTT / kTT + 1 are terminals
     __shared__ uint8_t reach[kTT + 2]; // segment is on the true chain
-    __shared__ uint32_t scr[8];
+    __shared__ uint32_t scr[16];
     __shared__ uint32_t sflag[4];      // [0] terminal of the chain, [1] failure, [2] pool base
     const uint32_t g = threadIdx.x;
     const DecUnit U = units[u];
@@ -332,8 +366,9 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
     }
     [[maybe_unused]] const uint64_t tp6 = FP_NOW();
     uint32_t Utot, N;
-    const uint32_t obase = wg_excl_scan<kTT / 64>(o, scr, &Utot);
-    (void)wg_excl_scan<kTT / 64>(ntok, scr, &N);
+    uint32_t obase, tbase;
+    wg_excl_scan2<kTT / 64>(o, ntok, scr, &obase, &tbase, &Utot, &N);
+    (void)tbase;
     const bool fail = bad || (valid && (int64_t)obase + minsl < 0);
     if (fail) sflag[1] = 1u;
     __syncthreads();
