@@ -601,3 +601,38 @@ def test_host_calls_large_and_pinned_buffers(engine, oracle, mib, policy):
     assert rc == 0 and bytes(h_dst.view()[:n.value]) == frame
     for h in (h_in, h_out, h_src, h_dst):
         h.free()
+
+
+def test_encoder_literal_runs_of_every_length(engine, oracle):
+    # the emitter copies literal runs of <= 48 bytes as 16-byte chunks (last chunk and last byte
+    # first, the record bytes stored after them) and longer runs wave-wide: runs of every length
+    # 1..200 between repeated phrases, at every alignment, in single frames and one device batch,
+    # decoded by the oracle (decompress_data, compression.rs:463-502)
+    import random
+
+    rng = random.Random(2024)
+    phrase = b"GET /bucket/key-000042 HTTP/1.1 200 "
+    parts = []
+    for n in list(range(1, 201)) * 2:
+        parts.append(phrase[: 8 + (n % 29)])
+        parts.append(rng.randbytes(n))
+    data = b"".join(parts)
+    for off in (0, 1, 5, 15, 16, 17, 47, 48, 49):
+        d = data[off:]
+        f = engine.compress_frame(d)
+        assert oracle.decompress_data(f) == d, off
+        assert engine.decompress_frames(f) == d, off
+    blocks = [data[i:i + 65536] for i in range(0, len(data), 65536)]
+    blob = b"".join(blocks)
+    d_src = engine.upload(blob)
+    offs = [i * 65536 for i in range(len(blocks))]
+    lens = [len(b) for b in blocks]
+    plan = engine.plan_encode(offs, lens)
+    dst = engine.alloc(plan.dst_bound)
+    ioff, ilen = engine.alloc(8 * len(lens)), engine.alloc(4 * len(lens))
+    engine.encode_dev(plan, d_src, dst, ioff, ilen)
+    engine.sync()
+    fo, fl = ioff.u64(len(lens)), ilen.u32(len(lens))
+    raw = dst.read(fo[-1] + fl[-1])
+    for k, b in enumerate(blocks):
+        assert oracle.decompress_data(raw[fo[k]:fo[k] + fl[k]]) == b, k
