@@ -1954,7 +1954,14 @@ __global__ __launch_bounds__(256) void k_enc_emit(const uint8_t* __restrict__ sr
     uint32_t o = P.out_off;  // payload-relative write cursor
     if (S.nseq > 0) {
         const uint2* rr = recs + (size_t)s * kMaxSeqPerSeg;
-        const uint32_t ml0 = rr[0].x >> 16;
+        // the first four groups' records are loaded now, in flight with the input staging
+        // below (each group used to wait for its own records: one HBM round trip per group)
+        auto ldr = [&](uint32_t k) -> uint2 {
+            const uint32_t jk = 64u * k + (uint32_t)lane;
+            return rr[jk < S.nseq ? jk : 0u];
+        };
+        const uint2 pre0 = ldr(0), pre1 = ldr(1), pre2 = ldr(2), pre3 = ldr(3);
+        const uint32_t ml0 = rdl(pre0.x, 0) >> 16;
         // first token: literal run = carry bytes (earlier segments) + ll0 (this segment)
         const uint32_t lle = P.carry + S.ll0;
         const uint32_t ne = ext_bytes(lle);
@@ -1974,7 +1981,9 @@ __global__ __launch_bounds__(256) void k_enc_emit(const uint8_t* __restrict__ sr
         for (uint32_t g = 0; g < S.nseq; g += 64) {
             const uint32_t j = g + lane;
             const bool act = j < S.nseq;
-            const uint2 r = act ? rr[j] : make_uint2(0, 0);
+            uint2 r = g == 0 ? pre0 : (g == 64 ? pre1 : (g == 128 ? pre2 : pre3));
+            if (g >= 256u) r = act ? rr[j] : make_uint2(0, 0);
+            if (!act) r = make_uint2(0, 0);
             const uint32_t ll = r.x & 0xFFFFu, ml = r.x >> 16, off = r.y;
             const uint32_t hsz = j == 0 ? 0u : 1 + ext_bytes(ll);
             const uint32_t sz = act ? hsz + ll + 2 + ext_bytes(ml - 4) : 0u;
