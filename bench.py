@@ -56,6 +56,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=1.0, help="wall seconds of each of the 5 CPU baseline runs")
     ap.add_argument("--selftest", action="store_true",
                     help="launcher/rank plumbing only (no GPU): every rank reports in, rank 0 prints the summary")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal only: allow more ranks than visible GPUs (ranks then share devices; "
+                         "the line says so). Without it, N ranks on fewer than N devices are refused")
     return ap.parse_args(argv)
 
 
@@ -220,6 +223,21 @@ def cpu_baseline(data_chunk: bytes, block: int, seconds: float):
     }
 
 
+# ------------------------------------------------------------------ device assignment
+def assign_device(world: int, local: int, ndev: int, share: bool):
+    """(device index, None) for this rank, or (None, reason) when the run must be refused: N ranks
+    on fewer than N visible devices would report N "GPUs" that are fewer GPUs (one process per
+    GPU). --share-gpu makes it an explicit rehearsal instead."""
+    if ndev <= 0:
+        return None, "no visible GPU"
+    if world > ndev and not share:
+        return None, (f"{world} ranks but only {ndev} visible GPU(s): refusing to report {world} GPUs "
+                      f"(pass --share-gpu for a shared-device rehearsal)")
+    if local >= ndev and not share:
+        return None, f"LOCAL_RANK {local} has no GPU of its own ({ndev} visible)"
+    return local % ndev, None
+
+
 # ------------------------------------------------------------------ the GPU bench (one rank)
 # decode: the fast path's token index + executor (k_dtok + k_dexec; k_decode_pe then only exits for
 # the units they took), or with S3HC_FAST=0 / S3HC_FAST_DISABLE the parser + executor kernel
@@ -266,6 +284,36 @@ def roofline_obj(kt, name, alg_bytes, profiled_shape: bool):
     return roof
 
 
+DECODE_PHASES = ("dec_plan", "decode", "dec_close")
+KERNEL_SYMBOL["dec_plan"] = "k_dframe_count+k_scan_u32_u64+k_dframe_fill"
+
+
+def roofline_whole_decode(kt, alg_bytes, profiled_shape: bool):
+    """(C + U) per step over the summed average time of the decode's three phases (frame walk,
+    block decode, verify), one event pair each on the launch stream."""
+    parts = [p for p in DECODE_PHASES if p in kt]
+    ms = sum(kt[p][0] / kt[p][1] for p in parts)
+    achieved = alg_bytes / (ms / 1e3) / 1e9
+    traffic, tsrc = None, None
+    if profiled_shape:
+        tot = 0
+        for p in parts:
+            t, tsrc = pmc_traffic(p)
+            if t is None:
+                tot = None
+                break
+            tot += t
+        traffic = tot
+    roof = {
+        "bound": "hbm", "kernel": "+".join(KERNEL_SYMBOL.get(p, p) for p in parts), "phases": parts,
+        "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+        "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(ms, 4),
+    }
+    if traffic is not None and tsrc:
+        roof["traffic_source"] = tsrc + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same bench command)"
+    return roof
+
+
 def chunk_seed(rank: int, c: int) -> int:
     import synth
     return synth.SEED_BASE + 1 + 1000 * rank + 7919 * c
@@ -276,6 +324,13 @@ def run_rank(args):
     import shard
     import synth
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    ndev = S.device_count()
+    dev, why = assign_device(world, local, ndev, args.share_gpu)
+    if dev is None:  # before any collective: the launcher kills the other ranks
+        sys.stderr.write(f"bench.py: {why}\n")
+        sys.exit(2)
     g = shard.Group()
     world, rank, local = g.world, g.rank, g.local
     block = 65536
@@ -284,7 +339,7 @@ def run_rank(args):
         nb = hi - lo
     else:
         nb = args.blocks
-    eng = S.Engine(local % max(1, S.device_count()))  # one process per GPU (shared GPU only in 1-GPU rehearsals)
+    eng = S.Engine(dev)  # one process per GPU (devices shared only with --share-gpu)
 
     # ---- synthetic batch (distinct content, 256 MiB chunks), resident in HBM before timing
     nchunks = -(-nb // CHUNK_BLOCKS)
@@ -364,16 +419,21 @@ def run_rank(args):
     dom = max(excl, key=lambda k: excl[k][0]) if excl else None
     prof = nb == 4096 and not args.total_blocks
     roof = roofline_obj(kt, dom, alg.get(dom, nb * block), prof) if dom else None
-    roof_dec = roofline_obj(kt, "decode", alg["decode"], prof) if "decode" in kt else None
+    # north_star decode figure over the whole decode the reference does in one FrameDecoder pass
+    # (compression.rs:479-480): the plan's device frame walk, the block decode and the content
+    # xxh32 verify + EndMark checks; the block-decode kernels alone are the extra key
+    roof_dec = roofline_whole_decode(kt, alg["decode"], prof) if "decode" in kt else None
+    roof_dec_k = roofline_obj(kt, "decode", alg["decode"], prof) if "decode" in kt else None
     per_kernel = {k: round(v[0] / args.steps, 4) for k, v in kt.items()}
     rank_rate = nb * block * args.steps / (t1 - t0) / GiB
-    rates = [rank_rate]
+    rates, devs = [rank_rate], [dev]
     if g.dist is not None:
         import torch
-        t = torch.tensor([rank_rate], dtype=torch.float64)
-        lst = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        t = torch.tensor([rank_rate, float(dev)], dtype=torch.float64)
+        lst = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
         g.dist.all_gather(lst, t)
-        rates = [float(x.item()) for x in lst]
+        rates = [float(x[0].item()) for x in lst]
+        devs = [int(x[1].item()) for x in lst]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(first_chunk, block, args.cpu_seconds)
@@ -402,10 +462,12 @@ def run_rank(args):
                                "runs on the device inside every timed step",
             },
             "per_gpu_gibps": [round(x, 3) for x in rates],
+            "devices": {"visible": ndev, "rank_device": devs, "shared": len(set(devs)) < len(devs)},
             "blocks_checked": int(checked_all),
             "kernel_ms_per_step": per_kernel,
             "roofline": roof,
             "roofline_decode": roof_dec,
+            "roofline_decode_kernels": roof_dec_k,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

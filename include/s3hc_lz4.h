@@ -54,6 +54,14 @@ void s3hc_destroy(s3hc_ctx* ctx);
 const char* s3hc_last_error(void);
 const char* s3hc_version(void);
 
+/* Diagnostic / A-B switches (no reference counterpart: the reference has one codec). Read from
+ * the environment (S3HC_FAST_DISABLE, S3HC_FAST, S3HC_LB_DISABLE, S3HC_LBW_DISABLE, S3HC_LBW_CAP,
+ * S3HC_LBW_ROUNDS, S3HC_DEC_ONEWAVE, S3HC_FAST_TRACE, S3HC_LB_TRACE, S3HC_HOST_TRACE) once per
+ * process at the first s3hc_create; this call changes one afterwards (value NULL = default; a
+ * flag knob is on when its value is non-NULL, S3HC_FAST is on unless "0"). Process-wide. The
+ * per-call decode path only reads the cached values. S3HC_INVALID_ARG for an unknown name. */
+int s3hc_set_knob(const char* name, const char* value);
+
 /* Largest framed size any s3hc_compress_* call can produce for n input bytes. */
 size_t s3hc_frame_bound(size_t n);
 

@@ -386,7 +386,7 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
         }
         uint32_t tot;
         uint32_t r = wg_excl_scan<kTT / 64>(cnt, scr, &tot);
-        uint16_t* tk = a.tok + (size_t)u * kFastMaxTok;
+        uint16_t* tk = a.tok + B.tok;
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
             uint32_t x = wv[j];
@@ -718,7 +718,7 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
     const FastUnit F = a.fu[u];
     const uint8_t* in = src + B.src_off;
     uint8_t* out = dst + B.dst_off;
-    const uint16_t* tk = a.tok + (size_t)u * kFastMaxTok;
+    const uint16_t* tk = a.tok + B.tok;
     const uint32_t N = F.ntok, C = B.csize;
     uint32_t upos = 0, flushed = 0;
     auto flush_full = [&]() {

@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "s3hc_plan.hpp"
+#include "s3hc_knobs.hpp"
 #include "s3hc_lz4.h"
 
 namespace s3hc {
@@ -2153,7 +2154,7 @@ struct FrameWalk {
 };
 
 __device__ FrameWalk walk_frame(const uint8_t* f, uint32_t avail, DecBlock* out_blocks, uint64_t src_base,
-                                uint64_t dst_base, uint32_t dst_cap, uint32_t frame) {
+                                uint64_t dst_base, uint32_t dst_cap, uint32_t frame, uint64_t tok_base = 0) {
     FrameWalk r = {S3HC_OK, 0, 0, 0, 0, 0, 0, 0};
     if (avail < 4) { r.status = S3HC_CORRUPT; return r; }
     const uint32_t magic = rd32(f);
@@ -2198,6 +2199,7 @@ __device__ FrameWalk walk_frame(const uint8_t* f, uint32_t avail, DecBlock* out_
             D.cap = room < D.limit ? (uint32_t)room : D.limit;
             D.flags = ((w & kStoredBit) ? DB_STORED : 0u) | ((flg & 0x20) ? 0u : DB_LINKED);
             D.frame = frame;
+            D.tok = (uint32_t)(tok_base + ip / 3u);  // (tok_frame_entries: disjoint per block)
             out_blocks[k] = D;
         }
         ip += len + ((flg & 0x10) ? 4u : 0u);
@@ -2227,12 +2229,13 @@ __global__ void k_dframe_fill(const uint8_t* __restrict__ src, const uint64_t* _
                               const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
                               const uint64_t* __restrict__ blk_base, const int32_t* __restrict__ fstatus,
                               DecBlock* __restrict__ blocks, DecUnit* __restrict__ units,
-                              uint32_t* __restrict__ fwant) {
+                              uint32_t* __restrict__ fwant, const uint64_t* __restrict__ ftok) {
     const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
     if (fstatus[f] != S3HC_OK) return;
     const uint32_t b0 = (uint32_t)blk_base[f];
-    FrameWalk r = walk_frame(src + frame_off[f], frame_len[f], blocks + b0, frame_off[f], dst_off[f], dst_cap[f], f);
+    FrameWalk r = walk_frame(src + frame_off[f], frame_len[f], blocks + b0, frame_off[f], dst_off[f], dst_cap[f], f,
+                             ftok[f]);
     fwant[f] = r.want;
     const bool linked = !(r.flg & 0x20);
     for (uint32_t k = 0; k < r.nblk; ++k) {
@@ -2351,7 +2354,7 @@ hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock*
                                int32_t* blk_status, const uint8_t* unit_lb, const uint8_t* unit_fast, hipStream_t st) {
     if (!nunits || !grid) return hipSuccess;
     // S3HC_DEC_ONEWAVE=1 (comparisons): one wave per unit doing both halves (k_decode_units)
-    const bool onewave = getenv("S3HC_DEC_ONEWAVE") != nullptr;  // read per launch (tests toggle it)
+    const bool onewave = knob_on(KN_DEC_ONEWAVE);
     if (onewave)
         hipLaunchKernelGGL(k_decode_units, dim3(cdiv(grid, dec::kWaves)), dim3(64 * dec::kWaves), 0, st, src, dst,
                            blk, units, nunits, ucount, blk_out, blk_status, unit_lb, unit_fast);
@@ -2412,10 +2415,10 @@ hipError_t launch_dframe_count(const uint8_t* src, const uint64_t* frame_off, co
 hipError_t launch_dframe_fill(const uint8_t* src, const uint64_t* frame_off, const uint32_t* frame_len, uint32_t n,
                               const uint64_t* dst_off, const uint32_t* dst_cap, const uint64_t* blk_base,
                               const int32_t* fstatus, DecBlock* blocks, DecUnit* units, uint32_t* fwant,
-                              hipStream_t st) {
+                              const uint64_t* ftok, hipStream_t st) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_dframe_fill, dim3(cdiv(n, 256)), dim3(256), 0, st, src, frame_off, frame_len, n, dst_off,
-                       dst_cap, blk_base, fstatus, blocks, units, fwant);
+                       dst_cap, blk_base, fstatus, blocks, units, fwant, ftok);
     return hipGetLastError();
 }
 hipError_t launch_dframe_finish(const uint64_t* blk_base, uint32_t n, const uint32_t* nblk, const DecBlock* blocks,

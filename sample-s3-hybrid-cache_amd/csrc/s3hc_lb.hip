@@ -40,6 +40,7 @@
 
 #include "s3hc_lz4.h"
 #include "s3hc_plan.hpp"
+#include "s3hc_knobs.hpp"
 
 namespace s3hc {
 namespace lb {
@@ -1392,7 +1393,7 @@ hipError_t launch_lb_exec(const LbArgs& A, const uint8_t* src, uint8_t* dst, uin
         hipLaunchKernelGGL(k_lbw_init, dim3(tiles < 512u ? tiles : 512u), dim3(lb::kXT), 0, st, src, dst, A);
         // S3HC_LBW_ROUNDS (tests): fewer launches, so k_lbw_gather walks long chains itself
         uint32_t rounds = kLbwRounds;
-        if (const char* ev = getenv("S3HC_LBW_ROUNDS")) rounds = std::min<uint32_t>(rounds, (uint32_t)atoi(ev));
+        if (knob(KN_LBW_ROUNDS) >= 0) rounds = std::min<uint32_t>(rounds, (uint32_t)knob(KN_LBW_ROUNDS));
         for (uint32_t r = 0; r < rounds; ++r)
             hipLaunchKernelGGL(k_lbw_round, dim3(tiles < 512u ? tiles : 512u), dim3(lb::kXT), 0, st, A, r);
         hipLaunchKernelGGL(k_lbw_gather, dim3(tiles < 1024u ? tiles : 1024u), dim3(lb::kXT), 0, st, dst, A);

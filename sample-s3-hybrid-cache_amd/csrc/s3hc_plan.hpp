@@ -76,8 +76,17 @@ struct DecBlock {        // 40 bytes
     uint32_t cap;        // room in the caller's buffer at dst_off (more = DST_TOO_SMALL)
     uint32_t flags;      // DB_*
     uint32_t frame;      // owning frame
-    uint32_t pad;
+    uint32_t tok;        // 64 KiB fast path: first entry of this block's token-position slot in
+                         // FastArgs::tok (slots sized by compressed bytes: (csize - 1) / 3 + 1
+                         // entries, disjoint per block of a launch; see tok_slot_entries)
 };
+
+// Token-position slots of the fast path (s3hc_fast.hip): a block of c compressed bytes has at most
+// (c - 1) / 3 + 1 tokens. Device plans give frame f the entries [ftok[f], ftok[f] + len_f / 3 + 2)
+// and a block at byte ip of its frame the slot ftok[f] + ip / 3: blocks of a frame are >= 4 bytes
+// apart, so their slots are disjoint (floor(a/3) + floor((c-1)/3) + 1 <= floor((a + c + 2)/3)).
+inline uint64_t tok_frame_entries(uint64_t frame_len) { return frame_len / 3 + 2; }
+inline uint64_t tok_slot_entries(uint32_t csize) { return csize ? (uint64_t)(csize - 1) / 3 + 1 : 0; }
 
 struct DecUnit {         // a run of blocks decoded in order by one wave
     uint32_t first;
@@ -195,7 +204,7 @@ struct FastUnit {        // 16 bytes, written by k_dtok for every unit it takes
 };
 
 struct FastArgs {
-    uint16_t* tok;       // per unit, kFastMaxTok entries: the block's token positions in order
+    uint16_t* tok;       // per block, at DecBlock::tok: the block's token positions in order
     FastUnit* fu;        // per unit
     uint8_t* unit_fast;  // per unit: 1 = decoded by the fast path
 };

@@ -25,6 +25,7 @@
 #include "s3hc_lz4.h"
 #include "s3hc_plan.hpp"
 #include "s3hc_guard.hpp"
+#include "s3hc_knobs.hpp"
 
 namespace s3hc {
 hipError_t launch_xxh32(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, uint32_t*, hipStream_t);
@@ -55,7 +56,7 @@ hipError_t launch_dframe_count(const uint8_t*, const uint64_t*, const uint32_t*,
                                uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_dframe_fill(const uint8_t*, const uint64_t*, const uint32_t*, uint32_t, const uint64_t*,
                               const uint32_t*, const uint64_t*, const int32_t*, DecBlock*, DecUnit*, uint32_t*,
-                              hipStream_t);
+                              const uint64_t*, hipStream_t);
 hipError_t launch_dframe_finish(const uint64_t*, uint32_t, const uint32_t*, const DecBlock*, const uint32_t*,
                                 const int32_t*, int32_t*, uint32_t*, hipStream_t);
 hipError_t launch_dframe_verify(const uint8_t*, const uint64_t*, uint32_t, const uint32_t*, const uint32_t*,
@@ -374,11 +375,13 @@ struct LbScratch {
     DevBuf f_bmp, f_fu, f_unit_fast;  // (f_bmp: token positions)
     FastArgs fa{};
     bool fast_ready = false;
-    hipError_t prepare_fast(uint32_t nunits) {
+    // tok_entries: the launch's token-slot entries (DecBlock::tok + tok_slot_entries(csize) of
+    // every block stays below it; sized by compressed bytes, not by a per-unit maximum)
+    hipError_t prepare_fast(uint32_t nunits, uint64_t tok_entries) {
         fast_ready = false;
-        if (!nunits) return hipSuccess;
+        if (!nunits || tok_entries > 0xFFFFFFF0ull) return hipSuccess;  // (u32 slots: the fast path sits out)
         hipError_t e;
-        if ((e = f_bmp.ensure((size_t)nunits * kFastMaxTok * sizeof(uint16_t) + 64)) != hipSuccess) return e;
+        if ((e = f_bmp.ensure((size_t)tok_entries * sizeof(uint16_t) + 256)) != hipSuccess) return e;
         if ((e = f_fu.ensure((size_t)nunits * sizeof(FastUnit) + 64)) != hipSuccess) return e;
         if ((e = f_unit_fast.ensure((size_t)nunits + 64)) != hipSuccess) return e;
         fa.tok = f_bmp.as<uint16_t>();
@@ -408,9 +411,9 @@ struct LbScratch {
         // S3HC_LBW_CAP (positions, 0 = off; tests split a launch with it) replaces the size rule,
         // S3HC_LBW_DISABLE=1 turns it off
         uint64_t wcap = c.outb <= kLbwMaxOut ? c.outb : 0;
-        if (const char* ev = getenv("S3HC_LBW_CAP")) wcap = std::min<uint64_t>(c.outb, strtoull(ev, nullptr, 10));
+        if (knob(KN_LBW_CAP) >= 0) wcap = std::min<uint64_t>(c.outb, (uint64_t)knob(KN_LBW_CAP));
         // (a host walk knows its candidates: no spread launches that would find nothing to do)
-        if (getenv("S3HC_LBW_DISABLE") || (c.exact && (c.nbig == 0 || c.nbig > kLbwMaxBlocks))) wcap = 0;
+        if (knob_on(KN_LBW_DISABLE) || (c.exact && (c.nbig == 0 || c.nbig > kLbwMaxBlocks))) wcap = 0;
         wcap = std::min<uint64_t>(wcap, kLbwCapMax);
         const size_t tcap = wcap ? wcap / kLbStep + nlb + 1 : 0;
         if (wcap) {
@@ -443,15 +446,21 @@ struct LbScratch {
     }
 };
 
-// The 64 KiB-block fast path (s3hc_fast.hip) is opt-in while it is slower than the per-unit
-// decoder on config 2 (S3HC_FAST=1 enables it; S3HC_FAST_DISABLE=1 always wins).
-// The 64 KiB-block fast path (k_dtok + k_dexec) is on by default; S3HC_FAST=0 or
-// S3HC_FAST_DISABLE leave every unit to the per-unit decoder (A/B runs, parity tests).
-static bool fast_path_enabled() {
-    if (getenv("S3HC_FAST_DISABLE")) return false;
-    const char* e = getenv("S3HC_FAST");
-    return !(e && e[0] == '0');
+// Token-position slots of host-built block tables: consecutive per block, sized by compressed
+// bytes (s3hc_plan.hpp tok_slot_entries). Returns the launch's entries.
+static uint64_t assign_tok_slots(DecBlock* b, size_t n) {
+    uint64_t t = 0;
+    for (size_t i = 0; i < n; ++i) {
+        b[i].tok = (uint32_t)std::min<uint64_t>(t, 0xFFFFFFFFull);
+        t += tok_slot_entries(b[i].csize);
+    }
+    return t;
 }
+
+// The 64 KiB-block fast path (k_dtok + k_dexec) is on by default; the knob
+// KN_FAST_DISABLE (S3HC_FAST=0 / S3HC_FAST_DISABLE=1) leaves every unit to the per-unit decoder
+// (A/B runs, parity tests).
+static bool fast_path_enabled() { return !knob_on(KN_FAST_DISABLE); }
 
 // Block decode of a batch: large blocks by the large-block path (when L is active), the rest
 // one wave per unit. *blk_hash: the large-block path's per-block output hashes (single-block
@@ -464,7 +473,7 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
                                 uint32_t grid = 0) {
     if (!grid || grid > nunits) grid = nunits;
     // S3HC_LB_DISABLE (tests, comparisons): every block goes to the one-wave decoder
-    const bool lb = L && L->active && nunits && !getenv("S3HC_LB_DISABLE");
+    const bool lb = L && L->active && nunits && !knob_on(KN_LB_DISABLE);
     if (blk_hash) *blk_hash = lb ? L->a.blk_hash : nullptr;
     hipError_t e;
     if (lb && (e = launch_lb_parse(L->a, src, blk, units, nunits, ucount, blk_out, blk_status, st)) != hipSuccess) return e;
@@ -478,7 +487,7 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
         if ((e = launch_fast_exec(src, dst, blk, units, nunits, ucount, grid, blk_out, blk_status, L->fa, st)) !=
             hipSuccess)
             return e;
-        if (getenv("S3HC_FAST_TRACE")) {  // diagnostics: units the fast path took
+        if (knob_on(KN_FAST_TRACE)) {  // diagnostics (serialises the stream): units the fast path took
             uint64_t nu = nunits;
             if (ucount && (e = hipMemcpyAsync(&nu, ucount, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
             if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
@@ -501,7 +510,7 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
                                  lb ? L->a.unit_lb : nullptr, fast ? L->fa.unit_fast : nullptr, st)) != hipSuccess)
         return e;
     if (lb && (e = launch_lb_exec(L->a, src, dst, blk_out, blk_status, st)) != hipSuccess) return e;
-    if (lb && getenv("S3HC_LB_TRACE")) {  // diagnostics: blocks and chunks taken
+    if (lb && knob_on(KN_LB_TRACE)) {  // diagnostics (serialises the stream): blocks and chunks taken
         LbCtl c;
         if ((e = hipMemcpyAsync(&c, L->a.ctl, sizeof c, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
@@ -574,7 +583,8 @@ struct s3hc_plan {
     // ---- decode
     uint32_t nframes = 0;
     uint32_t blk_cap = 0;
-    DevBuf d_frame_off, d_frame_len, d_dst_off, d_dst_cap;
+    uint32_t dec_grid = 1;  // per-unit decode workgroups (one per 64 KiB of frame room, <= blk_cap)
+    DevBuf d_frame_off, d_frame_len, d_dst_off, d_dst_cap, d_ftok;
     DevBuf d_nblk, d_fstatus, d_blk_base, d_fwant, d_dblocks, d_units, d_blk_out, d_blk_status, d_got;
     LbScratch lb;                        // large-block path scratch (frames allowing > 64 KiB blocks)
 };
@@ -708,11 +718,65 @@ static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t
     return S3HC_OK;
 }
 
+// ------------------------------------------------------------ knobs (s3hc_knobs.hpp)
+namespace s3hc {
+std::atomic<long long> g_knob[KN_COUNT];
+namespace {
+struct KnobName {
+    const char* name;
+    Knob k;
+    long long dflt;
+};
+constexpr KnobName kKnobNames[] = {
+    {"S3HC_FAST_DISABLE", KN_FAST_DISABLE, 0}, {"S3HC_LB_DISABLE", KN_LB_DISABLE, 0},
+    {"S3HC_LBW_DISABLE", KN_LBW_DISABLE, 0},   {"S3HC_LBW_CAP", KN_LBW_CAP, -1},
+    {"S3HC_LBW_ROUNDS", KN_LBW_ROUNDS, -1},    {"S3HC_DEC_ONEWAVE", KN_DEC_ONEWAVE, 0},
+    {"S3HC_FAST_TRACE", KN_FAST_TRACE, 0},     {"S3HC_LB_TRACE", KN_LB_TRACE, 0},
+    {"S3HC_HOST_TRACE", KN_HOST_TRACE, 0},
+};
+// a flag knob is on when its variable is set at all (the env convention of earlier rounds);
+// the numeric ones take the value
+long long knob_value(const KnobName& n, const char* v) {
+    if (!v) return n.dflt;
+    if (n.k == KN_LBW_CAP || n.k == KN_LBW_ROUNDS) return strtoll(v, nullptr, 10);
+    return 1;
+}
+int knob_set(const char* name, const char* v) {
+    if (!strcmp(name, "S3HC_FAST")) {  // S3HC_FAST=0 is the other spelling of S3HC_FAST_DISABLE=1
+        g_knob[KN_FAST_DISABLE].store(v && v[0] == '0' ? 1 : 0, std::memory_order_relaxed);
+        return S3HC_OK;
+    }
+    for (const auto& n : kKnobNames)
+        if (!strcmp(n.name, name)) {
+            g_knob[n.k].store(knob_value(n, v), std::memory_order_relaxed);
+            return S3HC_OK;
+        }
+    return S3HC_INVALID_ARG;
+}
+std::once_flag g_knob_once;
+}  // namespace
+void knobs_load_env_once() {
+    std::call_once(g_knob_once, [] {
+        for (const auto& n : kKnobNames) g_knob[n.k].store(knob_value(n, getenv(n.name)), std::memory_order_relaxed);
+        const char* f = getenv("S3HC_FAST");
+        if (f && f[0] == '0') g_knob[KN_FAST_DISABLE].store(1, std::memory_order_relaxed);
+    });
+}
+}  // namespace s3hc
+
+extern "C" int s3hc_set_knob(const char* name, const char* value) {
+    if (!name) return fail(S3HC_INVALID_ARG, "name is NULL");
+    knobs_load_env_once();  // (a knob set before the first context keeps its value)
+    if (knob_set(name, value) != S3HC_OK) return fail(S3HC_INVALID_ARG, "unknown knob");
+    return S3HC_OK;
+}
+
 // ------------------------------------------------------------ C ABI: ctx
 extern "C" int s3hc_create(s3hc_ctx** out, int device) {
     return guarded([&]() -> int {
         if (!out) return fail(S3HC_INVALID_ARG, "out is NULL");
         *out = nullptr;
+        knobs_load_env_once();
         int n = 0;
         hipError_t e = hipGetDeviceCount(&n);
         if (e != hipSuccess || n == 0) return fail(S3HC_DEVICE, "no HIP device available (the engine has no CPU path)");
@@ -832,8 +896,20 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
         hipStream_t st = ctx->stream;
         std::vector<uint64_t> fo(frame_off, frame_off + n), d(dst_off, dst_off + n);
         std::vector<uint32_t> fl(frame_len, frame_len + n), dc(dst_cap, dst_cap + n);
+        // token-position slots per frame (tok_frame_entries) and the per-unit grid: one workgroup
+        // per 64 KiB of each frame's room (frames of several independent blocks keep their
+        // parallelism; the grid still strides over any extra units)
+        std::vector<uint64_t> ftok(n);
+        uint64_t tok_entries = 0, grid = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            ftok[i] = tok_entries;
+            tok_entries += tok_frame_entries(frame_len[i]);
+            grid += std::max<uint64_t>(1, (dst_cap[i] + 65535u) / 65536u);
+        }
+        P->dec_grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(grid, cap));
         HIPCHK(upload(P->d_frame_off, fo, st));
         HIPCHK(upload(P->d_frame_len, fl, st));
+        HIPCHK(upload(P->d_ftok, ftok, st));
         HIPCHK(upload(P->d_dst_off, d, st));
         HIPCHK(upload(P->d_dst_cap, dc, st));
         HIPCHK(P->d_nblk.ensure(n * 4 + 16));
@@ -867,7 +943,7 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
             }
         }
         HIPCHK(P->lb.prepare(P->blk_cap, P->blk_cap, lc));
-        HIPCHK(P->lb.prepare_fast(P->blk_cap));
+        HIPCHK(P->lb.prepare_fast(P->blk_cap, tok_entries));
         HIPCHK(hipStreamSynchronize(st));
         *out = P.release();
         return S3HC_OK;
@@ -892,7 +968,7 @@ extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src
         HIPCHK(launch_dframe_fill(d_src, P->d_frame_off.as<uint64_t>(), P->d_frame_len.as<uint32_t>(), n,
                                   P->d_dst_off.as<uint64_t>(), P->d_dst_cap.as<uint32_t>(), P->d_blk_base.as<uint64_t>(),
                                   d_status, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(),
-                                  P->d_fwant.as<uint32_t>(), st));
+                                  P->d_fwant.as<uint32_t>(), P->d_ftok.as<uint64_t>(), st));
         T.end();
         T.begin("decode");
         const uint64_t* bh = nullptr;
@@ -900,7 +976,7 @@ extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src
         // several independent blocks have their extra units taken by a stride of the grid
         HIPCHK(decode_launch(&P->lb, d_src, d_dst, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(), P->blk_cap,
                              P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st, &bh,
-                             P->d_total.as<uint64_t>(), std::max<uint32_t>(1u, std::min(n, P->blk_cap))));
+                             P->d_total.as<uint64_t>(), P->dec_grid));
         T.end();
         // frame results, content xxh32 and EndMark checks (one launch)
         T.begin("dec_close");
@@ -1210,7 +1286,7 @@ static double host_us() {
 static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bool stream_mode,
                        std::vector<uint8_t>* vout, uint8_t* dst, size_t cap, size_t* out_len,
                        bool upload_in = true, bool* stopped_out = nullptr) {
-    static const bool trace = getenv("S3HC_HOST_TRACE") != nullptr;  // diagnostics: stage times
+    const bool trace = knob_on(KN_HOST_TRACE);  // diagnostics: stage times
     const double t_0 = trace ? host_us() : 0.0;
 #define HTRACE(tag) if (trace) fprintf(stderr, "[s3hc host] %-10s %8.1f us\n", tag, host_us() - t_0);
     hipStream_t st = ctx->stream;
@@ -1235,6 +1311,7 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
             if (!(F.flg & 0x20)) units.push_back(DecUnit{F.blk0, F.nblk});
             else for (uint32_t k = 0; k < F.nblk; ++k) units.push_back(DecUnit{F.blk0 + k, 1});
         }
+        const uint64_t tok_entries = assign_tok_slots(W.blocks.data(), W.blocks.size());
         HIPCHK(upload(ctx->d_blocks, W.blocks, st));
         HIPCHK(upload(ctx->d_units, units, st));
         HIPCHK(ctx->d_blk_out.ensure(nb * 4));
@@ -1245,7 +1322,7 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         for (auto& U : units)
             if (lb_candidate(W.blocks[U.first], U.n == 1, lc.min_limit)) lc.add_block(W.blocks[U.first].csize, std::min(W.blocks[U.first].limit, W.blocks[U.first].cap), W.blocks[U.first].limit);
         HIPCHK(ctx->lb.prepare((uint32_t)units.size(), (uint32_t)nb, lc));
-        HIPCHK(ctx->lb.prepare_fast((uint32_t)units.size()));
+        HIPCHK(ctx->lb.prepare_fast((uint32_t)units.size(), tok_entries));
         const uint64_t* bh = nullptr;
         HTRACE("launch")
         HIPCHK(decode_launch(&ctx->lb, ctx->d_in.as<uint8_t>(), ctx->d_out.as<uint8_t>(), ctx->d_blocks.as<DecBlock>(),
@@ -1889,6 +1966,7 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
         D.frame -= (uint32_t)(&F0 - W.frames.data());
         mb[k] = D;
     }
+    const uint64_t tok_entries = assign_tok_slots(mb, nbk);
     if (nu) memcpy(m + o_u, units.data(), sizeof(DecUnit) * nu);
     hipStream_t st = S.st;
     HIPCHK(S.h_in.ensure(nin));
@@ -1907,7 +1985,7 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
         for (auto& U : units)
             if (lb_candidate(mb[U.first], U.n == 1, lc.min_limit)) lc.add_block(mb[U.first].csize, std::min(mb[U.first].limit, mb[U.first].cap), mb[U.first].limit);
         HIPCHK(S.lb.prepare(nu, nbk, lc));
-        HIPCHK(S.lb.prepare_fast(nu));
+        HIPCHK(S.lb.prepare_fast(nu, tok_entries));
     }
     HIPCHK(S.h_res.ensure(8ull * n));
     HIPCHK(hipMemcpyAsync(S.d_in.p, S.h_in.p, nin, hipMemcpyHostToDevice, st));

@@ -57,6 +57,7 @@ def _load():
         "s3hc_device_count": (i32, []),
         "s3hc_last_error": (ctypes.c_char_p, []),
         "s3hc_version": (ctypes.c_char_p, []),
+        "s3hc_set_knob": (i32, [ctypes.c_char_p, ctypes.c_char_p]),
         "s3hc_frame_bound": (sz, [sz]),
         "s3hc_compat_encode_dev": (i32, [vp, vp, vp, vp, u32, vp, vp, vp, vp]),
         "s3hc_compress_frame": (i32, [vp, u8p, sz, i32, u8p, sz, szp, ip]),
@@ -184,6 +185,29 @@ def effective_compression(resolved: ResolvedSettings, compression_threshold: int
 
 def device_count() -> int:
     return lib.s3hc_device_count()
+
+
+def set_knob(name: str, value=None) -> None:
+    """Process-wide diagnostic / A-B switch (s3hc_set_knob): value None = default."""
+    _check(lib.s3hc_set_knob(name.encode(), None if value is None else str(value).encode()))
+
+
+class knobs:
+    """Context manager: set knobs (name -> value) for the block, then restore their defaults.
+    Replaces the environment toggles of earlier rounds (the library reads the environment once)."""
+
+    def __init__(self, env: dict):
+        self.env = dict(env)
+
+    def __enter__(self):
+        for k, v in self.env.items():
+            set_knob(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.env:
+            set_knob(k, os.environ.get(k))
+        return False
 
 
 def frame_bound(n: int) -> int:

@@ -71,3 +71,28 @@ def test_synthetic_corpus_distinct_and_deterministic():
     assert j.startswith(b'{"id":1,') and len({j[i:i + 65536] for i in range(0, len(j), 65536)}) == 64
     m, modes = synth.mixed_blocks(6, 65536)
     assert modes == [0, 1, 0, 1, 0, 1] and m[65536:65540] == b"\xff\xd8\xff\xe0"
+
+
+def test_assign_device_refuses_shared_gpus():
+    # one process per GPU: N ranks on fewer than N visible devices must not report N GPUs
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.assign_device(8, 3, 8, False) == (3, None)
+    assert bench.assign_device(1, 0, 1, False) == (0, None)
+    dev, why = bench.assign_device(8, 3, 1, False)
+    assert dev is None and "refusing" in why and "--share-gpu" in why
+    assert bench.assign_device(8, 3, 1, True) == (0, None)  # explicit rehearsal
+    assert bench.assign_device(2, 1, 4, True) == (1, None)
+    assert bench.assign_device(1, 0, 0, True)[0] is None    # no device at all
+    dev, why = bench.assign_device(2, 2, 2, False)          # a local rank past the devices
+    assert dev is None and "LOCAL_RANK" in why
+
+
+def test_gpus_flag_refused_without_enough_devices():
+    # this container has no GPU: two ranks are refused before any collective or HIP work,
+    # and the launcher reports the refusal's status instead of a bench line
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"], timeout=300)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "visible GPU" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -18,16 +18,11 @@ pytestmark = pytest.mark.gpu
 
 
 def _with_env(env, fn):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
+    # library knobs (s3hc_set_knob): the library reads the environment only once per process
+    import s3hc_lz4 as S
+
+    with S.knobs(env):
         return fn()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 def _both(fn):

@@ -22,16 +22,11 @@ BLOCK = 65536
 
 
 def _with_env(env, fn):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
+    # library knobs (s3hc_set_knob): the library reads the environment only once per process
+    import s3hc_lz4 as S
+
+    with S.knobs(env):
         return fn()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 def _slow(fn):  # the per-unit decoder alone
@@ -44,14 +39,12 @@ def _fast(fn):  # host calls of few blocks otherwise take the large-block path
 
 @pytest.fixture(autouse=True)
 def _fast_path_on():
-    # every test here runs with the fast path enabled (opt-in in the library)
-    old = os.environ.get("S3HC_FAST")
-    os.environ["S3HC_FAST"] = "1"
-    yield
-    if old is None:
-        os.environ.pop("S3HC_FAST", None)
-    else:
-        os.environ["S3HC_FAST"] = old
+    # every test here runs with the fast path enabled (the library default; a stray S3HC_FAST=0
+    # in the environment must not turn these tests into per-unit-decoder tests)
+    import s3hc_lz4 as S
+
+    with S.knobs({"S3HC_FAST": "1", "S3HC_FAST_DISABLE": None}):
+        yield
 
 
 def _period(k, n):
@@ -328,3 +321,33 @@ def test_fast_path_densest_token_blocks(engine, oracle):
     for i, (f, d) in enumerate(items):
         assert ost[i] == 0 and olen[i] == len(d), i
         assert out.read(len(d), offs[i]) == d, i
+
+
+def test_device_plan_multiblock_frames_keep_their_parallelism(engine, capfd):
+    # more than 64 frames (past the all-blocks-to-LB threshold) made of independent
+    # 64 KiB blocks (liblz4 BD 0x40, 16 blocks per 1 MiB frame). The device plan's grid is one
+    # workgroup per 64 KiB of frame room (1280 here, not one per frame), every block takes the
+    # fast path, and the token slots (per frame, sized by compressed bytes) stay disjoint even
+    # when two plan entries name the same frame.
+    if not lz4ref.available:
+        pytest.skip("liblz4 absent")
+    n, MiB = 80, 1 << 20
+    data = synth.log_text(n * MiB, 91)
+    frames = [lz4ref.compress_frame(data[i * MiB:(i + 1) * MiB], block_size_id=4, linked=False) for i in range(n)]
+    blob = b"".join(frames)
+    fo = [sum(len(f) for f in frames[:i]) for i in range(n)]
+    fl = [len(f) for f in frames]
+    fo.append(fo[3])  # a duplicate entry: frame 3 decoded a second time into its own slot
+    fl.append(fl[3])
+    offs = [i * MiB for i in range(n + 1)]
+    src = engine.upload(blob)
+    capfd.readouterr()
+    out, olen, ost = _with_env({"S3HC_FAST_TRACE": "1"},
+                               lambda: _decode_batch(engine, src, fo, fl, offs, [MiB] * (n + 1)))
+    err = capfd.readouterr().err
+    m = re.search(r"\[s3hc fast\] units (\d+) taken (\d+) tokens (\d+) grid (\d+)", err)
+    assert m, err
+    assert int(m.group(2)) == 16 * (n + 1) and int(m.group(4)) == 16 * (n + 1), err
+    assert ost == [0] * (n + 1) and olen == [MiB] * (n + 1)
+    got = out.read((n + 1) * MiB)
+    assert got[:n * MiB] == data and got[n * MiB:] == data[3 * MiB:4 * MiB]

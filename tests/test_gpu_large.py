@@ -70,11 +70,11 @@ def _data(name):
 
 
 def _with_env(var, value, fn):
-    os.environ[var] = value
-    try:
+    # library knob (s3hc_set_knob): the library reads the environment only once per process
+    import s3hc_lz4 as S
+
+    with S.knobs({var: value}):
         return fn()
-    finally:
-        del os.environ[var]
 
 
 def _wave_path(fn):

@@ -38,7 +38,7 @@ def case(eng, data, item, reps=5):
     res = {"frames": n, "frame_bytes": item, "ratio": round(C / (n * item), 4)}
     for mode in ("lb", "wave"):
         if mode == "wave":
-            os.environ["S3HC_LB_DISABLE"] = "1"
+            S.set_knob("S3HC_LB_DISABLE", "1")
         try:
             d_out.fill(0)
             eng.decode_dev(dp, d_fr, d_out, d_ol, d_os)
@@ -55,7 +55,7 @@ def case(eng, data, item, reps=5):
             kt = eng.timing()
             eng.set_timing(False)
         finally:
-            os.environ.pop("S3HC_LB_DISABLE", None)
+            S.set_knob("S3HC_LB_DISABLE", None)
         res[mode] = {"ms": round(dt * 1e3, 3), "GiBps": round(n * item / dt / GiB, 3),
                      "decode_kernels_ms": round(kt.get("decode", (0, 1))[0] / reps, 3), "check": ok}
     res["speedup"] = round(res["wave"]["ms"] / res["lb"]["ms"], 2)

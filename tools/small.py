@@ -45,9 +45,9 @@ def dev_latency(eng, blob, fo, fl, item, n, reps=20):
     res = {}
     for lb in (True, False):
         if lb:
-            os.environ.pop("S3HC_LB_DISABLE", None)
+            S.set_knob("S3HC_LB_DISABLE", None)
         else:
-            os.environ["S3HC_LB_DISABLE"] = "1"
+            S.set_knob("S3HC_LB_DISABLE", "1")
         eng.decode_dev(dp, d_in, d_out, d_ol, d_os)
         eng.sync()
         assert d_os.i32(n) == [0] * n
@@ -65,7 +65,7 @@ def dev_latency(eng, blob, fo, fl, item, n, reps=20):
         eng.set_timing(False)
         res["lb" if lb else "nolb"] = {"wall_ms": round(1e3 * float(np.median(ts)), 4),
                                        "stages_ms": {k: round(v[0], 4) for k, v in kt.items()}}
-    os.environ.pop("S3HC_LB_DISABLE", None)
+    S.set_knob("S3HC_LB_DISABLE", None)
     return res
 
 
