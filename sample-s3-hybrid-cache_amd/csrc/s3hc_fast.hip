@@ -337,66 +337,62 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
         }
     }
     __syncthreads();
+    // ---- the chain's tokens past my segment (walk 2's positions, from my walk 1's exit to the
+    // merge point) are true tokens too: mark them
+    if (valid) {
+        for (uint32_t q = x; q < C && q != m;) {
+            atomicOr(&bits[q >> 5], 1u << (q & 31u));
+            q = hop(stage, mis, q, C).nxt;
+        }
+    }
+    __syncthreads();
     [[maybe_unused]] const uint64_t tp5 = FP_NOW();
-    // ---- validate (lz4_flex bounds: output within the block limit and the caller's capacity,
-    // every offset non-zero and within the bytes produced before its match) while marking the
-    // tokens past my segment
-    uint32_t o = 0, ntok = 0;
+    // ---- sequence records, in stream order: each thread decodes the true tokens of four
+    // consecutive bitmap words (positions [128 g, 128 g + 128)) at its scanned rank, and checks
+    // the lz4_flex bounds (every offset non-zero and within the bytes produced before its match;
+    // output within the block limit and the caller's capacity). Record: {lit | ll << 15,
+    // off | (ml - 4) << 16}, off = 0 for the last sequence (no match).
+    const uint32_t nbw = (C + 31u) / 32u;
+    uint32_t wv[4], cnt = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t k = 4u * g + j;
+        wv[j] = k < nbw ? bits[k] : 0u;
+        cnt += (uint32_t)__builtin_popcount(wv[j]);
+    }
+    uint32_t N;
+    uint32_t r = wg_excl_scan<kTT / 64>(cnt, scr, &N);
+    uint2* rec = a.rec + B.tok;
+    uint32_t o = 0;
     int32_t minsl = 0x7FFFFFFF;
     bool bad = false;
-    if (valid) {
-        p = vf;
-        while (p != m) {
-            if (p >= C) {  // END or DEAD before the merge point: not the walk 2 saw
-                bad = true;
-                break;
-            }
-            if (p >= s1) atomicOr(&bits[p >> 5], 1u << (p & 31u));
-            const Tok T = hop(stage, mis, p, C);
-            ++ntok;
-            if (T.nxt == DEAD) bad = true;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        uint32_t xb = wv[j];
+        const uint32_t wb = (4u * g + j) << 5;
+        while (xb) {
+            const uint32_t q = wb + (uint32_t)__builtin_ctz(xb);
+            xb &= xb - 1u;
+            const Tok T = hop(stage, mis, q, C);
+            const uint32_t lit = T.ll == 0 ? 0u : q + 1u + (T.ll >= 15u ? (T.ll - 15u) / 255u + 1u : 0u);
             o += T.ll;
+            uint32_t y = 0;
             if (T.nxt != END) {
                 bad |= T.off == 0u;
                 minsl = min(minsl, (int32_t)o - (int32_t)T.off);
                 o += T.ml;
+                y = T.off | ((T.ml - 4u) << 16);
             }
-            p = T.nxt;
+            rec[r++] = make_uint2(lit | (T.ll << 15), y);
         }
     }
     [[maybe_unused]] const uint64_t tp6 = FP_NOW();
-    uint32_t Utot, N;
-    uint32_t obase, tbase;
-    wg_excl_scan2<kTT / 64>(o, ntok, scr, &obase, &tbase, &Utot, &N);
-    (void)tbase;
-    const bool fail = bad || (valid && (int64_t)obase + minsl < 0);
+    uint32_t Utot;
+    const uint32_t obase = wg_excl_scan<kTT / 64>(o, scr, &Utot);
+    const bool fail = bad || (int64_t)obase + minsl < 0;
     if (fail) sflag[1] = 1u;
     __syncthreads();
     const bool ok = !sflag[1] && Utot <= B.limit && Utot <= B.cap;
-    if (ok) {
-        // the token positions in order (k_dexec reads 64 per window): each thread expands four
-        // consecutive bitmap words at its scanned rank
-        const uint32_t nbw = (C + 31u) / 32u;
-        uint32_t wv[4], cnt = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            const uint32_t k = 4u * g + j;
-            wv[j] = k < nbw ? bits[k] : 0u;
-            cnt += (uint32_t)__builtin_popcount(wv[j]);
-        }
-        uint32_t tot;
-        uint32_t r = wg_excl_scan<kTT / 64>(cnt, scr, &tot);
-        uint16_t* tk = a.tok + B.tok;
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
-            uint32_t x = wv[j];
-            const uint32_t wb = (4u * g + j) << 5;
-            while (x) {
-                tk[r++] = (uint16_t)(wb + (uint32_t)__builtin_ctz(x));
-                x &= x - 1u;
-            }
-        }
-    }
     if (g == 0) {
         if (ok) {
             FastUnit F;
@@ -718,7 +714,7 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
     const FastUnit F = a.fu[u];
     const uint8_t* in = src + B.src_off;
     uint8_t* out = dst + B.dst_off;
-    const uint16_t* tk = a.tok + B.tok;
+    const uint2* rec = a.rec + B.tok;
     const uint32_t N = F.ntok, C = B.csize;
     uint32_t upos = 0, flushed = 0;
     auto flush_full = [&]() {
@@ -728,42 +724,24 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
         }
     };
     const uint32_t nwin = (N + 63u) >> 6;
-    auto tpos = [&](uint32_t w) -> uint32_t {  // my token's position in window w (or C: none)
+    // my sequence record in window w (zeros past the last: no literal, no match); the load is
+    // unconditional (a clamped index), so no branch forces an early wait
+    auto ldrec = [&](uint32_t w) -> uint2 {
         const uint32_t t = 64u * w + lane;
-        const uint32_t v = tk[t < N ? t : N - 1u];  // (unconditional load)
-        return t < N ? v : C;
+        const uint2 v = rec[t < N ? t : N - 1u];
+        return t < N ? v : make_uint2(0u, 0u);
     };
-    auto ld_w0 = [&](uint32_t pos) -> uint32_t { return gld4(in + umin_(pos, C)); };
-    // ---- pipeline prologue: window 2's token dword, window 1's offset dword, window 0 decoded
-    const uint32_t pos_0 = tpos(0);
-    uint32_t pos_n = tpos(1);
-    uint32_t pos_2 = tpos(2);
-    uint32_t pos_3r = tpos(3);  // window w + 3's positions, read one window ahead of their use
-    uint32_t w0_c = ld_w0(pos_0);
-    uint32_t w0_n = ld_w0(pos_n);
-    uint32_t w0_2 = ld_w0(pos_2);
-    // window 0: token + offset dwords now
-    SeqF fc, fn;
-    uint32_t mp_n = 0, w1_n = 0;
-    {
-        const uint32_t pos = pos_0;
-        fc.ll = pos < C ? lit_len(in, pos, w0_c, fc.lit) : 0u;
-        const uint32_t mp = fc.lit + fc.ll;
-        fc.off = fc.ml = 0;
-        if (pos < C && mp < C) {
-            const uint32_t w1 = gld4(in + mp);
-            fc.off = w1 & 0xFFFFu;
-            fc.ml = match_len(in, mp, w0_c & 0xFFu, w1);
-        }
-        mp_n = C;
-        if (pos_n < C) {
-            uint32_t lit;
-            const uint32_t ll = lit_len(in, pos_n, w0_n, lit);
-            mp_n = umin_(lit + ll, C);
-        }
-        w1_n = gld4(in + mp_n);
-    }
-
+    auto unpack = [&](uint2 r) -> SeqF {
+        SeqF f;
+        f.ll = r.x >> 15;
+        f.lit = f.ll ? (r.x & 0x7FFFu) : C;
+        f.off = r.y & 0xFFFFu;
+        f.ml = f.off ? (r.y >> 16) + 4u : 0u;
+        return f;
+    };
+    // ---- pipeline prologue: records of windows 1 and 2 in flight, window 0 unpacked
+    uint2 r_n = ldrec(1), r_2 = ldrec(2);
+    SeqF fc = unpack(ldrec(0)), fn;
     uint32_t Sincl_c = incl_scan(fc.ll + fc.ml, lane);
     uint32_t S_c = rdlane(Sincl_c, 63);
     bool far_c = false, pf_c = S_c <= kWin;  // window 0: nothing is far
@@ -784,31 +762,10 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
         [[maybe_unused]] uint64_t tq0 = FP_NOW();
         const uint32_t nact = umin_(64u, N - 64u * w);
         const bool act = lane < nact;
-        // ---- stage A: window w+3's token dword (loads are unconditional: a lane without a
-        // token reads a harmless in-frame address, so no branch forces an early wait) and
-        // window w+4's token positions
-        const uint32_t pos_3 = pos_3r;
-        pos_3r = tpos(w + 4);
-        const uint32_t w0_3 = gld4(in + pos_3);
-        // ---- stage B: window w+2's offset dword
-        uint32_t mp_2;
-        {
-            uint32_t lit;
-            const uint32_t ll = pos_2 < C ? lit_len(in, pos_2, w0_2, lit) : 0u;
-            mp_2 = pos_2 < C ? umin_(lit + ll, C) : C;
-        }
-        const uint32_t w1_2 = gld4(in + mp_2);
-        // ---- stage C: decode window w+1, prefetch its literals and far match sources
-        fn.ll = 0;
-        fn.lit = C;
-        fn.off = fn.ml = 0;
-        if (pos_n < C) {
-            fn.ll = lit_len(in, pos_n, w0_n, fn.lit);
-            if (mp_n < C) {
-                fn.off = w1_n & 0xFFFFu;
-                fn.ml = match_len(in, mp_n, w0_n & 0xFFu, w1_n);
-            }
-        }
+        // ---- stage A: window w+3's records (two windows of lead); stage C: window w+1 unpacked,
+        // its literals and far match sources prefetched
+        const uint2 r_3 = ldrec(w + 3);
+        fn = unpack(r_n);
         const uint32_t Sincl_n = incl_scan(fn.ll + fn.ml, lane);
         const uint32_t S_n = rdlane(Sincl_n, 63);
         const bool pf_n = S_c <= kWin && S_n <= kWin;
@@ -1133,12 +1090,8 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
         lsh_c = lsh_n;
         far0_c = far0_n;
         far1_c = far1_n;
-        pos_n = pos_2;
-        w0_n = w0_2;
-        mp_n = mp_2;
-        w1_n = w1_2;
-        pos_2 = pos_3;
-        w0_2 = w0_3;
+        r_n = r_2;
+        r_2 = r_3;
     }
     // ---- the rest of the output (< kFl bytes)
     if (upos > flushed) {

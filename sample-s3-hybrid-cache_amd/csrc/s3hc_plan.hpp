@@ -77,7 +77,7 @@ struct DecBlock {        // 40 bytes
     uint32_t flags;      // DB_*
     uint32_t frame;      // owning frame
     uint32_t tok;        // 64 KiB fast path: first entry of this block's token-position slot in
-                         // FastArgs::tok (slots sized by compressed bytes: (csize - 1) / 3 + 1
+                         // FastArgs::rec (slots sized by compressed bytes: (csize - 1) / 3 + 1
                          // entries, disjoint per block of a launch; see tok_slot_entries)
 };
 
@@ -204,7 +204,8 @@ struct FastUnit {        // 16 bytes, written by k_dtok for every unit it takes
 };
 
 struct FastArgs {
-    uint16_t* tok;       // per block, at DecBlock::tok: the block's token positions in order
+    uint2* rec;          // per block, at DecBlock::tok: the block's sequence records in stream order,
+                         // {lit | ll << 15, off | (ml - 4) << 16} (off = 0: the last, match-less one)
     FastUnit* fu;        // per unit
     uint8_t* unit_fast;  // per unit: 1 = decoded by the fast path
 };

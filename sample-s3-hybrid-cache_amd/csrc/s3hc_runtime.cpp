@@ -372,7 +372,7 @@ struct LbScratch {
         seqoff, lb_err, lb_size, lb_stat, lb_tok0, lb_ntok, rfirst, blk_hash, wbase, wtile0, wP, tpend, tinit;
     LbArgs a{};
     // 64 KiB-block fast path (s3hc_fast.hip): per-unit token bitmaps and results
-    DevBuf f_bmp, f_fu, f_unit_fast;  // (f_bmp: token positions)
+    DevBuf f_bmp, f_fu, f_unit_fast;  // (f_bmp: sequence records)
     FastArgs fa{};
     bool fast_ready = false;
     // tok_entries: the launch's token-slot entries (DecBlock::tok + tok_slot_entries(csize) of
@@ -381,10 +381,10 @@ struct LbScratch {
         fast_ready = false;
         if (!nunits || tok_entries > 0xFFFFFFF0ull) return hipSuccess;  // (u32 slots: the fast path sits out)
         hipError_t e;
-        if ((e = f_bmp.ensure((size_t)tok_entries * sizeof(uint16_t) + 256)) != hipSuccess) return e;
+        if ((e = f_bmp.ensure((size_t)tok_entries * sizeof(uint2) + 256)) != hipSuccess) return e;
         if ((e = f_fu.ensure((size_t)nunits * sizeof(FastUnit) + 64)) != hipSuccess) return e;
         if ((e = f_unit_fast.ensure((size_t)nunits + 64)) != hipSuccess) return e;
-        fa.tok = f_bmp.as<uint16_t>();
+        fa.rec = f_bmp.as<uint2>();
         fa.fu = f_fu.as<FastUnit>();
         fa.unit_fast = f_unit_fast.as<uint8_t>();
         fast_ready = true;
