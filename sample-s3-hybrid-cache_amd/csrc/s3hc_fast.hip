@@ -46,6 +46,17 @@ constexpr uint32_t kMaxC = kFastMaxC;
 #ifndef S3HC_DTOK_TT
 #define S3HC_DTOK_TT 256
 #endif
+#ifndef S3HC_HOP2  // 1: k_dtok parses tokens with hop2 (branch-light), 0: hop
+#define S3HC_HOP2 1
+#endif
+#if S3HC_HOP2
+#define S3HC_HOPF hop2
+#else
+#define S3HC_HOPF hop
+#endif
+#ifndef S3HC_DTOK_BAL  // 1: records by sequence rank, K per thread (0: by bitmap words)
+#define S3HC_DTOK_BAL 0
+#endif
 constexpr uint32_t kTT = S3HC_DTOK_TT;         // k_dtok threads = speculative segments per block
 constexpr uint32_t kStage = kMaxC + 64;        // staged block: 16-B alignment slack + zero read-ahead
 constexpr uint32_t kBitW = kMaxC / 32;         // bitmap words, one bit per compressed position
@@ -144,6 +155,47 @@ __device__ __forceinline__ Tok hop(const uint8_t* st, uint32_t mis, uint32_t p, 
     return T;
 }
 
+// The same token parse with the common cases branch-free (one length-extension byte per field as
+// selects; two or more extension bytes, rare, in a branch) and the verdicts computed last as
+// selects: the same (nxt, ll, off, ml) as hop() for every input (an offset word past the block is
+// read at a clamped address and ignored: the verdict is DEAD or END there).
+__device__ __forceinline__ Tok hop2(const uint8_t* st, uint32_t mis, uint32_t p, uint32_t C) {
+    Tok T;
+    const uint32_t w0 = st32(st, p + mis);
+    const uint32_t t = w0 & 0xFFu;
+    uint32_t L = t >> 4, q = p + 1u;
+    const uint32_t b1 = (w0 >> 8) & 0xFFu;
+    const bool x1 = L == 15u;
+    L += x1 ? b1 : 0u;
+    q += x1 ? 1u : 0u;
+    if (x1 && b1 == 255u) {  // rare: a second extension byte (and more)
+        const uint32_t b2 = (w0 >> 16) & 0xFFu;
+        L += b2;
+        ++q;
+        if (b2 == 255u) L += ext_tail(st, mis, q, C);
+    }
+    const uint32_t mp = q + L;
+    const uint32_t w1 = st32(st, umin_(mp, C) + mis);
+    uint32_t M = (t & 15u) + 4u, q2 = mp + 2u;
+    const uint32_t f1 = (w1 >> 16) & 0xFFu;
+    const bool x2 = (t & 15u) == 15u;
+    M += x2 ? f1 : 0u;
+    q2 += x2 ? 1u : 0u;
+    if (x2 && f1 == 255u && mp <= C) {  // rare
+        const uint32_t f2 = w1 >> 24;
+        M += f2;
+        ++q2;
+        if (f2 == 255u) M += ext_tail(st, mis, q2, C);
+    }
+    const bool dead_lit = q > C || L > C - q;
+    const bool end = mp == C;
+    T.ll = L;
+    T.off = dead_lit || end ? 0u : w1 & 0xFFFFu;
+    T.ml = dead_lit || end ? 0u : M;
+    T.nxt = dead_lit ? fst::DEAD : (end ? fst::END : ((C - mp < 2u || q2 >= C) ? fst::DEAD : q2));
+    return T;
+}
+
 // exclusive scan over the NW waves of a workgroup; *total = sum
 template <uint32_t NW>
 __device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
@@ -204,12 +256,18 @@ __device__ __forceinline__ void wg_excl_scan2(uint32_t v, uint32_t u, uint32_t* 
 }  // namespace
 
 // ------------------------------------------------------------------ k_dtok
-__device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __restrict__ src,
+// Returns whether the fast path took unit u (workgroup-uniform); *fo = its (sequences, bytes).
+__device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __restrict__ src,
                                           const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
-                                          const uint8_t* __restrict__ unit_lb, const FastArgs& a) {
+                                          const uint8_t* __restrict__ unit_lb, const FastArgs& a,
+                                          uint32_t maxc, FastUnit* fo) {
     using namespace fst;
-    __shared__ __attribute__((aligned(16))) uint8_t stage[kStage];
-    __shared__ uint32_t bits[kBitW];
+    // the staged block and the token bitmap live in dynamic LDS sized to the launch's largest
+    // compressed block (fast_lds_bytes): config 2's ~26 KB blocks fit five workgroups per CU
+    // instead of four at the 32 KiB maximum
+    extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
+    uint8_t* stage = dsm;
+    uint32_t* bits = (uint32_t*)(dsm + fast_stage_bytes(maxc));
     __shared__ uint16_t svfrom[kTT];   // per segment on the true chain: its first true token (else M_BAD)
     __shared__ uint16_t J[2][kTT + 2]; // succ^(2^k) per segment, ping-pong; kTT / kTT + 1 are terminals
     __shared__ uint8_t reach[kTT + 2]; // segment is on the true chain
@@ -221,11 +279,11 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
     DecBlock B;
     if (take) {
         B = blk[U.first];
-        take = !(B.flags & DB_STORED) && B.csize >= 1u && B.csize <= kMaxC;
+        take = !(B.flags & DB_STORED) && B.csize >= 1u && B.csize <= maxc;
     }
     if (!take) {
         if (g == 0) a.unit_fast[u] = 0;
-        return;
+        return false;
     }
     const uint32_t C = B.csize;
     [[maybe_unused]] const uint64_t tp0 = FP_NOW();
@@ -266,7 +324,7 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
     uint32_t p = s0;
     while (p < s1) {
         atomicOr(&bits[p >> 5], 1u << (p & 31u));
-        p = hop(stage, mis, p, C).nxt;
+        p = S3HC_HOPF(stage, mis, p, C).nxt;
     }
     const uint32_t x = s0 < s1 ? p : DEAD;
     __syncthreads();
@@ -279,7 +337,7 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
             m = DEAD;
             break;
         }
-        m = hop(stage, mis, m, C).nxt;
+        m = S3HC_HOPF(stage, mis, m, C).nxt;
         ++ovf;
     }
 #ifdef FPROF
@@ -319,7 +377,7 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
     __syncthreads();
     if (sflag[0] != kTermEnd) {
         if (g == 0) a.unit_fast[u] = 0;
-        return;
+        return false;
     }
     [[maybe_unused]] const uint64_t tp4 = FP_NOW();
     // ---- the true token bitmap: in a segment on the chain the marks before its first true
@@ -342,16 +400,15 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
     if (valid) {
         for (uint32_t q = x; q < C && q != m;) {
             atomicOr(&bits[q >> 5], 1u << (q & 31u));
-            q = hop(stage, mis, q, C).nxt;
+            q = S3HC_HOPF(stage, mis, q, C).nxt;
         }
     }
     __syncthreads();
     [[maybe_unused]] const uint64_t tp5 = FP_NOW();
-    // ---- sequence records, in stream order: each thread decodes the true tokens of four
-    // consecutive bitmap words (positions [128 g, 128 g + 128)) at its scanned rank, and checks
-    // the lz4_flex bounds (every offset non-zero and within the bytes produced before its match;
-    // output within the block limit and the caller's capacity). Record: {lit | ll << 15,
-    // off | (ml - 4) << 16}, off = 0 for the last sequence (no match).
+    // ---- sequence records, in stream order, and the lz4_flex bounds (every offset non-zero and
+    // within the bytes produced before its match; output within the block limit and the caller's
+    // capacity). Record: {lit | ll << 15, off | (ml - 4) << 16}, off = 0 for the last sequence
+    // (no match).
     const uint32_t nbw = (C + 31u) / 32u;
     uint32_t wv[4], cnt = 0;
 #pragma unroll
@@ -361,11 +418,57 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
         cnt += (uint32_t)__builtin_popcount(wv[j]);
     }
     uint32_t N;
-    uint32_t r = wg_excl_scan<kTT / 64>(cnt, scr, &N);
+    const uint32_t r0 = wg_excl_scan<kTT / 64>(cnt, scr, &N);
     uint2* rec = a.rec + B.tok;
     uint32_t o = 0;
     int32_t minsl = 0x7FFFFFFF;
     bool bad = false;
+    auto emit = [&](uint32_t q, uint32_t k) {  // the token at q is sequence k
+        const Tok T = S3HC_HOPF(stage, mis, q, C);
+        const uint32_t lit = T.ll == 0 ? 0u : q + 1u + (T.ll >= 15u ? (T.ll - 15u) / 255u + 1u : 0u);
+        o += T.ll;
+        uint32_t y = 0;
+        if (T.nxt != END) {
+            bad |= T.off == 0u;
+            minsl = min(minsl, (int32_t)o - (int32_t)T.off);
+            o += T.ml;
+            y = T.off | ((T.ml - 4u) << 16);
+        }
+        rec[k] = make_uint2(lit | (T.ll << 15), y);
+    };
+#if S3HC_DTOK_BAL
+    // balanced: thread g decodes sequences [g K, g K + K) (K = ceil(N / kTT)), found from the
+    // scanned per-thread counts (J[0] is free after the doubling) by binary search, then by the
+    // bitmap words from there
+    uint16_t* base = J[0];
+    base[g] = (uint16_t)r0;
+    if (g == 0) base[kTT] = (uint16_t)N;
+    __syncthreads();
+    {
+        const uint32_t K = (N + kTT - 1u) / kTT, R0 = g * K, R1 = umin_(N, R0 + K);
+        if (R0 < R1) {
+            uint32_t t = 0;
+#pragma unroll
+            for (uint32_t step = kTT / 2; step; step >>= 1)
+                if (base[t + step] <= R0) t += step;
+            uint32_t w = 4u * t, xb = bits[w], skip = R0 - base[t];
+            for (uint32_t pc = (uint32_t)__builtin_popcount(xb); skip >= pc; pc = (uint32_t)__builtin_popcount(xb)) {
+                skip -= pc;
+                xb = bits[++w];
+            }
+            for (; skip; --skip) xb &= xb - 1u;
+            for (uint32_t k = R0; k < R1; ++k) {
+                while (!xb) xb = bits[++w];
+                const uint32_t q = (w << 5) + (uint32_t)__builtin_ctz(xb);
+                xb &= xb - 1u;
+                emit(q, k);
+            }
+        }
+    }
+#else
+    // each thread decodes the true tokens of its four bitmap words (positions [128 g, 128 g + 128))
+    // at its scanned rank
+    uint32_t r = r0;
 #pragma unroll
     for (uint32_t j = 0; j < 4; ++j) {
         uint32_t xb = wv[j];
@@ -373,19 +476,10 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
         while (xb) {
             const uint32_t q = wb + (uint32_t)__builtin_ctz(xb);
             xb &= xb - 1u;
-            const Tok T = hop(stage, mis, q, C);
-            const uint32_t lit = T.ll == 0 ? 0u : q + 1u + (T.ll >= 15u ? (T.ll - 15u) / 255u + 1u : 0u);
-            o += T.ll;
-            uint32_t y = 0;
-            if (T.nxt != END) {
-                bad |= T.off == 0u;
-                minsl = min(minsl, (int32_t)o - (int32_t)T.off);
-                o += T.ml;
-                y = T.off | ((T.ml - 4u) << 16);
-            }
-            rec[r++] = make_uint2(lit | (T.ll << 15), y);
+            emit(q, r++);
         }
     }
+#endif
     [[maybe_unused]] const uint64_t tp6 = FP_NOW();
     uint32_t Utot;
     const uint32_t obase = wg_excl_scan<kTT / 64>(o, scr, &Utot);
@@ -393,14 +487,13 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
     if (fail) sflag[1] = 1u;
     __syncthreads();
     const bool ok = !sflag[1] && Utot <= B.limit && Utot <= B.cap;
+    FastUnit F;
+    F.ntok = N;
+    F.U = Utot;
+    F.pad0 = F.pad1 = 0;
+    *fo = F;
     if (g == 0) {
-        if (ok) {
-            FastUnit F;
-            F.ntok = N;
-            F.U = Utot;
-            F.pad0 = F.pad1 = 0;
-            a.fu[u] = F;
-        }
+        if (ok) a.fu[u] = F;
         a.unit_fast[u] = ok ? 1 : 0;
     }
 #ifdef FPROF
@@ -415,6 +508,7 @@ __device__ __forceinline__ void dtok_unit(const uint32_t u, const uint8_t* __res
         FP_ADD(7, 1);
     }
 #endif
+    return ok;
 }
 
 // units [0, count) of a plan, count read on the device (a device-built plan: the frame walk's
@@ -426,10 +520,11 @@ __device__ __forceinline__ uint32_t unit_count(const uint64_t* ucount, uint32_t 
 __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ src, const DecBlock* __restrict__ blk,
                                                    const DecUnit* __restrict__ units, uint32_t nunits,
                                                    const uint64_t* __restrict__ ucount,
-                                                   const uint8_t* __restrict__ unit_lb, FastArgs a) {
+                                                   const uint8_t* __restrict__ unit_lb, FastArgs a, uint32_t maxc) {
     const uint32_t nu = unit_count(ucount, nunits);
     for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
-        dtok_unit(u, src, blk, units, unit_lb, a);
+        FastUnit F;
+        (void)dtok_unit(u, src, blk, units, unit_lb, a, maxc, &F);
         __syncthreads();  // (the next unit reuses the LDS)
     }
 }
@@ -449,6 +544,9 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
 // growing multiples of their period).
 #ifndef S3HC_FXOR  // 1: a window's output range is cleared, then or-written (0: masked writes)
 #define S3HC_FXOR 0
+#endif
+#ifndef S3HC_LIT32  // 1: the first literal chunk as four unaligned dword stores (0: 16 byte stores)
+#define S3HC_LIT32 0
 #endif
 #ifndef S3HC_FXSKIP  // diagnostic builds: phases of k_dexec left out (timing only; output wrong)
 #define S3HC_FXSKIP 0
@@ -699,19 +797,33 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t x, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
 }
 
+// One wave executes unit u (taken by the token index: F = its sequences and bytes) into the
+// 8 KiB LDS ring `ring`. hsync (k_dsmall, nullptr otherwise): a hashing wave of the workgroup
+// reads the ring behind the executor; hsync[0] = bytes final (published after each window),
+// hsync[1] = bytes hashed; the executor never overwrites ring bytes that are not hashed yet.
 __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                            const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
                                            uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
-                                           const FastArgs& a) {
+                                           const FastArgs& a, const FastUnit F, uint32_t* __restrict__ ring,
+                                           volatile uint32_t* hsync) {
     using namespace fst;
-    __shared__ __attribute__((aligned(16))) uint32_t ring[kORW];
     __shared__ uint4 pinfo[64];              // pending matches: md, ms, ml | off << 16, first dword - rank
     __shared__ uint8_t gmk[kGW];             // pending dwords: rank of each lane's first dword -> lane + 1
-    if (!a.unit_fast[u]) return;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
     const DecUnit Un = units[u];
     const DecBlock B = blk[Un.first];
-    const FastUnit F = a.fu[u];
+    // ring bytes [end - kOR + 16, end) may be overwritten once the hashing wave is past them;
+    // bytes below upos are published to it after every window / batch / piece
+    auto hwait = [&](uint32_t end) {
+        if (hsync)
+            while (end + 16u > hsync[1] + kOR) __builtin_amdgcn_s_sleep(1);
+    };
+    auto hpub = [&](uint32_t done) {
+        if (hsync) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) hsync[0] = done;
+        }
+    };
     const uint8_t* in = src + B.src_off;
     uint8_t* out = dst + B.dst_off;
     const uint2* rec = a.rec + B.tok;
@@ -791,6 +903,7 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
         const uint32_t ll = act ? fc.ll : 0u, lit = fc.lit, off = fc.off, ml = act ? fc.ml : 0u;
         const uint32_t len = ll + ml;
         if (pf_c && S_c <= kWin) {
+            hwait(upos + S_c);
             const uint32_t d0 = upos + Sincl_c - len;
             // literals (first 32 bytes prefetched; near the block's end they were loaded from a
             // clamped address: shift them back)
@@ -827,12 +940,27 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                 const bool bytew = !S3HC_FXOR && act && ll && A0 + 16u <= kOR && d0 + 16u <= upos + S_c;
                 if (bytew) {
                     uint8_t* rb = (uint8_t*)ring + A0;
+#if S3HC_LIT32
+                    // four unaligned dword stores, highest first: a lane's bytes past its
+                    // literals that land in a later lane's literals sit >= 5 bytes further into
+                    // this lane's chunk (ll >= 1, ml >= 4), so always in a higher dword, stored
+                    // by an earlier instruction than the later lane's own store of that byte
+                    *(u32u*)(rb + 12) = lit0_c.w;
+                    __builtin_amdgcn_sched_barrier(0);
+                    *(u32u*)(rb + 8) = lit0_c.z;
+                    __builtin_amdgcn_sched_barrier(0);
+                    *(u32u*)(rb + 4) = lit0_c.y;
+                    __builtin_amdgcn_sched_barrier(0);
+                    *(u32u*)(rb + 0) = lit0_c.x;
+                    __builtin_amdgcn_sched_barrier(0);
+#else
                     const uint32_t x[4] = {lit0_c.x, lit0_c.y, lit0_c.z, lit0_c.w};
 #pragma unroll
                     for (int k = 15; k >= 0; --k) {
                         rb[k] = (uint8_t)(x[k >> 2] >> (8 * (k & 3)));
                         __builtin_amdgcn_sched_barrier(0);  // (the stores' order is the contract)
                     }
+#endif
                 }
                 asm volatile("" ::: "memory");
                 if (act && ll && !bytew) wr16(ring, d0, lit0_c, umin_(16u, ll));
@@ -1001,6 +1129,7 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
 #endif
             upos += S_c;
             flush_full();
+            hpub(upos);
         } else {
             // ---- a window of more than kWin output bytes (or right after one): batches of
             // <= kWin bytes in lane order, sources read at once; sequences longer than a batch run
@@ -1016,9 +1145,11 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                     for (uint32_t k = 0; k < sll; k += kFl) {
                         const uint32_t piece = umin_(kFl, sll - k);
                         const uint32_t j = 16u * lane;
+                        hwait(upos + piece);
                         if (j < piece) rst(ring, upos + j, gld16_blk(in, slit + k + j, C), umin_(16u, piece - j));
                         upos += piece;
                         flush_full();
+                        hpub(upos);
                     }
                     const uint32_t mdst = upos;
                     for (uint32_t k = 0; k < sml;) {
@@ -1028,6 +1159,7 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                             if (P > k + soff) P = soff * ((k + soff) / soff);
                             piece = umin_(piece, P);
                         }
+                        hwait(upos + piece);
                         const uint32_t j = 16u * lane;
                         if (j < piece) {
                             const uint32_t y = mdst + k - P + j, n = umin_(16u, piece - j);
@@ -1039,12 +1171,14 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                         k += piece;
                         upos += piece;
                         flush_full();
+                        hpub(upos);
                     }
                     i0 = i0 + 1;
                     continue;
                 }
                 const bool inb = act && lane >= i0 && lane < i1;
                 const uint32_t Sb = rdlane(Sincl_c, (int)(i1 - 1)) - base;
+                hwait(upos + Sb);
                 const uint32_t d0 = upos + Sincl_c - len - base;
                 for (uint32_t c = 0; __ballot(inb && c < ll); c += 16u)
                     if (inb && c < ll) rst(ring, d0 + c, gld16_blk(in, lit + c, C), umin_(16u, ll - c));
@@ -1072,6 +1206,7 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                 }
                 upos += Sb;
                 flush_full();
+                hpub(upos);
                 i0 = i1;
             }
         }
@@ -1093,6 +1228,7 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
         r_n = r_2;
         r_2 = r_3;
     }
+    hpub(upos);
     // ---- the rest of the output (< kFl bytes)
     if (upos > flushed) {
         const uint32_t n = upos - flushed, first = kOR - (flushed & kORM);
@@ -1124,9 +1260,106 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                                               uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
                                               FastArgs a) {
     const uint32_t nu = unit_count(ucount, nunits);
+    __shared__ __attribute__((aligned(16))) uint32_t ring[fst::kORW];
     for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
-        dexec_unit(u, src, dst, blk, units, blk_out, blk_status, a);
+        if (!a.unit_fast[u]) continue;
+        dexec_unit(u, src, dst, blk, units, blk_out, blk_status, a, a.fu[u], ring, nullptr);
         wsync();
+    }
+}
+
+// ------------------------------------------------------------------ k_dsmall
+namespace {
+constexpr uint32_t XH1 = 2654435761U, XH2 = 2246822519U, XH3 = 3266489917U, XH4 = 668265263U, XH5 = 374761393U;
+__device__ __forceinline__ uint32_t xh_rotl(uint32_t x, int r) { return __builtin_amdgcn_alignbit(x, x, 32 - r); }
+__device__ __forceinline__ uint32_t xh_round(uint32_t acc, uint32_t in) { return xh_rotl(acc + in * XH2, 13) * XH1; }
+}  // namespace
+
+// The hashing wave of k_dsmall: xxh32 (seed 0) of the unit's U output bytes, read from the
+// executor's LDS ring behind it (hsync protocol of dexec_unit). Lane a = lane & 3 runs accumulator
+// a; for 16 stripes at a time lane 4k + a loads stripe k's dword a and multiplies it by P2 (off the
+// chain), the chain then adds, rotates and multiplies by P1 (k_lb_run's hashing wave, §4b).
+__device__ __forceinline__ uint32_t hash_ring(const uint32_t* ring, volatile uint32_t* hsync, uint32_t U) {
+    using namespace fst;
+    const uint32_t lane = threadIdx.x & 63u, ha = lane & 3u;
+    uint32_t hacc = ha == 0 ? XH1 + XH2 : (ha == 1 ? XH2 : (ha == 2 ? 0u : 0u - XH1));
+    const uint32_t hns = U >> 4;
+    uint32_t hs = 0;
+    for (;;) {
+        const uint32_t avail = hsync[0];
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t lim = umin_(avail >> 4, hns);
+        for (; hs + 16u <= lim; hs += 16u) {
+            const uint32_t mv = ring[((16u * hs + 4u * lane) & kORM) >> 2] * XH2;
+            uint32_t m[16];
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) m[k] = (uint32_t)__shfl((int)mv, (int)(4u * k + ha), 64);
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) hacc = xh_rotl(hacc + m[k], 13) * XH1;
+        }
+        for (; hs < lim; ++hs) hacc = xh_round(hacc, ring[((16u * hs + 4u * ha) & kORM) >> 2]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) hsync[1] = 16u * hs;
+        if (avail >= U) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    const int qb = (int)(lane & ~3u);
+    const uint32_t v1 = (uint32_t)__shfl((int)hacc, qb, 64), v2 = (uint32_t)__shfl((int)hacc, qb + 1, 64);
+    const uint32_t v3 = (uint32_t)__shfl((int)hacc, qb + 2, 64), v4 = (uint32_t)__shfl((int)hacc, qb + 3, 64);
+    uint32_t h = U >= 16u ? xh_rotl(v1, 1) + xh_rotl(v2, 7) + xh_rotl(v3, 12) + xh_rotl(v4, 18) : XH5;
+    h += U;
+    const uint8_t* rb = (const uint8_t*)ring;
+    uint32_t p = hns * 16u;
+    for (; p + 4u <= U; p += 4u) {
+        const uint32_t w = (uint32_t)rb[p & kORM] | ((uint32_t)rb[(p + 1u) & kORM] << 8) |
+                           ((uint32_t)rb[(p + 2u) & kORM] << 16) | ((uint32_t)rb[(p + 3u) & kORM] << 24);
+        h = xh_rotl(h + w * XH3, 17) * XH4;
+    }
+    for (; p < U; ++p) h = xh_rotl(h + (uint32_t)rb[p & kORM] * XH5, 11) * XH1;
+    h ^= h >> 15;
+    h *= XH2;
+    h ^= h >> 13;
+    h *= XH3;
+    h ^= h >> 16;
+    return h;
+}
+
+// Small host-walked launches (<= kLbFewBlocks blocks, e.g. the range reader's 256 KiB batches):
+// one 256-thread workgroup per unit runs the token index (k_dtok's algorithm, all four waves),
+// then wave 0 executes the block (k_dexec's) while wave 1 hashes its output from the LDS ring
+// (the frame's content xxh32 when the block is the whole frame: blk_hash, which k_dframe_close
+// takes instead of hashing again). One launch instead of the large-block path's chain; units it
+// does not take are left to k_decode_pe (exact statuses) and get blk_hash 0.
+__global__ __launch_bounds__(fst::kTT) void k_dsmall(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                     const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+                                                     uint32_t nunits, const uint8_t* __restrict__ unit_lb, FastArgs a,
+                                                     uint32_t maxc, uint32_t* __restrict__ blk_out,
+                                                     int32_t* __restrict__ blk_status, uint64_t* __restrict__ blk_hash) {
+    __shared__ __attribute__((aligned(16))) uint32_t ring[fst::kORW];
+    __shared__ uint32_t hsync[2];
+    const uint32_t wv = threadIdx.x >> 6;
+    for (uint32_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+        FastUnit F;
+        const bool ok = dtok_unit(u, src, blk, units, unit_lb, a, maxc, &F);
+        const DecUnit Un = units[u];
+        if (!ok) {
+            if (threadIdx.x == 0 && Un.n == 1 && !(unit_lb && unit_lb[u])) blk_hash[Un.first] = 0;
+            __syncthreads();
+            continue;
+        }
+        if (threadIdx.x == 0) {
+            hsync[0] = 0u;
+            hsync[1] = 0u;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the records are in memory before the barrier
+        __syncthreads();
+        if (wv == 0) {
+            dexec_unit(u, src, dst, blk, units, blk_out, blk_status, a, F, ring, hsync);
+        } else if (wv == 1) {
+            const uint32_t h = hash_ring(ring, hsync, F.U);
+            if ((threadIdx.x & 63u) == 0) blk_hash[Un.first] = (1ull << 32) | h;
+        }
+        __syncthreads();
     }
 }
 
@@ -1136,8 +1369,10 @@ static inline uint32_t fcdiv(uint64_t x, uint64_t y) { return (uint32_t)((x + y 
 hipError_t launch_fast_tok(const uint8_t* src, const DecBlock* blk, const DecUnit* units, uint32_t nunits,
                            const uint64_t* ucount, uint32_t grid, const uint8_t* unit_lb, const FastArgs& a,
                            hipStream_t st) {
-    if (!nunits || !grid) return hipSuccess;
-    hipLaunchKernelGGL(k_dtok, dim3(grid), dim3(fst::kTT), 0, st, src, blk, units, nunits, ucount, unit_lb, a);
+    if (!nunits || !grid || !a.maxc) return hipSuccess;
+    const uint32_t maxc = a.maxc < kFastMaxC ? a.maxc : kFastMaxC;
+    hipLaunchKernelGGL(k_dtok, dim3(grid), dim3(fst::kTT), fast_lds_bytes(maxc), st, src, blk, units, nunits, ucount,
+                       unit_lb, a, maxc);
     return hipGetLastError();
 }
 #ifdef FPROF
@@ -1152,6 +1387,15 @@ extern "C" int s3hc_diag_fprof(unsigned long long* out, int n, int reset) {
     return 0;
 }
 #endif
+hipError_t launch_fast_small(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
+                             uint32_t nunits, const uint8_t* unit_lb, const FastArgs& a, uint32_t* blk_out,
+                             int32_t* blk_status, uint64_t* blk_hash, hipStream_t st) {
+    if (!nunits || !a.maxc) return hipSuccess;
+    const uint32_t maxc = a.maxc < kFastMaxC ? a.maxc : kFastMaxC;
+    hipLaunchKernelGGL(k_dsmall, dim3(nunits), dim3(fst::kTT), fast_lds_bytes(maxc), st, src, dst, blk, units, nunits,
+                       unit_lb, a, maxc, blk_out, blk_status, blk_hash);
+    return hipGetLastError();
+}
 hipError_t launch_fast_exec(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
                             uint32_t nunits, const uint64_t* ucount, uint32_t grid, uint32_t* blk_out,
                             int32_t* blk_status, const FastArgs& a, hipStream_t st) {

@@ -1421,6 +1421,9 @@ constexpr uint32_t kTbl = 1u << kHashLog;
 #ifndef S3HC_STEPS
 #define S3HC_STEPS 8
 #endif
+#ifndef S3HC_LAZY  // diagnostic builds: one-step lazy match selection in the greedy walk
+#define S3HC_LAZY 0
+#endif
 #ifndef S3HC_ENC_MINWAVES
 #define S3HC_ENC_MINWAVES 1
 #endif
@@ -1742,6 +1745,14 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             // per lane: greedy position after taking this lane's match (chunk-relative);
             // 0x1000 marks a match that reached kFwd and needs the wave-wide extension
             const uint32_t nxr = kPS * (uint32_t)lane + flen[q] + (flen[q] == kFwd ? 0x1000u : 0u);
+#if S3HC_LAZY
+            // one-step lazy evaluation: a landing on lane j takes lane j + 1's match instead when
+            // that one is longer (and j's is not a wave-extended one): one literal for >= 2 more
+            // matched bytes; lane j + 1's flen by a wave shift
+            const uint32_t fnext = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)flen[q], 0x130, 0xF, 0xF, false);
+            const bool nxm = ((mm[q] >> (uint32_t)lane) >> 1) & 1ull;
+            const uint64_t lz = __ballot(nxm && flen[q] < kFwd && fnext > flen[q]);
+#endif
             uint32_t r = x > base ? x - base : 0u, rend = 0;
             while (r < kStepPos) {
                 // the first probed position at or after r (a probe after r reaches back to it)
@@ -1749,7 +1760,12 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
                 if (j0 >= 64u) break;
                 const uint64_t av = mm[q] & (~0ull << j0);
                 if (!av) break;
+#if S3HC_LAZY
+                uint32_t j = (uint32_t)__builtin_ctzll(av);
+                j += (uint32_t)(lz >> j) & 1u;
+#else
                 const uint32_t j = (uint32_t)__builtin_ctzll(av);
+#endif
                 hm |= 1ull << j;
                 r = rdl(nxr, j);
                 if (r & 0x1000u) {  // long match: wave-wide forward extension

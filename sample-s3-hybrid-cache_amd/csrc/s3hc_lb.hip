@@ -301,8 +301,8 @@ __global__ __launch_bounds__(1024) void k_lb_classify(const DecBlock* __restrict
                 bi = U.first;
                 B = blk[bi];
                 A.blk_hash[bi] = 0;  // k_lb_run sets it for the blocks it decodes
-                cand = !(B.flags & (DB_STORED | DB_LINKED)) && B.limit >= A.min_limit && B.csize > 0 &&
-                       B.limit <= kLbMaxSteps * kLbStep;
+                cand = !(B.flags & (DB_STORED | DB_LINKED)) && (B.limit >= A.min_limit || B.csize > A.big_csize) &&
+                       B.csize > 0 && B.limit <= kLbMaxSteps * kLbStep;
             }
         }
         const uint32_t nch = cand ? (B.csize + kLbChunk - 1) / kLbChunk : 0u;

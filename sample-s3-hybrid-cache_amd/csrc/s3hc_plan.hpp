@@ -152,6 +152,9 @@ struct LbArgs {
     uint32_t wcap;         // spread execution: positions of P (0: every block runs the step loop)
     uint32_t tile_cap;     // spread execution: tiles (kLbStep output bytes) of the spread blocks, at most
     uint32_t all_spread;   // the host's bounds show every taken block runs spread: no k_lb_run launch
+    uint32_t big_csize;    // a block of a frame allowing <= min_limit takes the path anyway when its
+                           // compressed size exceeds this (small launches: blocks the fused fast
+                           // path k_dsmall cannot take; 0xFFFFFFFF = never)
     LbBlock* lbt;
     LbCtl* ctl;
     uint8_t* unit_lb;      // per unit: 1 = decoded by this path
@@ -203,11 +206,18 @@ struct FastUnit {        // 16 bytes, written by k_dtok for every unit it takes
     uint32_t pad0, pad1;
 };
 
+// k_dtok's dynamic LDS for blocks of at most maxc compressed bytes: the staged block (16-byte
+// alignment slack + zero read-ahead) and one bitmap bit per compressed position
+constexpr uint32_t fast_stage_bytes(uint32_t maxc) { return (maxc + 64u + 15u) & ~15u; }
+constexpr uint32_t fast_lds_bytes(uint32_t maxc) { return fast_stage_bytes(maxc) + 4u * ((maxc + 31u) / 32u + 1u); }
+
 struct FastArgs {
     uint2* rec;          // per block, at DecBlock::tok: the block's sequence records in stream order,
                          // {lit | ll << 15, off | (ml - 4) << 16} (off = 0: the last, match-less one)
     FastUnit* fu;        // per unit
     uint8_t* unit_fast;  // per unit: 1 = decoded by the fast path
+    uint32_t maxc;       // largest compressed block of the launch (<= kFastMaxC: sizes k_dtok's LDS);
+                         // 0 = no block for the fast path
 };
 
 }  // namespace s3hc

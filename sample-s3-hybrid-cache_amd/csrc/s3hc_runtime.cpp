@@ -39,6 +39,8 @@ hipError_t launch_fast_tok(const uint8_t*, const DecBlock*, const DecUnit*, uint
                            const uint8_t*, const FastArgs&, hipStream_t);
 hipError_t launch_fast_exec(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*,
                             uint32_t, uint32_t*, int32_t*, const FastArgs&, hipStream_t);
+hipError_t launch_fast_small(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint8_t*,
+                             const FastArgs&, uint32_t*, int32_t*, uint64_t*, hipStream_t);
 hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*,
                            uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, uint32_t*, int32_t*, hipStream_t);
@@ -151,6 +153,21 @@ struct PinnedBuf {
         hipError_t e = hipHostMalloc((void**)&p, want, hipHostMallocDefault);
         if (e == hipSuccess) cap = want;
         return e;
+    }
+    // grow to n bytes keeping the first `keep` (no copy into the buffer may be in flight)
+    hipError_t ensure_keep(size_t n, size_t keep) {
+        if (n <= cap) return hipSuccess;
+        uint8_t* q = nullptr;
+        const size_t want = std::max<size_t>(n, 1 << 16);
+        hipError_t e = hipHostMalloc((void**)&q, want, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        if (p) {
+            memcpy(q, p, std::min(keep, cap));
+            (void)hipHostFree(p);
+        }
+        p = q;
+        cap = want;
+        return hipSuccess;
     }
 };
 
@@ -350,6 +367,7 @@ struct HostStage {
 struct LbCaps {
     uint32_t lb = 0, chunks = 0;
     uint32_t min_limit = kLbMinLimit;
+    uint32_t big_csize = 0xFFFFFFFFu;  // (LbArgs::big_csize)
     uint64_t outb = 0;  // decoded bytes of the candidate blocks, at most (sizes the spread execution)
     bool exact = false; // lb is the candidate count itself (host walk), not a bound (device plans)
     uint32_t nbig = 0;  // candidates of frames that allow more than 64 KiB (the spread ones; exact only)
@@ -362,8 +380,9 @@ struct LbCaps {
         }
     }
 };
-static bool lb_candidate(const DecBlock& D, bool unit_single, uint32_t min_limit) {
-    return unit_single && !(D.flags & (DB_STORED | DB_LINKED)) && D.limit >= min_limit && D.csize > 0 &&
+static bool lb_candidate(const DecBlock& D, bool unit_single, uint32_t min_limit, uint32_t big_csize = 0xFFFFFFFFu) {
+    return unit_single && !(D.flags & (DB_STORED | DB_LINKED)) && (D.limit >= min_limit || D.csize > big_csize) &&
+           D.csize > 0 &&
            D.limit <= kLbMaxSteps * kLbStep;
 }
 
@@ -373,12 +392,19 @@ struct LbScratch {
     LbArgs a{};
     // 64 KiB-block fast path (s3hc_fast.hip): per-unit token bitmaps and results
     DevBuf f_bmp, f_fu, f_unit_fast;  // (f_bmp: sequence records)
+    DevBuf f_hash;                     // small launches without the large-block path: per-block hashes
     FastArgs fa{};
     bool fast_ready = false;
+    // small launch (host-walked, <= kLbFewBlocks blocks): 64 KiB blocks run the fused k_dsmall
+    // (token index + executor + content xxh32 in one workgroup per block) instead of the
+    // large-block chain; set by small_caps()
+    bool small = false;
     // tok_entries: the launch's token-slot entries (DecBlock::tok + tok_slot_entries(csize) of
     // every block stays below it; sized by compressed bytes, not by a per-unit maximum)
-    hipError_t prepare_fast(uint32_t nunits, uint64_t tok_entries) {
+    // maxc: the largest compressed block the launch may hand the fast path (sizes k_dtok's LDS)
+    hipError_t prepare_fast(uint32_t nunits, uint64_t tok_entries, uint64_t maxc) {
         fast_ready = false;
+        fa.maxc = (uint32_t)std::min<uint64_t>(maxc, kFastMaxC);
         if (!nunits || tok_entries > 0xFFFFFFF0ull) return hipSuccess;  // (u32 slots: the fast path sits out)
         hipError_t e;
         if ((e = f_bmp.ensure((size_t)tok_entries * sizeof(uint2) + 256)) != hipSuccess) return e;
@@ -423,6 +449,7 @@ struct LbScratch {
         a.lb_cap = c.lb;
         a.chunk_cap = c.chunks;
         a.min_limit = c.min_limit;
+        a.big_csize = c.big_csize;
         a.lbt = lbt.as<LbBlock>(); a.ctl = ctl.as<LbCtl>(); a.unit_lb = unit_lb.as<uint8_t>();
         a.chunk_blk = chunk_blk.as<uint32_t>(); a.nzg = nzg.as<uint32_t>(); a.E = E.as<uint32_t>(); a.J0 = J0.as<uint16_t>();
         a.entry = entry.as<uint32_t>(); a.trec = trec.as<uint4>(); a.ntok = ntok.as<uint32_t>();
@@ -446,15 +473,49 @@ struct LbScratch {
     }
 };
 
-// Token-position slots of host-built block tables: consecutive per block, sized by compressed
-// bytes (s3hc_plan.hpp tok_slot_entries). Returns the launch's entries.
+static uint64_t max_csize(const DecBlock* b, size_t n) {
+    uint64_t m = 0;
+    for (size_t i = 0; i < n; ++i) m = std::max<uint64_t>(m, b[i].csize);
+    return m;
+}
+
+// Sequence-record slots of host-built block tables: consecutive per block, sized by compressed
+// bytes (s3hc_plan.hpp tok_slot_entries), each starting on a 128-byte line (16 records): k_dsmall
+// writes a block's records and reads them back in the same launch, so no two blocks may share a
+// cache line. Returns the launch's entries.
 static uint64_t assign_tok_slots(DecBlock* b, size_t n) {
     uint64_t t = 0;
     for (size_t i = 0; i < n; ++i) {
         b[i].tok = (uint32_t)std::min<uint64_t>(t, 0xFFFFFFFFull);
-        t += tok_slot_entries(b[i].csize);
+        t += (tok_slot_entries(b[i].csize) + 15u) & ~15ull;
     }
     return t;
+}
+
+// Scratch and routing of a host-walked decode launch. Small launches (<= kLbFewBlocks blocks):
+// with the fast path on, 64 KiB blocks it can take run k_dsmall (one fused launch); every other
+// compressed block (frames allowing more than 64 KiB, blocks above kFastMaxC compressed bytes)
+// runs the large-block path. Without the fast path every compressed block of a small launch
+// takes the large-block path (many workgroups per block). Larger launches: large blocks only.
+static hipError_t prepare_host_launch(LbScratch& L, const DecBlock* blocks, size_t nb, const DecUnit* units,
+                                      uint32_t nu, uint64_t tok_entries) {
+    LbCaps lc;
+    lc.exact = true;
+    const bool few = nb <= kLbFewBlocks;
+    const bool small = few && !knob_on(KN_FAST_DISABLE) && !knob_on(KN_LB_DISABLE);
+    if (small) lc.big_csize = kFastMaxC;
+    else if (few) lc.min_limit = 1;  // few blocks: all of them on many workgroups
+    for (uint32_t k = 0; k < nu; ++k) {
+        const DecBlock& D = blocks[units[k].first];
+        if (lb_candidate(D, units[k].n == 1, lc.min_limit, lc.big_csize))
+            lc.add_block(D.csize, std::min(D.limit, D.cap), D.limit);
+    }
+    hipError_t e;
+    if ((e = L.prepare(nu, (uint32_t)nb, lc)) != hipSuccess) return e;
+    if ((e = L.prepare_fast(nu, tok_entries, max_csize(blocks, nb))) != hipSuccess) return e;
+    L.small = small && L.fast_ready;
+    if (L.small && !L.active && (e = L.f_hash.ensure(nb * 8 + 64)) != hipSuccess) return e;
+    return hipSuccess;
 }
 
 // The 64 KiB-block fast path (k_dtok + k_dexec) is on by default; the knob
@@ -480,7 +541,15 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
     // 64 KiB blocks: token index + executor (S3HC_FAST_DISABLE=1: every block on the per-unit
     // decoder, for comparisons); blocks the fast path leaves go to the per-unit decoder below
     const bool fast = L && L->fast_ready && nunits && !(lb && L->all_lb) && fast_path_enabled();
-    if (fast) {
+    if (fast && L->small) {
+        // small host-walked launch: token index + executor + content xxh32 in one launch; the
+        // frame close takes its hashes (blk_hash) like the large-block path's
+        uint64_t* hb = lb ? L->a.blk_hash : L->f_hash.as<uint64_t>();
+        if (blk_hash) *blk_hash = hb;
+        if ((e = launch_fast_small(src, dst, blk, units, nunits, lb ? L->a.unit_lb : nullptr, L->fa, blk_out,
+                                   blk_status, hb, st)) != hipSuccess)
+            return e;
+    } else if (fast) {
         if ((e = launch_fast_tok(src, blk, units, nunits, ucount, grid, lb ? L->a.unit_lb : nullptr, L->fa, st)) !=
             hipSuccess)
             return e;
@@ -900,9 +969,10 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
         // per 64 KiB of each frame's room (frames of several independent blocks keep their
         // parallelism; the grid still strides over any extra units)
         std::vector<uint64_t> ftok(n);
-        uint64_t tok_entries = 0, grid = 0;
+        uint64_t tok_entries = 0, grid = 0, max_frame_len = 0;
         for (uint32_t i = 0; i < n; ++i) {
             ftok[i] = tok_entries;
+            max_frame_len = std::max<uint64_t>(max_frame_len, frame_len[i]);  // (a block is shorter than its frame)
             tok_entries += tok_frame_entries(frame_len[i]);
             grid += std::max<uint64_t>(1, (dst_cap[i] + 65535u) / 65536u);
         }
@@ -943,7 +1013,8 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
             }
         }
         HIPCHK(P->lb.prepare(P->blk_cap, P->blk_cap, lc));
-        HIPCHK(P->lb.prepare_fast(P->blk_cap, tok_entries));
+        HIPCHK(P->lb.prepare_fast(P->blk_cap, tok_entries, max_frame_len));
+        P->lb.small = false;
         HIPCHK(hipStreamSynchronize(st));
         *out = P.release();
         return S3HC_OK;
@@ -1178,7 +1249,10 @@ static int parse_header_h(const uint8_t* p, size_t avail, uint32_t* flg, uint32_
 
 // Walk frames from src; `stream_mode` = stream_range_data semantics (an incomplete final
 // frame is left for later instead of being an error; an empty frame does not stop).
-static void walk_frames(const uint8_t* src, size_t n, HWalk& W, bool allow_incomplete, bool stop_on_empty) {
+// stop_after: the walk ends after the first complete frame that ends at or past this byte (a
+// range reader batch needs no more; default: walk everything)
+static void walk_frames(const uint8_t* src, size_t n, HWalk& W, bool allow_incomplete, bool stop_on_empty,
+                        size_t stop_after = ~(size_t)0) {
     const bool stream_mode = allow_incomplete;
     size_t pos = 0;
     while (pos < n) {
@@ -1198,9 +1272,9 @@ static void walk_frames(const uint8_t* src, size_t n, HWalk& W, bool allow_incom
         uint64_t slot = 0;
         int st = S3HC_OK;
         bool complete = false;
-        std::vector<DecBlock> fb;
-        std::vector<uint32_t> fcs;
-        std::vector<uint8_t> fhas;
+        // blocks go straight into W (rolled back when the frame turns out incomplete in
+        // stream mode): no per-frame allocations on the range reader's per-batch path
+        const size_t b0 = W.blocks.size();
         for (;;) {
             if (n - ip < 4) { st = S3HC_CORRUPT; break; }
             uint32_t w = rd32h(src + ip);
@@ -1230,22 +1304,24 @@ static void walk_frames(const uint8_t* src, size_t n, HWalk& W, bool allow_incom
             D.cap = (uint32_t)std::min<uint64_t>(D.limit, 255ull * len);
             D.flags = ((w & kStoredBit) ? DB_STORED : 0u) | (linked ? DB_LINKED : 0u);
             D.frame = (uint32_t)W.frames.size();
-            fb.push_back(D);
-            fhas.push_back((F.flg & 0x10) ? 1 : 0);
-            fcs.push_back((F.flg & 0x10) ? rd32h(src + ip + len) : 0);
+            W.blocks.push_back(D);
+            W.blk_has_cs.push_back((F.flg & 0x10) ? 1 : 0);
+            W.blk_cs_want.push_back((F.flg & 0x10) ? rd32h(src + ip + len) : 0);
             slot += D.cap;
             ip += need;
         }
         if (!complete) {
-            if (stream_mode && st == S3HC_CORRUPT) break;  // wait for more bytes
+            if (stream_mode && st == S3HC_CORRUPT) {  // wait for more bytes
+                W.blocks.resize(b0);
+                W.blk_has_cs.resize(b0);
+                W.blk_cs_want.resize(b0);
+                break;
+            }
             // Blocks before the failure still decode (their errors come first in order).
             W.tail_status = st;
             W.last_incomplete = true;
         }
-        F.nblk = (uint32_t)fb.size();
-        W.blocks.insert(W.blocks.end(), fb.begin(), fb.end());
-        W.blk_cs_want.insert(W.blk_cs_want.end(), fcs.begin(), fcs.end());
-        W.blk_has_cs.insert(W.blk_has_cs.end(), fhas.begin(), fhas.end());
+        F.nblk = (uint32_t)(W.blocks.size() - b0);
         W.slot_total += slot;
         W.frames.push_back(F);
         if (!complete) return;
@@ -1255,6 +1331,7 @@ static void walk_frames(const uint8_t* src, size_t n, HWalk& W, bool allow_incom
             W.stopped_empty = true;
             return;
         }
+        if (pos >= stop_after) return;
     }
 }
 
@@ -1316,13 +1393,7 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         HIPCHK(upload(ctx->d_units, units, st));
         HIPCHK(ctx->d_blk_out.ensure(nb * 4));
         HIPCHK(ctx->d_blk_status.ensure(nb * 4));
-        LbCaps lc;
-        if (W.blocks.size() <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
-        lc.exact = true;
-        for (auto& U : units)
-            if (lb_candidate(W.blocks[U.first], U.n == 1, lc.min_limit)) lc.add_block(W.blocks[U.first].csize, std::min(W.blocks[U.first].limit, W.blocks[U.first].cap), W.blocks[U.first].limit);
-        HIPCHK(ctx->lb.prepare((uint32_t)units.size(), (uint32_t)nb, lc));
-        HIPCHK(ctx->lb.prepare_fast((uint32_t)units.size(), tok_entries));
+        HIPCHK(prepare_host_launch(ctx->lb, W.blocks.data(), nb, units.data(), (uint32_t)units.size(), tok_entries));
         const uint64_t* bh = nullptr;
         HTRACE("launch")
         HIPCHK(decode_launch(&ctx->lb, ctx->d_in.as<uint8_t>(), ctx->d_out.as<uint8_t>(), ctx->d_blocks.as<DecBlock>(),
@@ -1901,6 +1972,8 @@ struct RSlot {
     uint32_t good = 0;      // frames before the first failing one
     uint64_t out_len = 0;   // bytes in h_out
     uint64_t out_pos = 0;   // bytes already read
+    uint64_t spec = 0;      // decoded-slot prefix copied to h_out right behind the decode (one round trip)
+    bool covered = false;   // the good frames' bytes lie in that prefix: no second copy
 };
 }  // namespace
 
@@ -1979,13 +2052,7 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     HIPCHK(S.d_blk_status.ensure(4ull * nbk + 16));
     {
         // large blocks of the batch (the host walk knows every block)
-        LbCaps lc;
-        if (nbk <= kLbFewBlocks) lc.min_limit = 1;  // few blocks: all of them on many workgroups
-        lc.exact = true;
-        for (auto& U : units)
-            if (lb_candidate(mb[U.first], U.n == 1, lc.min_limit)) lc.add_block(mb[U.first].csize, std::min(mb[U.first].limit, mb[U.first].cap), mb[U.first].limit);
-        HIPCHK(S.lb.prepare(nu, nbk, lc));
-        HIPCHK(S.lb.prepare_fast(nu, tok_entries));
+        HIPCHK(prepare_host_launch(S.lb, mb, nbk, units.data(), nu, tok_entries));
     }
     HIPCHK(S.h_res.ensure(8ull * n));
     HIPCHK(hipMemcpyAsync(S.d_in.p, S.h_in.p, nin, hipMemcpyHostToDevice, st));
@@ -2008,9 +2075,16 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
                                (const uint32_t*)(dm + o_w), n, nullptr, d_st, d_olen, nullptr, st));
     T.end();
     HIPCHK(hipMemcpyAsync(S.h_res.p, S.d_res.p, 8ull * n, hipMemcpyDeviceToHost, st));
+    // speculative copy of the decoded slots behind the decode, in the same round trip: frames of
+    // 64 KiB blocks fill their slots, so the prefix is the batch's output; a frame whose slot is
+    // its block capacity (BD 0x70: 4 MiB) only gets the prefix a 4:1 ratio can fill
+    S.spec = std::min<uint64_t>(slot, std::max<uint64_t>(4ull * nin, 1ull << 20));
+    HIPCHK(S.h_out.ensure(S.spec + 16));
+    HIPCHK(hipMemcpyAsync(S.h_out.p, S.d_out.p, S.spec, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(S.ev, st));
     S.state = 0;
     S.ready = false;
+    S.covered = false;
     r->in_head += end;
     return S3HC_OK;
 }
@@ -2026,12 +2100,13 @@ static int reader_pump(s3hc_reader* r) {
         const size_t want = r->inflight.empty() ? r->batch_bytes : r->batch_max;
         const size_t lim = std::min(avail, want + ((size_t)8 << 20));
         HWalk W;
-        walk_frames(r->in.data() + r->in_head, lim, W, true, false);
+        // frames up to `want` bytes and one past it: the batch never takes more
+        walk_frames(r->in.data() + r->in_head, lim, W, true, false, want);
         size_t nf = W.frames.size();
         if (nf && W.last_incomplete) nf--;  // (stream mode leaves incomplete frames unwalked)
         if (nf == 0 && lim < avail) {
             W = HWalk();
-            walk_frames(r->in.data() + r->in_head, avail, W, true, false);
+            walk_frames(r->in.data() + r->in_head, avail, W, true, false, want);
             nf = W.frames.size();
             if (nf && W.last_incomplete) nf--;
         }
@@ -2071,11 +2146,27 @@ static int reader_issue_copy(RSlot& S) {
     uint32_t good = 0;
     uint64_t bytes = 0;
     while (good < S.n && st[good] == S3HC_OK) bytes += olen[good++];
-    HIPCHK(S.h_out.ensure(bytes + 16));
     // frames decode into slots of their block capacity; when every frame but the last filled
-    // its slot (the normal case) the good output is already contiguous: one copy
+    // its slot (the normal case) the good output is already contiguous: one copy, or none when
+    // the speculative prefix already holds it
     bool packed = true;
     for (uint32_t f = 0; f + 1 < good; ++f) packed &= S.dst_off[f] + olen[f] == S.dst_off[f + 1];
+    S.good = good;
+    S.out_len = bytes;
+    S.out_pos = 0;
+    S.state = 1;
+    if (packed && bytes <= S.spec) {
+        S.covered = true;
+        return S3HC_OK;
+    }
+    if (packed && S.spec) {  // the rest beyond the prefix (h_out keeps the prefix it holds)
+        HIPCHK(S.h_out.ensure_keep(bytes + 16, S.spec));
+        HIPCHK(hipMemcpyAsync(S.h_out.p + S.spec, S.d_out.as<uint8_t>() + S.spec, bytes - S.spec,
+                              hipMemcpyDeviceToHost, S.st));
+        HIPCHK(hipEventRecord(S.ev2, S.st));
+        return S3HC_OK;
+    }
+    HIPCHK(S.h_out.ensure(bytes + 16));
     if (packed) {
         if (bytes) HIPCHK(hipMemcpyAsync(S.h_out.p, S.d_out.p, bytes, hipMemcpyDeviceToHost, S.st));
     } else {
@@ -2087,12 +2178,9 @@ static int reader_issue_copy(RSlot& S) {
         }
     }
     HIPCHK(hipEventRecord(S.ev2, S.st));
-    S.good = good;
-    S.out_len = bytes;
-    S.out_pos = 0;
-    S.state = 1;
     return S3HC_OK;
 }
+static bool reader_copy_done(RSlot& S) { return S.state == 1 && (S.covered || hipEventQuery(S.ev2) == hipSuccess); }
 
 // Queue the D2H of every batch whose decode has finished (any order: separate queues).
 static int reader_advance(s3hc_reader* r) {
@@ -2114,7 +2202,7 @@ static int reader_complete(s3hc_reader* r) {
         int rc = reader_issue_copy(S);
         if (rc) return rc;
     }
-    HIPCHK(hipEventSynchronize(S.ev2));
+    if (!S.covered) HIPCHK(hipEventSynchronize(S.ev2));
     S.state = 2;
     S.ready = true;
     r->total += S.out_len;
@@ -2245,7 +2333,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
             // the oldest batch is still running: wait for it only when the pipeline is full, the
             // input is finished or it is already done; otherwise ask the caller for more input
             RSlot& H = r->slots[r->inflight.front()];
-            const bool done = H.state == 1 && hipEventQuery(H.ev2) == hipSuccess;
+            const bool done = reader_copy_done(H);
             if (!done && r->inflight.size() < r->slots.size() && !r->finished && !r->error) return S3HC_OK;
             int rc = reader_complete(r);
             if (rc) return rc;

@@ -105,3 +105,16 @@ def test_reader_large_object_4mib_feeds(engine, policy, batch, batch_max):
         else engine.compress_frame(data, 1)
     out, r = _run(engine, frames, 4 * MiB, batch, 3, batch_max=batch_max)
     assert len(out) == len(data) and out == data
+
+
+@pytest.mark.parametrize("item", [65536, MiB])
+def test_reader_output_beyond_speculative_prefix(engine, oracle, item):
+    # zeros and byte runs compress far below 4:1, so a batch decodes to more than the prefix the
+    # reader copies back right behind the decode (max(4 x input, 1 MiB)): the rest takes a second
+    # copy; 64 KiB blocks of zeros also run k_dsmall's longest overlapping matches
+    data = bytes(6 * MiB) + synth.log_text(MiB, 46) + b"\x07" * (3 * MiB + 5)
+    frames = b"".join(oracle.lz4flex_compress_frame(data[i:i + item]) for i in range(0, len(data), item))
+    for batch, depth in ((256 << 10, 3), (4 << 20, 2), (1, 1)):
+        out, r = _run(engine, frames, 4 * MiB, batch, depth)
+        assert out == data, (batch, depth)
+        assert r.total == len(data)
