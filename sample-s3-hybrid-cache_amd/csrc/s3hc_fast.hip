@@ -820,7 +820,9 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
     };
     auto hpub = [&](uint32_t done) {
         if (hsync) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            // the ring bytes before the progress word (LDS only: a workgroup-scope fence would
+            // also drain this wave's global prefetches)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) hsync[0] = done;
         }
     };
@@ -1287,7 +1289,7 @@ __device__ __forceinline__ uint32_t hash_ring(const uint32_t* ring, volatile uin
     uint32_t hs = 0;
     for (;;) {
         const uint32_t avail = hsync[0];
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const uint32_t lim = umin_(avail >> 4, hns);
         for (; hs + 16u <= lim; hs += 16u) {
             const uint32_t mv = ring[((16u * hs + 4u * lane) & kORM) >> 2] * XH2;
@@ -1298,7 +1300,7 @@ __device__ __forceinline__ uint32_t hash_ring(const uint32_t* ring, volatile uin
             for (uint32_t k = 0; k < 16; ++k) hacc = xh_rotl(hacc + m[k], 13) * XH1;
         }
         for (; hs < lim; ++hs) hacc = xh_round(hacc, ring[((16u * hs + 4u * ha) & kORM) >> 2]);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (ring reads done before the slots are released)
         if (lane == 0) hsync[1] = 16u * hs;
         if (avail >= U) break;
         __builtin_amdgcn_s_sleep(2);

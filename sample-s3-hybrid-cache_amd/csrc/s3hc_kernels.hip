@@ -1421,6 +1421,9 @@ constexpr uint32_t kTbl = 1u << kHashLog;
 #ifndef S3HC_STEPS
 #define S3HC_STEPS 8
 #endif
+#ifndef S3HC_SHORT_GATE  // diagnostic builds: distance-1..4 candidate only without a verified table one
+#define S3HC_SHORT_GATE 0
+#endif
 #ifndef S3HC_LAZY  // diagnostic builds: one-step lazy match selection in the greedy walk
 #define S3HC_LAZY 0
 #endif
@@ -1710,7 +1713,14 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
 #endif
             // the distance-1..4 candidate is measured only where the table candidate is absent
             // or shorter than S3HC_SHORT_MIN bytes (a long table match is kept as is)
+#if S3HC_SHORT_GATE
+            // the distance-1..4 candidate only where the table has no verified candidate (a run's
+            // first positions: inside a run the table candidate lies in the run and measures the
+            // same); the step's ballot then fires far less often
+            const bool want_short = valid & (e1 | e2 | e3 | e4) & !gt;
+#else
             const bool want_short = valid & (e1 | e2 | e3 | e4) & !(gt & (lt >= S3HC_SHORT_MIN));
+#endif
             if (S3HC_SHORT_CAND == 1 && __ballot(want_short)) {
                 const uint32_t df = (e1 & (i >= 1)) ? 1u : ((e2 & (i >= 2)) ? 2u : ((e3 & (i >= 3)) ? 3u : ((e4 & (i >= 4)) ? 4u : 0u)));
                 gf = want_short & (df != 0);

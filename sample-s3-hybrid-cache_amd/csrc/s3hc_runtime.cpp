@@ -1961,8 +1961,8 @@ namespace {
 struct RSlot {
     hipStream_t st = nullptr;
     hipEvent_t ev = nullptr;
-    PinnedBuf h_in, h_meta, h_res, h_out;
-    DevBuf d_in, d_out, d_meta, d_res, d_blk_out, d_blk_status;
+    PinnedBuf h_in, h_out;  // h_in: input + tables; h_out: frame results + decoded slots
+    DevBuf d_in, d_out, d_blk_out, d_blk_status;
     LbScratch lb;
     uint32_t n = 0;
     std::vector<uint64_t> dst_off;
@@ -1974,6 +1974,8 @@ struct RSlot {
     uint64_t out_pos = 0;   // bytes already read
     uint64_t spec = 0;      // decoded-slot prefix copied to h_out right behind the decode (one round trip)
     bool covered = false;   // the good frames' bytes lie in that prefix: no second copy
+    uint64_t R = 0;         // d_out / h_out: frame results (u32 lengths, i32 statuses) in [0, R), slots after
+    int32_t err = 0;        // status of the first failing frame (good < n)
 };
 }  // namespace
 
@@ -2021,8 +2023,10 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     const size_t o_fo = 0, o_bb = al(8ull * n), o_oo = o_bb + al(8ull * n), o_nb = o_oo + al(8ull * n),
                  o_w = o_nb + al(4ull * n), o_blk = o_w + al(4ull * n), o_u = o_blk + al(sizeof(DecBlock) * nbk),
                  nmeta = o_u + al(sizeof(DecUnit) * nu);
-    HIPCHK(S.h_meta.ensure(nmeta));
-    uint8_t* m = S.h_meta.p;
+    // one host-to-device copy per batch: the input, then (256-byte aligned) the tables
+    const size_t o_meta = (nin + 255) & ~(size_t)255;
+    HIPCHK(S.h_in.ensure(o_meta + nmeta));
+    uint8_t* m = S.h_in.p + o_meta;
     for (uint32_t f = 0; f < n; ++f) {
         const HFrame& F = W.frames[f];
         ((uint64_t*)(m + o_fo))[f] = F.pos - F0.pos;
@@ -2042,45 +2046,42 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     const uint64_t tok_entries = assign_tok_slots(mb, nbk);
     if (nu) memcpy(m + o_u, units.data(), sizeof(DecUnit) * nu);
     hipStream_t st = S.st;
-    HIPCHK(S.h_in.ensure(nin));
     par_memcpy(S.h_in.p, r->in.data() + r->in_head + F0.pos, nin);
-    HIPCHK(S.d_in.ensure(nin + 64));
-    HIPCHK(S.d_out.ensure(slot + 64));
-    HIPCHK(S.d_meta.ensure(nmeta + 64));
-    HIPCHK(S.d_res.ensure(8ull * n + 64));
+    HIPCHK(S.d_in.ensure(o_meta + nmeta + 64));
+    // one device-to-host copy per batch: the frame results, then (256-byte aligned) the slots
+    S.R = (8ull * n + 255) & ~255ull;
+    HIPCHK(S.d_out.ensure(S.R + slot + 64));
     HIPCHK(S.d_blk_out.ensure(4ull * nbk + 16));
     HIPCHK(S.d_blk_status.ensure(4ull * nbk + 16));
     {
         // large blocks of the batch (the host walk knows every block)
         HIPCHK(prepare_host_launch(S.lb, mb, nbk, units.data(), nu, tok_entries));
     }
-    HIPCHK(S.h_res.ensure(8ull * n));
-    HIPCHK(hipMemcpyAsync(S.d_in.p, S.h_in.p, nin, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(S.d_meta.p, S.h_meta.p, nmeta, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.d_in.p, S.h_in.p, o_meta + nmeta, hipMemcpyHostToDevice, st));
     const uint8_t* src = S.d_in.as<uint8_t>();
-    const uint8_t* dm = S.d_meta.as<uint8_t>();
+    const uint8_t* dm = S.d_in.as<uint8_t>() + o_meta;
     const DecBlock* d_blk = (const DecBlock*)(dm + o_blk);
-    uint32_t* d_olen = S.d_res.as<uint32_t>();
-    int32_t* d_st = (int32_t*)(S.d_res.as<uint8_t>() + 4ull * n);
+    uint32_t* d_olen = S.d_out.as<uint32_t>();
+    int32_t* d_st = (int32_t*)(S.d_out.as<uint8_t>() + 4ull * n);
+    uint8_t* d_slots = S.d_out.as<uint8_t>() + S.R;
     KTimer T(r->ctx, st);
     T.begin("decode");
     const uint64_t* bh = nullptr;
-    HIPCHK(decode_launch(&S.lb, src, S.d_out.as<uint8_t>(), d_blk, (const DecUnit*)(dm + o_u), nu,
+    HIPCHK(decode_launch(&S.lb, src, d_slots, d_blk, (const DecUnit*)(dm + o_u), nu,
                          S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), st, &bh));
     T.end();
     T.begin("dec_close");
     HIPCHK(launch_dframe_close(src, (const uint64_t*)(dm + o_fo), (const uint64_t*)(dm + o_bb),
                                (const uint32_t*)(dm + o_nb), d_blk, S.d_blk_out.as<uint32_t>(),
-                               S.d_blk_status.as<int32_t>(), bh, S.d_out.as<uint8_t>(), (const uint64_t*)(dm + o_oo),
+                               S.d_blk_status.as<int32_t>(), bh, d_slots, (const uint64_t*)(dm + o_oo),
                                (const uint32_t*)(dm + o_w), n, nullptr, d_st, d_olen, nullptr, st));
     T.end();
-    HIPCHK(hipMemcpyAsync(S.h_res.p, S.d_res.p, 8ull * n, hipMemcpyDeviceToHost, st));
     // speculative copy of the decoded slots behind the decode, in the same round trip: frames of
     // 64 KiB blocks fill their slots, so the prefix is the batch's output; a frame whose slot is
     // its block capacity (BD 0x70: 4 MiB) only gets the prefix a 4:1 ratio can fill
     S.spec = std::min<uint64_t>(slot, std::max<uint64_t>(4ull * nin, 1ull << 20));
-    HIPCHK(S.h_out.ensure(S.spec + 16));
-    HIPCHK(hipMemcpyAsync(S.h_out.p, S.d_out.p, S.spec, hipMemcpyDeviceToHost, st));
+    HIPCHK(S.h_out.ensure(S.R + S.spec + 16));
+    HIPCHK(hipMemcpyAsync(S.h_out.p, S.d_out.p, S.R + S.spec, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(S.ev, st));
     S.state = 0;
     S.ready = false;
@@ -2141,11 +2142,13 @@ static int reader_pump(s3hc_reader* r) {
 // Decode of slot S finished: queue the D2H of its good frames' bytes (stream order) into its
 // pinned output buffer. A failing frame ends the stream after them (applied when S is the head).
 static int reader_issue_copy(RSlot& S) {
-    const uint32_t* olen = (const uint32_t*)S.h_res.p;
-    const int32_t* st = (const int32_t*)(S.h_res.p + 4ull * S.n);
+    // (the results head h_out; olen is copied before h_out may be reallocated below)
+    std::vector<uint32_t> olen((const uint32_t*)S.h_out.p, (const uint32_t*)S.h_out.p + S.n);
+    const int32_t* st = (const int32_t*)(S.h_out.p + 4ull * S.n);
     uint32_t good = 0;
     uint64_t bytes = 0;
     while (good < S.n && st[good] == S3HC_OK) bytes += olen[good++];
+    S.err = good < S.n ? st[good] : 0;
     // frames decode into slots of their block capacity; when every frame but the last filled
     // its slot (the normal case) the good output is already contiguous: one copy, or none when
     // the speculative prefix already holds it
@@ -2159,20 +2162,19 @@ static int reader_issue_copy(RSlot& S) {
         S.covered = true;
         return S3HC_OK;
     }
-    if (packed && S.spec) {  // the rest beyond the prefix (h_out keeps the prefix it holds)
-        HIPCHK(S.h_out.ensure_keep(bytes + 16, S.spec));
-        HIPCHK(hipMemcpyAsync(S.h_out.p + S.spec, S.d_out.as<uint8_t>() + S.spec, bytes - S.spec,
-                              hipMemcpyDeviceToHost, S.st));
+    const uint8_t* d_slots = S.d_out.as<uint8_t>() + S.R;
+    if (packed) {  // the rest beyond the prefix (h_out keeps the results and the prefix it holds)
+        HIPCHK(S.h_out.ensure_keep(S.R + bytes + 16, S.R + S.spec));
+        HIPCHK(hipMemcpyAsync(S.h_out.p + S.R + S.spec, d_slots + S.spec, bytes - S.spec, hipMemcpyDeviceToHost,
+                              S.st));
         HIPCHK(hipEventRecord(S.ev2, S.st));
         return S3HC_OK;
     }
-    HIPCHK(S.h_out.ensure(bytes + 16));
-    if (packed) {
-        if (bytes) HIPCHK(hipMemcpyAsync(S.h_out.p, S.d_out.p, bytes, hipMemcpyDeviceToHost, S.st));
-    } else {
+    HIPCHK(S.h_out.ensure(S.R + bytes + 16));
+    {
         uint64_t o = 0;
         for (uint32_t f = 0; f < good; ++f) {
-            if (olen[f]) HIPCHK(hipMemcpyAsync(S.h_out.p + o, S.d_out.as<uint8_t>() + S.dst_off[f], olen[f],
+            if (olen[f]) HIPCHK(hipMemcpyAsync(S.h_out.p + S.R + o, d_slots + S.dst_off[f], olen[f],
                                                hipMemcpyDeviceToHost, S.st));
             o += olen[f];
         }
@@ -2207,8 +2209,7 @@ static int reader_complete(s3hc_reader* r) {
     S.ready = true;
     r->total += S.out_len;
     if (S.good < S.n) {  // earlier in stream order than any error found while walking later input
-        const int32_t* st = (const int32_t*)(S.h_res.p + 4ull * S.n);
-        r->error = st[S.good];
+        r->error = S.err;
         r->error_msg = "frame decode failed";
         for (size_t k = 1; k < r->inflight.size(); ++k) {
             RSlot& L = r->slots[r->inflight[k]];
@@ -2286,7 +2287,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
             RSlot& S = r->slots[r->inflight.front()];
             if (S.out_pos < S.out_len) {
                 const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
-                if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
+                if (k) par_memcpy(dst, S.h_out.p + S.R + S.out_pos, k);
                 S.out_pos += k;
                 *n = k;
                 if (S.out_pos < S.out_len) return S3HC_OK;
@@ -2299,7 +2300,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
                 RSlot& S = r->slots[r->inflight.front()];
                 if (*n == 0 && S.out_pos < S.out_len) {
                     const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
-                    if (k) par_memcpy(dst, S.h_out.p + S.out_pos, k);
+                    if (k) par_memcpy(dst, S.h_out.p + S.R + S.out_pos, k);
                     S.out_pos += k;
                     *n = k;
                 }

@@ -14,3 +14,5 @@ for lib in "$@"; do
   S3HC_LIB_PATH=$lib timeout -k 10 300 python -u -m pytest tests/test_gpu_fullsize.py::test_config2_full_batch_every_frame_oracle tests/test_gpu_parity.py -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/encab_tests.log 2>&1
   echo "$lib: $(tail -1 gpurun_out/encab_tests.log)"
 done
+timeout -k 10 300 python -u tools/ratio_cmp.py $L/libs3hc_lz4.so "$@" > gpurun_out/ratio_cmp.json 2>&1 || exit $?
+cat gpurun_out/ratio_cmp.json
