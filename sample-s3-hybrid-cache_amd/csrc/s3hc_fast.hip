@@ -279,7 +279,9 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
     DecBlock B;
     if (take) {
         B = blk[U.first];
-        take = !(B.flags & DB_STORED) && B.csize >= 1u && B.csize <= maxc;
+        // (blocks of frames allowing at most 64 KiB: a sequence record holds ll < 2^17 and
+        // ml - 4 < 2^16; larger blocks take the large-block path or the per-unit decoder)
+        take = !(B.flags & DB_STORED) && B.csize >= 1u && B.csize <= maxc && B.limit <= 65536u;
     }
     if (!take) {
         if (g == 0) a.unit_fast[u] = 0;

@@ -93,3 +93,18 @@ def test_frame_bound():
 
     for n in (0, 1, 65535, 65536, 65537, 1 << 20, 5 << 20):
         assert S.frame_bound(n) >= n + 4 * (n // 65536 + 1) + 15
+
+
+def test_knobs_set_and_reject_unknown():
+    # diagnostic switches are read from the environment once per process and changed only
+    # through s3hc_set_knob; unknown names are rejected (no GPU needed)
+    import s3hc_lz4 as S
+
+    for name, value in (("S3HC_FAST_DISABLE", "1"), ("S3HC_FAST", "0"), ("S3HC_LBW_CAP", "4096"),
+                        ("S3HC_LBW_ROUNDS", "2"), ("S3HC_HOST_TRACE", None)):
+        S.set_knob(name, value)
+        S.set_knob(name, None)
+    with pytest.raises(S.CodecError):
+        S.set_knob("S3HC_NO_SUCH_KNOB", "1")
+    with S.knobs({"S3HC_LB_DISABLE": "1", "S3HC_FAST": "1"}):
+        pass
