@@ -255,6 +255,12 @@ __device__ __forceinline__ void wg_excl_scan2(uint32_t v, uint32_t u, uint32_t* 
 }
 }  // namespace
 
+__device__ __forceinline__ void wsync_blk() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ------------------------------------------------------------------ k_dtok
 // Returns whether the fast path took unit u (workgroup-uniform); *fo = its (sequences, bytes).
 __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __restrict__ src,
@@ -466,6 +472,92 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
                 emit(q, k);
             }
         }
+    }
+#elif S3HC_DTOK_BAL == 2
+    // wave-interleaved: wave wq takes the sequences [wq Q, wq Q + Q) (Q a multiple of 64) in
+    // rounds of 64 consecutive ones, lane l the round's l-th; its token position comes from a
+    // 64-entry LDS list the wave expands from the bitmap words at its cursor, and the round's
+    // records are stored coalesced (one 512-byte store per round)
+    uint16_t* base = J[0];
+    base[g] = (uint16_t)r0;
+    if (g == 0) base[kTT] = (uint16_t)N;
+    __syncthreads();
+    {
+        const uint32_t wq = g >> 6, ln = g & 63u;
+        uint16_t* lst = &J[1][0] + 64u * wq;  // (J[1]: kTT + 2 >= 4 x 64 entries)
+        auto wscan = [&](uint32_t x) {        // inclusive scan over the wave
+#pragma unroll
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+                if (ln >= d) x += y;
+            }
+            return x;
+        };
+        const uint32_t Q = ((N + 255u) / 256u) * 64u;
+        const uint32_t R0 = umin_(N, wq * Q), R1 = umin_(N, R0 + Q);
+        uint32_t carry = 0;
+        if (R0 < R1) {
+            uint32_t t = 0;
+#pragma unroll
+            for (uint32_t step = kTT / 2; step; step >>= 1)
+                if (base[t + step] <= R0) t += step;
+            uint32_t w = 4u * t, xb = bits[w], skip = R0 - base[t];
+            for (uint32_t pc = (uint32_t)__builtin_popcount(xb); skip >= pc; pc = (uint32_t)__builtin_popcount(xb)) {
+                skip -= pc;
+                xb = bits[++w];
+            }
+            for (; skip; --skip) xb &= xb - 1u;
+            for (uint32_t R = R0; R < R1;) {
+                const uint32_t wl = ln == 0 ? xb : (w + ln < nbw ? bits[w + ln] : 0u);
+                const uint32_t c = (uint32_t)__builtin_popcount(wl);
+                const uint32_t inc = wscan(c), ex = inc - c;
+                {
+                    uint32_t x = wl, idx = ex;
+                    while (x && idx < 64u) {
+                        lst[idx++] = (uint16_t)(((w + ln) << 5) + (uint32_t)__builtin_ctz(x));
+                        x &= x - 1u;
+                    }
+                }
+                wsync_blk();
+                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+                const uint32_t got = umin_(umin_(tot, 64u), R1 - R);
+                const bool mine = ln < got;
+                const uint32_t q = mine ? lst[ln] : 0u;
+                Tok T;
+                T.ll = T.ml = T.off = 0;
+                T.nxt = END;
+                if (mine) T = S3HC_HOPF(stage, mis, q, C);
+                const uint32_t len = T.ll + T.ml;
+                const uint32_t li = wscan(len);
+                if (mine) {
+                    const uint32_t lit = T.ll == 0 ? 0u : q + 1u + (T.ll >= 15u ? (T.ll - 15u) / 255u + 1u : 0u);
+                    uint32_t y = 0;
+                    if (T.nxt != END) {
+                        bad |= T.off == 0u;
+                        minsl = min(minsl, (int32_t)(carry + li - len + T.ll) - (int32_t)T.off);
+                        y = T.off | ((T.ml - 4u) << 16);
+                    }
+                    rec[R + ln] = make_uint2(lit | (T.ll << 15), y);
+                }
+                carry += (uint32_t)__builtin_amdgcn_readlane((int)li, 63);
+                // the cursor past the round's last sequence
+                if (got >= tot) {
+                    w += 64u;
+                    xb = w < nbw ? bits[w] : 0u;
+                } else {
+                    const uint64_t hit = __ballot(ex <= got && got < inc);
+                    const uint32_t L = (uint32_t)__builtin_ctzll(hit);
+                    uint32_t x = wl;
+                    if (ln == L)
+                        for (uint32_t k = got - ex; k; --k) x &= x - 1u;
+                    w += L;
+                    xb = (uint32_t)__builtin_amdgcn_readlane((int)x, (int)L);
+                }
+                R += got;
+                wsync_blk();  // (the next round rewrites the list)
+            }
+        }
+        o = ln == 63u ? carry : 0u;  // (the scan below: earlier waves' bytes at every lane of mine)
     }
 #else
     // each thread decodes the true tokens of its four bitmap words (positions [128 g, 128 g + 128))
