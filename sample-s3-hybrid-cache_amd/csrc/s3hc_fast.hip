@@ -54,8 +54,8 @@ constexpr uint32_t kMaxC = kFastMaxC;
 #else
 #define S3HC_HOPF hop
 #endif
-#ifndef S3HC_DTOK_BAL  // 1: records by sequence rank, K per thread (0: by bitmap words)
-#define S3HC_DTOK_BAL 0
+#ifndef S3HC_DTOK_BAL  // 2: coalesced wave-interleaved record rounds, 1: by sequence rank, 0: by bitmap words
+#define S3HC_DTOK_BAL 2
 #endif
 constexpr uint32_t kTT = S3HC_DTOK_TT;         // k_dtok threads = speculative segments per block
 constexpr uint32_t kStage = kMaxC + 64;        // staged block: 16-B alignment slack + zero read-ahead
@@ -289,8 +289,15 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
         // ml - 4 < 2^16; larger blocks take the large-block path or the per-unit decoder)
         take = !(B.flags & DB_STORED) && B.csize >= 1u && B.csize <= maxc && B.limit <= 65536u;
     }
+    // a unit the fast path leaves: no hash for the frame close (large blocks: the large-block path's)
+    auto leave = [&]() {
+        if (g == 0) {
+            a.unit_fast[u] = 0;
+            if (a.bh && U.n == 1 && !(unit_lb && unit_lb[u])) a.bh[U.first] = 0;
+        }
+    };
     if (!take) {
-        if (g == 0) a.unit_fast[u] = 0;
+        leave();
         return false;
     }
     const uint32_t C = B.csize;
@@ -384,7 +391,7 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
     if (g == 0) svfrom[0] = 0;
     __syncthreads();
     if (sflag[0] != kTermEnd) {
-        if (g == 0) a.unit_fast[u] = 0;
+        leave();
         return false;
     }
     [[maybe_unused]] const uint64_t tp4 = FP_NOW();
@@ -444,7 +451,7 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
         }
         rec[k] = make_uint2(lit | (T.ll << 15), y);
     };
-#if S3HC_DTOK_BAL
+#if S3HC_DTOK_BAL == 1
     // balanced: thread g decodes sequences [g K, g K + K) (K = ceil(N / kTT)), found from the
     // scanned per-thread counts (J[0] is free after the doubling) by binary search, then by the
     // bitmap words from there
@@ -586,9 +593,13 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
     F.U = Utot;
     F.pad0 = F.pad1 = 0;
     *fo = F;
-    if (g == 0) {
-        if (ok) a.fu[u] = F;
-        a.unit_fast[u] = ok ? 1 : 0;
+    if (ok) {
+        if (g == 0) {
+            a.fu[u] = F;
+            a.unit_fast[u] = 1;
+        }
+    } else {
+        leave();
     }
 #ifdef FPROF
     if ((g & 63u) == 0) {
@@ -891,6 +902,12 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t x, uint32_t l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
 }
 
+// An executor wave's LDS besides its ring (k_dexec runs four executors per workgroup)
+struct DexLds {
+    uint4 pinfo[64];
+    uint8_t gmk[fst::kGW];
+};
+
 // One wave executes unit u (taken by the token index: F = its sequences and bytes) into the
 // 8 KiB LDS ring `ring`. hsync (k_dsmall, nullptr otherwise): a hashing wave of the workgroup
 // reads the ring behind the executor; hsync[0] = bytes final (published after each window),
@@ -899,10 +916,10 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                                            const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
                                            uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
                                            const FastArgs& a, const FastUnit F, uint32_t* __restrict__ ring,
-                                           volatile uint32_t* hsync) {
+                                           volatile uint32_t* hsync, DexLds* __restrict__ dl) {
     using namespace fst;
-    __shared__ uint4 pinfo[64];              // pending matches: md, ms, ml | off << 16, first dword - rank
-    __shared__ uint8_t gmk[kGW];             // pending dwords: rank of each lane's first dword -> lane + 1
+    uint4* pinfo = dl->pinfo;  // pending matches: md, ms, ml | off << 16, first dword - rank
+    uint8_t* gmk = dl->gmk;    // pending dwords: rank of each lane's first dword -> lane + 1
     const uint32_t lane = threadIdx.x & 63u;
     const DecUnit Un = units[u];
     const DecBlock B = blk[Un.first];
@@ -1349,21 +1366,6 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
 #endif
 }
 
-// (<= 128 VGPRs: 4 waves per SIMD, a 4096-block batch resident at once)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_dexec(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                              const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
-                                              uint32_t nunits, const uint64_t* __restrict__ ucount,
-                                              uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
-                                              FastArgs a) {
-    const uint32_t nu = unit_count(ucount, nunits);
-    __shared__ __attribute__((aligned(16))) uint32_t ring[fst::kORW];
-    for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
-        if (!a.unit_fast[u]) continue;
-        dexec_unit(u, src, dst, blk, units, blk_out, blk_status, a, a.fu[u], ring, nullptr);
-        wsync();
-    }
-}
-
 // ------------------------------------------------------------------ k_dsmall
 namespace {
 constexpr uint32_t XH1 = 2654435761U, XH2 = 2246822519U, XH3 = 3266489917U, XH4 = 668265263U, XH5 = 374761393U;
@@ -1430,16 +1432,16 @@ __global__ __launch_bounds__(fst::kTT) void k_dsmall(const uint8_t* __restrict__
                                                      const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
                                                      uint32_t nunits, const uint8_t* __restrict__ unit_lb, FastArgs a,
                                                      uint32_t maxc, uint32_t* __restrict__ blk_out,
-                                                     int32_t* __restrict__ blk_status, uint64_t* __restrict__ blk_hash) {
+                                                     int32_t* __restrict__ blk_status) {
     __shared__ __attribute__((aligned(16))) uint32_t ring[fst::kORW];
     __shared__ uint32_t hsync[2];
+    __shared__ DexLds dl;
     const uint32_t wv = threadIdx.x >> 6;
     for (uint32_t u = blockIdx.x; u < nunits; u += gridDim.x) {
         FastUnit F;
-        const bool ok = dtok_unit(u, src, blk, units, unit_lb, a, maxc, &F);
+        const bool ok = dtok_unit(u, src, blk, units, unit_lb, a, maxc, &F);  // (a unit it leaves: bh 0)
         const DecUnit Un = units[u];
         if (!ok) {
-            if (threadIdx.x == 0 && Un.n == 1 && !(unit_lb && unit_lb[u])) blk_hash[Un.first] = 0;
             __syncthreads();
             continue;
         }
@@ -1450,14 +1452,374 @@ __global__ __launch_bounds__(fst::kTT) void k_dsmall(const uint8_t* __restrict__
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the records are in memory before the barrier
         __syncthreads();
         if (wv == 0) {
-            dexec_unit(u, src, dst, blk, units, blk_out, blk_status, a, F, ring, hsync);
+            dexec_unit(u, src, dst, blk, units, blk_out, blk_status, a, F, ring, hsync, &dl);
         } else if (wv == 1) {
             const uint32_t h = hash_ring(ring, hsync, F.U);
-            if ((threadIdx.x & 63u) == 0) blk_hash[Un.first] = (1ull << 32) | h;
+            if ((threadIdx.x & 63u) == 0 && a.bh) a.bh[Un.first] = (1ull << 32) | h;
         }
         __syncthreads();
     }
 }
+
+// ------------------------------------------------------------------ k_djump
+#ifndef S3HC_SMALL_JUMP  // 1: small launches decode by pointer jumping (k_djump), 0: k_dsmall's executor
+#define S3HC_SMALL_JUMP 1
+#endif
+// Small host-walked launches by pointer jumping: one 256-thread workgroup per 64 KiB block
+// decodes it with every wave instead of k_dsmall's one executor, for the latency of a few-block
+// batch (the range reader's 256 KiB batches) rather than throughput:
+//   token index   dtok_unit (records in the block's token slot);
+//   pointers      one u16 per output byte in LDS (128 KiB over the staged block): a literal byte
+//                 points to itself (and is copied to the output), a match byte to its source byte
+//                 (an overlapping match's bytes to the period before the match), so every pointer
+//                 leads to a smaller position until a literal;
+//   jumping       P[b] = P[P[b]] in place until no pointer changes (log2 of the longest chain of
+//                 rounds, ~7 on log text);
+//   output        every dword holding a match byte gathers its bytes from their literals in the
+//                 output (one unaligned load when they are consecutive);
+//   hash          the block's xxh32 by one 16-lane row (the frame's content checksum: a.bh).
+namespace jmp {
+constexpr uint32_t kQ = 512;              // long sequences written by the whole workgroup
+constexpr uint32_t kShort = 64;           // sequence bytes one thread writes alone
+constexpr uint32_t kPBytes = 2u * 65536u; // P: u16 per output byte
+}  // namespace jmp
+constexpr uint32_t djump_lds_bytes(uint32_t maxc) {
+    return fast_lds_bytes(maxc) > jmp::kPBytes + 64u ? fast_lds_bytes(maxc) : jmp::kPBytes + 64u;
+}
+
+// xxh32 (seed 0) of [p, p + L) in global memory by lanes 0..15 (row 0 of the calling wave): lane
+// 4s + a loads dword a of stripe 4g + s (times P2), lane a runs accumulator a over the four
+// stripes with DPP row shifts (xxh32_row16 of s3hc_kernels.hip). Valid in lane 0.
+__device__ __forceinline__ uint32_t xxh32_row0(const uint8_t* __restrict__ p, uint32_t L) {
+    const uint32_t j = threadIdx.x & 15u, a = j & 3u, s = j >> 2;
+    const uint32_t ns = L >> 4, ng = ns >> 2;
+    uint32_t acc = a == 0 ? XH1 + XH2 : (a == 1 ? XH2 : (a == 2 ? 0u : 0u - XH1));
+    auto step4 = [&](uint32_t m) {
+        acc = xh_rotl(acc + m, 13) * XH1;
+        acc = xh_rotl(acc + fdpp<0x104, 0xF>(m), 13) * XH1;
+        acc = xh_rotl(acc + fdpp<0x108, 0xF>(m), 13) * XH1;
+        acc = xh_rotl(acc + fdpp<0x10C, 0xF>(m), 13) * XH1;
+    };
+    const uint8_t* q = p + 16u * s + 4u * a;  // group g: q + 64 g
+    constexpr uint32_t kB = 8;
+    uint32_t g = 0;
+    for (; g + kB <= ng; g += kB) {
+        uint32_t m[kB];
+#pragma unroll
+        for (uint32_t k = 0; k < kB; ++k) m[k] = gld4(q + 64u * (g + k)) * XH2;
+#pragma unroll
+        for (uint32_t k = 0; k < kB; ++k) step4(m[k]);
+    }
+    for (; g < ng; ++g) step4(gld4(q + 64u * g) * XH2);
+    for (uint32_t t = 4u * ng; t < ns; ++t) acc = xh_round(acc, gld4(p + 16u * t + 4u * a));
+    const uint32_t v1 = (uint32_t)__shfl((int)acc, 0, 16), v2 = (uint32_t)__shfl((int)acc, 1, 16);
+    const uint32_t v3 = (uint32_t)__shfl((int)acc, 2, 16), v4 = (uint32_t)__shfl((int)acc, 3, 16);
+    uint32_t h = L >= 16u ? xh_rotl(v1, 1) + xh_rotl(v2, 7) + xh_rotl(v3, 12) + xh_rotl(v4, 18) : XH5;
+    h += L;
+    uint32_t t = ns * 16u;
+    for (; t + 4u <= L; t += 4u) h = xh_rotl(h + gld4(p + t) * XH3, 17) * XH4;
+    for (; t < L; ++t) h = xh_rotl(h + (uint32_t)p[t] * XH5, 11) * XH1;
+    h ^= h >> 15;
+    h *= XH2;
+    h ^= h >> 13;
+    h *= XH3;
+    h ^= h >> 16;
+    return h;
+}
+
+__global__ __launch_bounds__(fst::kTT) void k_djump(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                    const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+                                                    uint32_t nunits, const uint8_t* __restrict__ unit_lb, FastArgs a,
+                                                    uint32_t maxc, uint32_t* __restrict__ blk_out,
+                                                    int32_t* __restrict__ blk_status) {
+    using namespace fst;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];  // (dtok_unit's stage, then P)
+    uint16_t* P = (uint16_t*)dsm;
+    uint32_t* P32 = (uint32_t*)dsm;
+    __shared__ uint32_t qrec[jmp::kQ], qpos[jmp::kQ];
+    __shared__ uint32_t qn;
+    __shared__ uint32_t jscr[16];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+        FastUnit F;
+        const bool ok = dtok_unit(u, src, blk, units, unit_lb, a, maxc, &F);  // (a unit it leaves: bh 0)
+        if (!ok) {
+            __syncthreads();
+            continue;
+        }
+        const DecUnit Un = units[u];
+        const DecBlock B = blk[Un.first];
+        const uint8_t* in = src + B.src_off;
+        uint8_t* out = dst + B.dst_off;
+        const uint2* rec = a.rec + B.tok;
+        const uint32_t N = F.ntok, U = F.U, C = B.csize;
+        if (t == 0) qn = 0u;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the records are in memory before the barrier
+        __syncthreads();
+        // ---- output positions: thread t's records [t K, t K + K)
+        const uint32_t K = (N + kTT - 1u) / kTT, r0 = umin_(N, t * K), r1 = umin_(N, r0 + K);
+        uint32_t mine = 0;
+        for (uint32_t r = r0; r < r1; ++r) {
+            const uint2 v = rec[r];
+            mine += (v.x >> 15) + ((v.y & 0xFFFFu) ? (v.y >> 16) + 4u : 0u);
+        }
+        uint32_t tot;
+        uint32_t o = wg_excl_scan<kTT / 64>(mine, jscr, &tot);
+        // ---- pointers and literals (sequences longer than kShort: the whole workgroup, below)
+        for (uint32_t r = r0; r < r1; ++r) {
+            const uint2 v = rec[r];
+            const uint32_t ll = v.x >> 15, lit = v.x & 0x7FFFu, off = v.y & 0xFFFFu;
+            const uint32_t ml = off ? (v.y >> 16) + 4u : 0u;
+            if (ll + ml > jmp::kShort) {
+                const uint32_t qi = atomicAdd(&qn, 1u);
+                if (qi < jmp::kQ) {
+                    qrec[qi] = r;
+                    qpos[qi] = o;
+                    o += ll + ml;
+                    continue;
+                }
+            }
+            for (uint32_t c = 0; c < ll; c += 16u) {  // (16-byte loads; the block's last bytes bytewise)
+                const uint4 x = gld16_blk(in, lit + c, C);
+                const uint32_t xw[4] = {x.x, x.y, x.z, x.w}, n = umin_(16u, ll - c);
+                for (uint32_t i = 0; i < n; ++i) {
+                    out[o + c + i] = (uint8_t)(xw[i >> 2] >> (8u * (i & 3u)));
+                    P[o + c + i] = (uint16_t)(o + c + i);
+                }
+            }
+            const uint32_t md = o + ll, ms = md - off;
+            if (off >= ml) {
+                for (uint32_t i = 0; i < ml; ++i) P[md + i] = (uint16_t)(ms + i);
+            } else {
+                uint32_t q = 0;
+                for (uint32_t i = 0; i < ml; ++i) {
+                    P[md + i] = (uint16_t)(ms + q);
+                    q = q + 1u == off ? 0u : q + 1u;
+                }
+            }
+            o += ll + ml;
+        }
+        __syncthreads();
+        const uint32_t nq = umin_(qn, jmp::kQ);
+        for (uint32_t e = 0; e < nq; ++e) {
+            const uint2 v = rec[qrec[e]];
+            const uint32_t o0 = qpos[e], ll = v.x >> 15, lit = v.x & 0x7FFFu, off = v.y & 0xFFFFu;
+            const uint32_t ml = off ? (v.y >> 16) + 4u : 0u;
+            for (uint32_t i = t; i < ll; i += kTT) {
+                out[o0 + i] = in[lit + i];
+                P[o0 + i] = (uint16_t)(o0 + i);
+            }
+            const uint32_t md = o0 + ll, ms = md - off;
+            for (uint32_t i = t; i < ml; i += kTT) P[md + i] = (uint16_t)(ms + (off >= ml ? i : i % off));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // literal bytes in memory before the gathers below
+        __syncthreads();
+        // ---- pointer jumping (pairs of u16 per dword; in place: a pointer read mid-update is an
+        // older or newer point of the same chain)
+        const uint32_t Up = (U + 1u) >> 1;
+        for (;;) {
+            int ch = 0;
+            for (uint32_t k = t; k < Up; k += kTT) {
+                const uint32_t pr = P32[k], b0 = 2u * k, b1 = b0 + 1u;
+                uint32_t lo = pr & 0xFFFFu, hi = pr >> 16;
+                bool c = false;
+                if (lo != b0) {
+                    const uint32_t q = P[lo];
+                    if (q != lo) { lo = q; c = true; }
+                }
+                if (b1 < U && hi != b1) {
+                    const uint32_t q = P[hi];
+                    if (q != hi) { hi = q; c = true; }
+                }
+                if (c) {
+                    P32[k] = lo | (hi << 16);
+                    ch = 1;
+                }
+            }
+            if (!__syncthreads_or(ch)) break;
+        }
+        // ---- every dword with a match byte: its bytes from their literals, eight dwords per thread
+        // at a time (every gather of a batch in flight before its stores)
+        const bool al = ((uintptr_t)out & 3u) == 0u;
+        constexpr uint32_t kE = 8;
+        for (uint32_t b0 = 4u * t; b0 < U; b0 += 4u * kTT * kE) {
+            uint32_t v[kE], pp[kE][4];
+            bool need[kE];
+#pragma unroll
+            for (uint32_t e = 0; e < kE; ++e) {
+                const uint32_t b = b0 + 4u * kTT * e;
+                const uint32_t n = b < U ? umin_(4u, U - b) : 0u;
+                const uint32_t w0 = n ? P32[b >> 1] : 0u, w1 = n ? P32[(b >> 1) + 1u] : 0u;
+                pp[e][0] = w0 & 0xFFFFu;
+                pp[e][1] = n > 1u ? w0 >> 16 : b + 1u;
+                pp[e][2] = n > 2u ? w1 & 0xFFFFu : b + 2u;
+                pp[e][3] = n > 3u ? w1 >> 16 : b + 3u;
+                need[e] = n && !(pp[e][0] == b && pp[e][1] == b + 1u && pp[e][2] == b + 2u && pp[e][3] == b + 3u);
+            }
+#pragma unroll
+            for (uint32_t e = 0; e < kE; ++e) {
+                const uint32_t b = b0 + 4u * kTT * e;
+                v[e] = 0u;
+                if (!need[e]) continue;
+                const uint32_t n = umin_(4u, U - b);
+                if (n == 4u && pp[e][1] == pp[e][0] + 1u && pp[e][2] == pp[e][0] + 2u && pp[e][3] == pp[e][0] + 3u) {
+                    v[e] = gld4(out + pp[e][0]);
+                } else {
+                    v[e] = (uint32_t)out[pp[e][0]];
+                    if (n > 1u) v[e] |= (uint32_t)out[pp[e][1]] << 8;
+                    if (n > 2u) v[e] |= (uint32_t)out[pp[e][2]] << 16;
+                    if (n > 3u) v[e] |= (uint32_t)out[pp[e][3]] << 24;
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every gather of the batch before its stores)
+#pragma unroll
+            for (uint32_t e = 0; e < kE; ++e) {
+                const uint32_t b = b0 + 4u * kTT * e;
+                if (!need[e]) continue;
+                const uint32_t n = umin_(4u, U - b);
+                if (n == 4u && al) {
+                    *(uint32_t*)(out + b) = v[e];
+                } else {
+                    for (uint32_t i = 0; i < n; ++i) out[b + i] = (uint8_t)(v[e] >> (8u * i));
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t < 16u) {
+            const uint32_t h = xxh32_row0(out, U);
+            if (t == 0) {
+                if (a.bh) a.bh[Un.first] = (1ull << 32) | h;
+                blk_out[Un.first] = U;
+                blk_status[Un.first] = S3HC_OK;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ k_dexec
+// The hashing wave of k_dexec: xxh32 (seed 0) of the output of up to four executor waves, one
+// 16-lane group per executor g (its LDS ring at rings + g kORW, its progress words hs[2g] bytes
+// final / hs[2g + 1] bytes hashed: the dexec_unit protocol), Ug bytes (a group without a unit:
+// has = false). Lane 4s + a of a group loads dword a of the next four stripes' stripe s (times
+// P2); accumulator a runs over the four with DPP row shifts (no LDS round trip), so every lane of
+// the group holds its accumulator's value. Returns the unit's hash (every lane of its group).
+__device__ __forceinline__ uint32_t hash_rings(const uint32_t* rings, volatile uint32_t* hs, uint32_t Ug, bool has) {
+    using namespace fst;
+    const uint32_t lane = threadIdx.x & 63u, grp = lane >> 4, j = lane & 15u, ha = j & 3u, s = j >> 2;
+    const uint32_t* ring = rings + grp * kORW;
+    uint32_t hacc = ha == 0 ? XH1 + XH2 : (ha == 1 ? XH2 : (ha == 2 ? 0u : 0u - XH1));
+    const uint32_t hns = Ug >> 4;  // whole stripes
+    uint32_t hsn = 0;              // stripes hashed (group-uniform)
+    bool done = !has;
+    for (;;) {
+        const uint32_t avail = done ? 0u : hs[2u * grp];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t lim = done ? 0u : umin_(avail >> 4, hns);
+        bool moved = false;
+        while (__ballot(hsn + 4u <= lim)) {
+            if (hsn + 4u <= lim) {
+                const uint32_t mv = ring[((16u * (hsn + s) + 4u * ha) & kORM) >> 2] * XH2;
+                hacc = xh_rotl(hacc + mv, 13) * XH1;
+                hacc = xh_rotl(hacc + fdpp<0x104, 0xF>(mv), 13) * XH1;
+                hacc = xh_rotl(hacc + fdpp<0x108, 0xF>(mv), 13) * XH1;
+                hacc = xh_rotl(hacc + fdpp<0x10C, 0xF>(mv), 13) * XH1;
+                hsn += 4u;
+                moved = true;
+            }
+        }
+        while (__ballot(hsn < lim)) {
+            if (hsn < lim) {
+                hacc = xh_round(hacc, ring[((16u * hsn + 4u * ha) & kORM) >> 2]);
+                ++hsn;
+                moved = true;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (ring reads done before the slots are released)
+        if (!done && moved && j == 0) hs[2u * grp + 1u] = 16u * hsn;
+        if (!done && avail >= Ug && hsn == hns) done = true;
+        if (!__ballot(!done)) break;
+        if (!__ballot(moved)) __builtin_amdgcn_s_sleep(2);
+    }
+    // (lanes 16 grp + a hold accumulator a; row broadcasts within the group)
+    const uint32_t v1 = (uint32_t)__shfl((int)hacc, (int)(16u * grp), 64), v2 = (uint32_t)__shfl((int)hacc, (int)(16u * grp + 1u), 64);
+    const uint32_t v3 = (uint32_t)__shfl((int)hacc, (int)(16u * grp + 2u), 64), v4 = (uint32_t)__shfl((int)hacc, (int)(16u * grp + 3u), 64);
+    uint32_t h = Ug >= 16u ? xh_rotl(v1, 1) + xh_rotl(v2, 7) + xh_rotl(v3, 12) + xh_rotl(v4, 18) : XH5;
+    h += Ug;
+    const uint8_t* rb = (const uint8_t*)ring;
+    uint32_t p = hns * 16u;
+    for (; p + 4u <= Ug; p += 4u) {
+        const uint32_t w = (uint32_t)rb[p & kORM] | ((uint32_t)rb[(p + 1u) & kORM] << 8) |
+                           ((uint32_t)rb[(p + 2u) & kORM] << 16) | ((uint32_t)rb[(p + 3u) & kORM] << 24);
+        h = xh_rotl(h + w * XH3, 17) * XH4;
+    }
+    for (; p < Ug; ++p) h = xh_rotl(h + (uint32_t)rb[p & kORM] * XH5, 11) * XH1;
+    h ^= h >> 15;
+    h *= XH2;
+    h ^= h >> 13;
+    h *= XH3;
+    h ^= h >> 16;
+    return h;
+}
+
+#ifndef S3HC_DEXEC_HASH  // 1: k_dexec = four executors + a hashing wave per workgroup; 0: one executor per workgroup, the frame close hashes
+#define S3HC_DEXEC_HASH 0
+#endif
+#if S3HC_DEXEC_HASH
+// Four executor waves (one unit each, k_dtok's records) and, when the frame close takes hashes
+// (a.bh), a fifth wave hashing their output from the LDS rings while they run: the frame's
+// content xxh32 without a second pass over the output. The four units of a workgroup are
+// consecutive; the grid strides over groups of four.
+// (<= 128 VGPRs: four waves per SIMD, three workgroups per CU)
+__global__ __launch_bounds__(5 * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_dexec(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                  const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+                                                  uint32_t nunits, const uint64_t* __restrict__ ucount,
+                                                  uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
+                                                  FastArgs a) {
+    const uint32_t nu = unit_count(ucount, nunits);
+    __shared__ __attribute__((aligned(16))) uint32_t ring[4 * fst::kORW];
+    __shared__ DexLds dl[4];
+    __shared__ uint32_t hs[8];
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // (wave-uniform: scalar ring base)
+    for (uint32_t b = 4u * blockIdx.x; b < nu; b += 4u * gridDim.x) {
+        if (threadIdx.x < 8u) hs[threadIdx.x] = 0u;
+        __syncthreads();
+        if (wv < 4u) {
+            const uint32_t u = b + wv;
+            if (u < nu && a.unit_fast[u])
+                dexec_unit(u, src, dst, blk, units, blk_out, blk_status, a, a.fu[u], ring + wv * fst::kORW,
+                           a.bh ? hs + 2u * wv : nullptr, dl + wv);
+        } else if (a.bh) {
+            const uint32_t u = b + ((threadIdx.x & 63u) >> 4);
+            const bool has = u < nu && a.unit_fast[u];
+            const uint32_t h = hash_rings(ring, hs, has ? a.fu[u].U : 0u, has);
+            if (has && (threadIdx.x & 15u) == 0u) a.bh[units[u].first] = (1ull << 32) | h;
+        }
+        __syncthreads();
+    }
+}
+constexpr uint32_t kDexecUnits = 4, kDexecThreads = 5 * 64;
+#else
+// One executor wave per workgroup (k_dtok's records); the frame close hashes the output.
+// (<= 128 VGPRs: 4 waves per SIMD, a 4096-block batch resident at once)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_dexec(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                              const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+                                              uint32_t nunits, const uint64_t* __restrict__ ucount,
+                                              uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
+                                              FastArgs a) {
+    const uint32_t nu = unit_count(ucount, nunits);
+    __shared__ __attribute__((aligned(16))) uint32_t ring[fst::kORW];
+    __shared__ DexLds dl;
+    for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
+        if (!a.unit_fast[u]) continue;
+        dexec_unit(u, src, dst, blk, units, blk_out, blk_status, a, a.fu[u], ring, nullptr, &dl);
+        wsync();
+    }
+}
+constexpr uint32_t kDexecUnits = 1, kDexecThreads = 64;
+#endif
+bool fast_exec_hashes() { return S3HC_DEXEC_HASH != 0; }
 
 // ================================================================ launchers
 static inline uint32_t fcdiv(uint64_t x, uint64_t y) { return (uint32_t)((x + y - 1) / y); }
@@ -1485,19 +1847,27 @@ extern "C" int s3hc_diag_fprof(unsigned long long* out, int n, int reset) {
 #endif
 hipError_t launch_fast_small(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
                              uint32_t nunits, const uint8_t* unit_lb, const FastArgs& a, uint32_t* blk_out,
-                             int32_t* blk_status, uint64_t* blk_hash, hipStream_t st) {
+                             int32_t* blk_status, hipStream_t st) {
     if (!nunits || !a.maxc) return hipSuccess;
     const uint32_t maxc = a.maxc < kFastMaxC ? a.maxc : kFastMaxC;
+#if S3HC_SMALL_JUMP
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k_djump, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)djump_lds_bytes(kFastMaxC));  // (> 64 KiB of dynamic LDS)
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL(k_djump, dim3(nunits), dim3(fst::kTT), djump_lds_bytes(maxc), st, src, dst, blk, units, nunits,
+                       unit_lb, a, maxc, blk_out, blk_status);
+#else
     hipLaunchKernelGGL(k_dsmall, dim3(nunits), dim3(fst::kTT), fast_lds_bytes(maxc), st, src, dst, blk, units, nunits,
-                       unit_lb, a, maxc, blk_out, blk_status, blk_hash);
+                       unit_lb, a, maxc, blk_out, blk_status);
+#endif
     return hipGetLastError();
 }
 hipError_t launch_fast_exec(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
                             uint32_t nunits, const uint64_t* ucount, uint32_t grid, uint32_t* blk_out,
                             int32_t* blk_status, const FastArgs& a, hipStream_t st) {
     if (!nunits || !grid) return hipSuccess;
-    hipLaunchKernelGGL(k_dexec, dim3(grid), dim3(64), 0, st, src, dst, blk, units, nunits, ucount, blk_out,
-                       blk_status, a);
+    hipLaunchKernelGGL(k_dexec, dim3((grid + kDexecUnits - 1u) / kDexecUnits), dim3(kDexecThreads), 0, st, src, dst,
+                       blk, units, nunits, ucount, blk_out, blk_status, a);
     return hipGetLastError();
 }
 }  // namespace s3hc

@@ -218,6 +218,9 @@ struct FastArgs {
     uint8_t* unit_fast;  // per unit: 1 = decoded by the fast path
     uint32_t maxc;       // largest compressed block of the launch (<= kFastMaxC: sizes k_dtok's LDS);
                          // 0 = no block for the fast path
+    uint64_t* bh;        // per DecBlock (nullable): 1 << 32 | content xxh32 of a single-block unit the
+                         // fast path decoded, 0 for the single-block units it left (frame close
+                         // takes the hash instead of reading the frame's output again)
 };
 
 }  // namespace s3hc

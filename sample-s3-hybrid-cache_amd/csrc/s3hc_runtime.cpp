@@ -39,8 +39,9 @@ hipError_t launch_fast_tok(const uint8_t*, const DecBlock*, const DecUnit*, uint
                            const uint8_t*, const FastArgs&, hipStream_t);
 hipError_t launch_fast_exec(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*,
                             uint32_t, uint32_t*, int32_t*, const FastArgs&, hipStream_t);
+bool fast_exec_hashes();
 hipError_t launch_fast_small(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint8_t*,
-                             const FastArgs&, uint32_t*, int32_t*, uint64_t*, hipStream_t);
+                             const FastArgs&, uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*,
                            uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, uint32_t*, int32_t*, hipStream_t);
@@ -392,7 +393,7 @@ struct LbScratch {
     LbArgs a{};
     // 64 KiB-block fast path (s3hc_fast.hip): per-unit token bitmaps and results
     DevBuf f_bmp, f_fu, f_unit_fast;  // (f_bmp: sequence records)
-    DevBuf f_hash;                     // small launches without the large-block path: per-block hashes
+    DevBuf f_hash;                     // launches without the large-block path: per-block hashes (FastArgs::bh)
     FastArgs fa{};
     bool fast_ready = false;
     // small launch (host-walked, <= kLbFewBlocks blocks): 64 KiB blocks run the fused k_dsmall
@@ -402,14 +403,17 @@ struct LbScratch {
     // tok_entries: the launch's token-slot entries (DecBlock::tok + tok_slot_entries(csize) of
     // every block stays below it; sized by compressed bytes, not by a per-unit maximum)
     // maxc: the largest compressed block the launch may hand the fast path (sizes k_dtok's LDS)
-    hipError_t prepare_fast(uint32_t nunits, uint64_t tok_entries, uint64_t maxc) {
+    // nblocks: the launch's DecBlock count (block hashes are per DecBlock)
+    hipError_t prepare_fast(uint32_t nunits, uint32_t nblocks, uint64_t tok_entries, uint64_t maxc) {
         fast_ready = false;
         fa.maxc = (uint32_t)std::min<uint64_t>(maxc, kFastMaxC);
+        fa.bh = nullptr;
         if (!nunits || tok_entries > 0xFFFFFFF0ull) return hipSuccess;  // (u32 slots: the fast path sits out)
         hipError_t e;
         if ((e = f_bmp.ensure((size_t)tok_entries * sizeof(uint2) + 256)) != hipSuccess) return e;
         if ((e = f_fu.ensure((size_t)nunits * sizeof(FastUnit) + 64)) != hipSuccess) return e;
         if ((e = f_unit_fast.ensure((size_t)nunits + 64)) != hipSuccess) return e;
+        if ((e = f_hash.ensure((size_t)std::max(nunits, nblocks) * 8 + 64)) != hipSuccess) return e;
         fa.rec = f_bmp.as<uint2>();
         fa.fu = f_fu.as<FastUnit>();
         fa.unit_fast = f_unit_fast.as<uint8_t>();
@@ -512,9 +516,8 @@ static hipError_t prepare_host_launch(LbScratch& L, const DecBlock* blocks, size
     }
     hipError_t e;
     if ((e = L.prepare(nu, (uint32_t)nb, lc)) != hipSuccess) return e;
-    if ((e = L.prepare_fast(nu, tok_entries, max_csize(blocks, nb))) != hipSuccess) return e;
+    if ((e = L.prepare_fast(nu, (uint32_t)nb, tok_entries, max_csize(blocks, nb))) != hipSuccess) return e;
     L.small = small && L.fast_ready;
-    if (L.small && !L.active && (e = L.f_hash.ensure(nb * 8 + 64)) != hipSuccess) return e;
     return hipSuccess;
 }
 
@@ -540,14 +543,20 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
     if (lb && (e = launch_lb_parse(L->a, src, blk, units, nunits, ucount, blk_out, blk_status, st)) != hipSuccess) return e;
     // 64 KiB blocks: token index + executor (S3HC_FAST_DISABLE=1: every block on the per-unit
     // decoder, for comparisons); blocks the fast path leaves go to the per-unit decoder below
-    const bool fast = L && L->fast_ready && nunits && !(lb && L->all_lb) && fast_path_enabled();
+    const bool fast = L && L->fast_ready && L->fa.maxc && nunits && !(lb && L->all_lb) && fast_path_enabled();
+    if (fast && (L->small || fast_exec_hashes())) {
+        // the executors hash their output (the frame close takes those hashes, like the
+        // large-block path's: one array, the large-block path zeroes it for every single-block
+        // unit, the fast path sets its own and zeroes those it leaves when the other path is off)
+        L->fa.bh = lb ? L->a.blk_hash : L->f_hash.as<uint64_t>();
+        if (blk_hash) *blk_hash = L->fa.bh;
+    } else {
+        L->fa.bh = nullptr;
+    }
     if (fast && L->small) {
-        // small host-walked launch: token index + executor + content xxh32 in one launch; the
-        // frame close takes its hashes (blk_hash) like the large-block path's
-        uint64_t* hb = lb ? L->a.blk_hash : L->f_hash.as<uint64_t>();
-        if (blk_hash) *blk_hash = hb;
+        // small host-walked launch: token index + executor + content xxh32 in one launch
         if ((e = launch_fast_small(src, dst, blk, units, nunits, lb ? L->a.unit_lb : nullptr, L->fa, blk_out,
-                                   blk_status, hb, st)) != hipSuccess)
+                                   blk_status, st)) != hipSuccess)
             return e;
     } else if (fast) {
         if ((e = launch_fast_tok(src, blk, units, nunits, ucount, grid, lb ? L->a.unit_lb : nullptr, L->fa, st)) !=
@@ -1013,7 +1022,7 @@ extern "C" int s3hc_plan_decode(s3hc_ctx* ctx, const uint64_t* frame_off, const 
             }
         }
         HIPCHK(P->lb.prepare(P->blk_cap, P->blk_cap, lc));
-        HIPCHK(P->lb.prepare_fast(P->blk_cap, tok_entries, max_frame_len));
+        HIPCHK(P->lb.prepare_fast(P->blk_cap, P->blk_cap, tok_entries, max_frame_len));
         P->lb.small = false;
         HIPCHK(hipStreamSynchronize(st));
         *out = P.release();
