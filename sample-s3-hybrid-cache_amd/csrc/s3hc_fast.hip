@@ -54,8 +54,8 @@ constexpr uint32_t kMaxC = kFastMaxC;
 #else
 #define S3HC_HOPF hop
 #endif
-#ifndef S3HC_DTOK_BAL  // 2: coalesced wave-interleaved record rounds, 1: by sequence rank, 0: by bitmap words
-#define S3HC_DTOK_BAL 2
+#ifndef S3HC_DTOK_BAL  // 1: records by sequence rank, 2: coalesced wave-interleaved rounds, 0: by bitmap words
+#define S3HC_DTOK_BAL 1
 #endif
 constexpr uint32_t kTT = S3HC_DTOK_TT;         // k_dtok threads = speculative segments per block
 constexpr uint32_t kStage = kMaxC + 64;        // staged block: 16-B alignment slack + zero read-ahead
@@ -63,10 +63,8 @@ constexpr uint32_t kBitW = kMaxC / 32;         // bitmap words, one bit per comp
 constexpr uint32_t END = 0xFFFFFFFEu;          // chain ended with the block's last sequence
 constexpr uint32_t DEAD = 0xFFFFFFFFu;         // malformed token (or a walk that gave up)
 constexpr uint32_t kOvfCap = 4096;             // hops a walk past its segment may take before giving up
-constexpr uint32_t kLv = kTT == 512 ? 9 : 8;   // doubling levels: chains over <= kTT segments
 static_assert(kTT == 256 || kTT == 512, "k_dtok: 4 or 8 waves");
 static_assert(kBitW <= 4 * 256, "k_dtok: four bitmap words per thread cover the block");
-constexpr uint32_t kTermEnd = kTT, kTermBad = kTT + 1;
 constexpr uint32_t kMEnd = 0xFFFEu, kMBad = 0xFFFFu;  // u16 merge codes (positions are < kMaxC)
 }  // namespace fst
 
@@ -263,20 +261,24 @@ __device__ __forceinline__ void wsync_blk() {
 
 // ------------------------------------------------------------------ k_dtok
 // Returns whether the fast path took unit u (workgroup-uniform); *fo = its (sequences, bytes).
+template <uint32_t TT>  // threads of the workgroup = speculative segments per block (256, 512 or 1024)
 __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __restrict__ src,
                                           const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
                                           const uint8_t* __restrict__ unit_lb, const FastArgs& a,
                                           uint32_t maxc, FastUnit* fo) {
     using namespace fst;
+    static_assert(TT == 256 || TT == 512 || TT == 1024, "dtok_unit: 4, 8 or 16 waves");
+    constexpr uint32_t kLv = TT == 1024 ? 10 : (TT == 512 ? 9 : 8);  // doubling levels: chains over <= TT segments
+    constexpr uint32_t kTermEnd = TT, kTermBad = TT + 1;
     // the staged block and the token bitmap live in dynamic LDS sized to the launch's largest
     // compressed block (fast_lds_bytes): config 2's ~26 KB blocks fit five workgroups per CU
     // instead of four at the 32 KiB maximum
     extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];
     uint8_t* stage = dsm;
     uint32_t* bits = (uint32_t*)(dsm + fast_stage_bytes(maxc));
-    __shared__ uint16_t svfrom[kTT];   // per segment on the true chain: its first true token (else M_BAD)
-    __shared__ uint16_t J[2][kTT + 2]; // succ^(2^k) per segment, ping-pong; kTT / kTT + 1 are terminals
-    __shared__ uint8_t reach[kTT + 2]; // segment is on the true chain
+    __shared__ uint16_t svfrom[TT];   // per segment on the true chain: its first true token (else M_BAD)
+    __shared__ uint16_t J[2][TT + 2]; // succ^(2^k) per segment, ping-pong; TT / TT + 1 are terminals
+    __shared__ uint8_t reach[TT + 2]; // segment is on the true chain
     __shared__ uint32_t scr[16];
     __shared__ uint32_t sflag[4];      // [0] terminal of the chain, [1] failure, [2] pool base
     const uint32_t g = threadIdx.x;
@@ -311,17 +313,17 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
         // all loads in flight at once
         const uint4* gw = (const uint4*)(in - mis);
         const uint32_t nv = (mis + C + 15u) >> 4;
-        static_assert((kMaxC + 30u) / 16u <= (kTT == 512 ? 5u : 9u) * kTT, "staging covers the largest block");
+        static_assert((kMaxC + 30u) / 16u <= (TT == 256 ? 9u : 5u) * TT, "staging covers the largest block");
         uint4 v0, v1, v2, v3, v4, v5, v6, v7, v8;
-#define S3HC_LDG(i, v) if (g + (i) * kTT < nv) v = gw[g + (i) * kTT];
-#define S3HC_STS(i, v) if (g + (i) * kTT < nv) ((uint4*)stage)[g + (i) * kTT] = v;
+#define S3HC_LDG(i, v) if (g + (i) * TT < nv) v = gw[g + (i) * TT];
+#define S3HC_STS(i, v) if (g + (i) * TT < nv) ((uint4*)stage)[g + (i) * TT] = v;
         S3HC_LDG(0, v0) S3HC_LDG(1, v1) S3HC_LDG(2, v2) S3HC_LDG(3, v3) S3HC_LDG(4, v4)
-        if (kTT == 256) { S3HC_LDG(5, v5) S3HC_LDG(6, v6) S3HC_LDG(7, v7) S3HC_LDG(8, v8) }
+        if (TT == 256) { S3HC_LDG(5, v5) S3HC_LDG(6, v6) S3HC_LDG(7, v7) S3HC_LDG(8, v8) }
         S3HC_STS(0, v0) S3HC_STS(1, v1) S3HC_STS(2, v2) S3HC_STS(3, v3) S3HC_STS(4, v4)
-        if (kTT == 256) { S3HC_STS(5, v5) S3HC_STS(6, v6) S3HC_STS(7, v7) S3HC_STS(8, v8) }
+        if (TT == 256) { S3HC_STS(5, v5) S3HC_STS(6, v6) S3HC_STS(7, v7) S3HC_STS(8, v8) }
 #undef S3HC_LDG
 #undef S3HC_STS
-        for (uint32_t k = g; k < (C + 31u) / 32u; k += kTT) bits[k] = 0u;
+        for (uint32_t k = g; k < (C + 31u) / 32u; k += TT) bits[k] = 0u;
         reach[g] = g == 0 ? 1 : 0;
         if (g == 0) {
             sflag[0] = kTermBad;
@@ -334,7 +336,7 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
 
     [[maybe_unused]] const uint64_t tp1 = FP_NOW();
     // ---- walk 1: from the start of my segment to its end, marking every position visited
-    const uint32_t segL = (C + kTT - 1u) / kTT;
+    const uint32_t segL = (C + TT - 1u) / TT;
     const uint32_t s0 = umin_(g * segL, C), s1 = umin_(s0 + segL, C);
     uint32_t p = s0;
     while (p < s1) {
@@ -367,8 +369,8 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
     // successor segment of my walk: the segment of the merge point, or a terminal
     J[0][g] = (uint16_t)(m < C ? m / segL : (m == END ? kTermEnd : kTermBad));
     if (g < 2) {
-        J[0][kTT + g] = J[1][kTT + g] = (uint16_t)(kTT + g);
-        reach[kTT + g] = 0;
+        J[0][TT + g] = J[1][TT + g] = (uint16_t)(TT + g);
+        reach[TT + g] = 0;
     }
     __syncthreads();
     [[maybe_unused]] const uint64_t tp3 = FP_NOW();
@@ -433,7 +435,7 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
         cnt += (uint32_t)__builtin_popcount(wv[j]);
     }
     uint32_t N;
-    const uint32_t r0 = wg_excl_scan<kTT / 64>(cnt, scr, &N);
+    const uint32_t r0 = wg_excl_scan<TT / 64>(cnt, scr, &N);
     uint2* rec = a.rec + B.tok;
     uint32_t o = 0;
     int32_t minsl = 0x7FFFFFFF;
@@ -452,19 +454,19 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
         rec[k] = make_uint2(lit | (T.ll << 15), y);
     };
 #if S3HC_DTOK_BAL == 1
-    // balanced: thread g decodes sequences [g K, g K + K) (K = ceil(N / kTT)), found from the
+    // balanced: thread g decodes sequences [g K, g K + K) (K = ceil(N / TT)), found from the
     // scanned per-thread counts (J[0] is free after the doubling) by binary search, then by the
     // bitmap words from there
     uint16_t* base = J[0];
     base[g] = (uint16_t)r0;
-    if (g == 0) base[kTT] = (uint16_t)N;
+    if (g == 0) base[TT] = (uint16_t)N;
     __syncthreads();
     {
-        const uint32_t K = (N + kTT - 1u) / kTT, R0 = g * K, R1 = umin_(N, R0 + K);
+        const uint32_t K = (N + TT - 1u) / TT, R0 = g * K, R1 = umin_(N, R0 + K);
         if (R0 < R1) {
             uint32_t t = 0;
 #pragma unroll
-            for (uint32_t step = kTT / 2; step; step >>= 1)
+            for (uint32_t step = TT / 2; step; step >>= 1)
                 if (base[t + step] <= R0) t += step;
             uint32_t w = 4u * t, xb = bits[w], skip = R0 - base[t];
             for (uint32_t pc = (uint32_t)__builtin_popcount(xb); skip >= pc; pc = (uint32_t)__builtin_popcount(xb)) {
@@ -485,13 +487,14 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
     // rounds of 64 consecutive ones, lane l the round's l-th; its token position comes from a
     // 64-entry LDS list the wave expands from the bitmap words at its cursor, and the round's
     // records are stored coalesced (one 512-byte store per round)
+    static_assert(TT == 256, "the interleaved record pass: four waves");
     uint16_t* base = J[0];
     base[g] = (uint16_t)r0;
-    if (g == 0) base[kTT] = (uint16_t)N;
+    if (g == 0) base[TT] = (uint16_t)N;
     __syncthreads();
     {
         const uint32_t wq = g >> 6, ln = g & 63u;
-        uint16_t* lst = &J[1][0] + 64u * wq;  // (J[1]: kTT + 2 >= 4 x 64 entries)
+        uint16_t* lst = &J[1][0] + 64u * wq;  // (J[1]: TT + 2 >= 4 x 64 entries)
         auto wscan = [&](uint32_t x) {        // inclusive scan over the wave
 #pragma unroll
             for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -506,7 +509,7 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
         if (R0 < R1) {
             uint32_t t = 0;
 #pragma unroll
-            for (uint32_t step = kTT / 2; step; step >>= 1)
+            for (uint32_t step = TT / 2; step; step >>= 1)
                 if (base[t + step] <= R0) t += step;
             uint32_t w = 4u * t, xb = bits[w], skip = R0 - base[t];
             for (uint32_t pc = (uint32_t)__builtin_popcount(xb); skip >= pc; pc = (uint32_t)__builtin_popcount(xb)) {
@@ -583,7 +586,7 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
 #endif
     [[maybe_unused]] const uint64_t tp6 = FP_NOW();
     uint32_t Utot;
-    const uint32_t obase = wg_excl_scan<kTT / 64>(o, scr, &Utot);
+    const uint32_t obase = wg_excl_scan<TT / 64>(o, scr, &Utot);
     const bool fail = bad || (int64_t)obase + minsl < 0;
     if (fail) sflag[1] = 1u;
     __syncthreads();
@@ -629,7 +632,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
     const uint32_t nu = unit_count(ucount, nunits);
     for (uint32_t u = blockIdx.x; u < nu; u += gridDim.x) {
         FastUnit F;
-        (void)dtok_unit(u, src, blk, units, unit_lb, a, maxc, &F);
+        (void)dtok_unit<fst::kTT>(u, src, blk, units, unit_lb, a, maxc, &F);
         __syncthreads();  // (the next unit reuses the LDS)
     }
 }
@@ -1439,7 +1442,7 @@ __global__ __launch_bounds__(fst::kTT) void k_dsmall(const uint8_t* __restrict__
     const uint32_t wv = threadIdx.x >> 6;
     for (uint32_t u = blockIdx.x; u < nunits; u += gridDim.x) {
         FastUnit F;
-        const bool ok = dtok_unit(u, src, blk, units, unit_lb, a, maxc, &F);  // (a unit it leaves: bh 0)
+        const bool ok = dtok_unit<fst::kTT>(u, src, blk, units, unit_lb, a, maxc, &F);  // (a unit it leaves: bh 0)
         const DecUnit Un = units[u];
         if (!ok) {
             __syncthreads();
@@ -1465,55 +1468,48 @@ __global__ __launch_bounds__(fst::kTT) void k_dsmall(const uint8_t* __restrict__
 #ifndef S3HC_SMALL_JUMP  // 1: small launches decode by pointer jumping (k_djump), 0: k_dsmall's executor
 #define S3HC_SMALL_JUMP 1
 #endif
-// Small host-walked launches by pointer jumping: one 256-thread workgroup per 64 KiB block
-// decodes it with every wave instead of k_dsmall's one executor, for the latency of a few-block
-// batch (the range reader's 256 KiB batches) rather than throughput:
-//   token index   dtok_unit (records in the block's token slot);
-//   pointers      one u16 per output byte in LDS (128 KiB over the staged block): a literal byte
-//                 points to itself (and is copied to the output), a match byte to its source byte
-//                 (an overlapping match's bytes to the period before the match), so every pointer
-//                 leads to a smaller position until a literal;
+// Small host-walked launches by pointer jumping, for the latency of a few-block batch (the range
+// reader's 256 KiB batches) rather than throughput: one 1024-thread workgroup per block indexes it
+// (dtok_unit with 1024 speculative segments: records, as k_dtok writes them) and decodes it with
+// all 16 waves instead of k_dsmall's one executor wave:
+//   positions     the records' output offsets (four per thread, one workgroup scan);
+//   pointers      one u16 per output byte in LDS (128 KiB): a literal byte points to itself (and is
+//                 copied to the output), a match byte to its source byte (an overlapping match's
+//                 bytes to the period before the match), so every pointer leads to a smaller
+//                 position until a literal; sequences longer than kShort by the whole workgroup;
 //   jumping       P[b] = P[P[b]] in place until no pointer changes (log2 of the longest chain of
-//                 rounds, ~7 on log text);
+//                 rounds: 6 on the bench's log text), eight pointer pairs per thread in flight;
 //   output        every dword holding a match byte gathers its bytes from their literals in the
-//                 output (one unaligned load when they are consecutive);
-//   hash          the block's xxh32 by one 16-lane row (the frame's content checksum: a.bh).
+//                 output (one unaligned load when they are consecutive), eight dwords in flight;
+//   hash          the block's xxh32 by four lanes (the frame's content checksum: a.bh).
 namespace jmp {
+constexpr uint32_t kT = 1024;             // threads per workgroup
 constexpr uint32_t kQ = 512;              // long sequences written by the whole workgroup
 constexpr uint32_t kShort = 64;           // sequence bytes one thread writes alone
 constexpr uint32_t kPBytes = 2u * 65536u; // P: u16 per output byte
+constexpr uint32_t kLds = kPBytes + 64u;
+static_assert(fast_lds_bytes(kFastMaxC) <= kLds, "the staged block fits P's LDS");
 }  // namespace jmp
-constexpr uint32_t djump_lds_bytes(uint32_t maxc) {
-    return fast_lds_bytes(maxc) > jmp::kPBytes + 64u ? fast_lds_bytes(maxc) : jmp::kPBytes + 64u;
-}
 
-// xxh32 (seed 0) of [p, p + L) in global memory by lanes 0..15 (row 0 of the calling wave): lane
-// 4s + a loads dword a of stripe 4g + s (times P2), lane a runs accumulator a over the four
-// stripes with DPP row shifts (xxh32_row16 of s3hc_kernels.hip). Valid in lane 0.
-__device__ __forceinline__ uint32_t xxh32_row0(const uint8_t* __restrict__ p, uint32_t L) {
-    const uint32_t j = threadIdx.x & 15u, a = j & 3u, s = j >> 2;
-    const uint32_t ns = L >> 4, ng = ns >> 2;
+// xxh32 (seed 0) of [p, p + L) in global memory by lanes 0..3 of the calling wave (lane a runs
+// accumulator a; 32 stripes of loads in flight ahead of the chain). Valid in lane 0.
+__device__ __forceinline__ uint32_t xxh32_lane4(const uint8_t* __restrict__ p, uint32_t L) {
+    const uint32_t a = threadIdx.x & 3u;
+    const uint32_t ns = L >> 4;
     uint32_t acc = a == 0 ? XH1 + XH2 : (a == 1 ? XH2 : (a == 2 ? 0u : 0u - XH1));
-    auto step4 = [&](uint32_t m) {
-        acc = xh_rotl(acc + m, 13) * XH1;
-        acc = xh_rotl(acc + fdpp<0x104, 0xF>(m), 13) * XH1;
-        acc = xh_rotl(acc + fdpp<0x108, 0xF>(m), 13) * XH1;
-        acc = xh_rotl(acc + fdpp<0x10C, 0xF>(m), 13) * XH1;
-    };
-    const uint8_t* q = p + 16u * s + 4u * a;  // group g: q + 64 g
-    constexpr uint32_t kB = 8;
-    uint32_t g = 0;
-    for (; g + kB <= ng; g += kB) {
+    const uint8_t* q = p + 4u * a;  // stripe s: q + 16 s
+    constexpr uint32_t kB = 32;
+    uint32_t s = 0;
+    for (; s + kB <= ns; s += kB) {
         uint32_t m[kB];
 #pragma unroll
-        for (uint32_t k = 0; k < kB; ++k) m[k] = gld4(q + 64u * (g + k)) * XH2;
+        for (uint32_t k = 0; k < kB; ++k) m[k] = gld4(q + 16u * (s + k));
 #pragma unroll
-        for (uint32_t k = 0; k < kB; ++k) step4(m[k]);
+        for (uint32_t k = 0; k < kB; ++k) acc = xh_round(acc, m[k]);
     }
-    for (; g < ng; ++g) step4(gld4(q + 64u * g) * XH2);
-    for (uint32_t t = 4u * ng; t < ns; ++t) acc = xh_round(acc, gld4(p + 16u * t + 4u * a));
-    const uint32_t v1 = (uint32_t)__shfl((int)acc, 0, 16), v2 = (uint32_t)__shfl((int)acc, 1, 16);
-    const uint32_t v3 = (uint32_t)__shfl((int)acc, 2, 16), v4 = (uint32_t)__shfl((int)acc, 3, 16);
+    for (; s < ns; ++s) acc = xh_round(acc, gld4(q + 16u * s));
+    const uint32_t v1 = (uint32_t)__shfl((int)acc, 0, 4), v2 = (uint32_t)__shfl((int)acc, 1, 4);
+    const uint32_t v3 = (uint32_t)__shfl((int)acc, 2, 4), v4 = (uint32_t)__shfl((int)acc, 3, 4);
     uint32_t h = L >= 16u ? xh_rotl(v1, 1) + xh_rotl(v2, 7) + xh_rotl(v3, 12) + xh_rotl(v4, 18) : XH5;
     h += L;
     uint32_t t = ns * 16u;
@@ -1527,26 +1523,29 @@ __device__ __forceinline__ uint32_t xxh32_row0(const uint8_t* __restrict__ p, ui
     return h;
 }
 
-__global__ __launch_bounds__(fst::kTT) void k_djump(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                    const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
-                                                    uint32_t nunits, const uint8_t* __restrict__ unit_lb, FastArgs a,
-                                                    uint32_t maxc, uint32_t* __restrict__ blk_out,
-                                                    int32_t* __restrict__ blk_status) {
-    using namespace fst;
-    extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];  // (dtok_unit's stage, then P)
+__global__ __launch_bounds__(jmp::kT) void k_djump(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
+                                                   uint32_t nunits, const uint8_t* __restrict__ unit_lb, FastArgs a,
+                                                   uint32_t maxc, uint32_t* __restrict__ blk_out,
+                                                   int32_t* __restrict__ blk_status) {
+    using namespace jmp;
+    extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];  // (dtok_unit's staged block, then P)
     uint16_t* P = (uint16_t*)dsm;
     uint32_t* P32 = (uint32_t*)dsm;
-    __shared__ uint32_t qrec[jmp::kQ], qpos[jmp::kQ];
+    __shared__ uint32_t qrec[kQ], qpos[kQ];
     __shared__ uint32_t qn;
-    __shared__ uint32_t jscr[16];
+    __shared__ uint32_t jscr[32];
     const uint32_t t = threadIdx.x;
     for (uint32_t u = blockIdx.x; u < nunits; u += gridDim.x) {
         FastUnit F;
-        const bool ok = dtok_unit(u, src, blk, units, unit_lb, a, maxc, &F);  // (a unit it leaves: bh 0)
-        if (!ok) {
+        // token index and records with all 16 waves (1024 speculative segments)
+        if (!dtok_unit<kT>(u, src, blk, units, unit_lb, a, maxc, &F)) {  // (a unit it leaves: bh 0)
             __syncthreads();
             continue;
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the records are in memory before the barrier
+        __syncthreads();
+        [[maybe_unused]] const uint64_t tj0 = FP_NOW();
         const DecUnit Un = units[u];
         const DecBlock B = blk[Un.first];
         const uint8_t* in = src + B.src_off;
@@ -1554,25 +1553,28 @@ __global__ __launch_bounds__(fst::kTT) void k_djump(const uint8_t* __restrict__ 
         const uint2* rec = a.rec + B.tok;
         const uint32_t N = F.ntok, U = F.U, C = B.csize;
         if (t == 0) qn = 0u;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the records are in memory before the barrier
-        __syncthreads();
-        // ---- output positions: thread t's records [t K, t K + K)
-        const uint32_t K = (N + kTT - 1u) / kTT, r0 = umin_(N, t * K), r1 = umin_(N, r0 + K);
+        // ---- output positions: thread t's records [t K, t K + K), K <= 11 (N <= kFastMaxTok)
+        const uint32_t K = (N + kT - 1u) / kT, r0 = umin_(N, t * K), r1 = umin_(N, r0 + K);
         uint32_t mine = 0;
-        for (uint32_t r = r0; r < r1; ++r) {
-            const uint2 v = rec[r];
-            mine += (v.x >> 15) + ((v.y & 0xFFFFu) ? (v.y >> 16) + 4u : 0u);
+        {
+            uint2 v[4];
+            for (uint32_t r = r0; r < r1; r += 4u) {
+#pragma unroll
+                for (uint32_t e = 0; e < 4u; ++e) v[e] = r + e < r1 ? rec[r + e] : make_uint2(0u, 0u);
+#pragma unroll
+                for (uint32_t e = 0; e < 4u; ++e) mine += (v[e].x >> 15) + ((v[e].y & 0xFFFFu) ? (v[e].y >> 16) + 4u : 0u);
+            }
         }
         uint32_t tot;
-        uint32_t o = wg_excl_scan<kTT / 64>(mine, jscr, &tot);
+        uint32_t o = wg_excl_scan<kT / 64>(mine, jscr, &tot);
         // ---- pointers and literals (sequences longer than kShort: the whole workgroup, below)
         for (uint32_t r = r0; r < r1; ++r) {
             const uint2 v = rec[r];
             const uint32_t ll = v.x >> 15, lit = v.x & 0x7FFFu, off = v.y & 0xFFFFu;
             const uint32_t ml = off ? (v.y >> 16) + 4u : 0u;
-            if (ll + ml > jmp::kShort) {
+            if (ll + ml > kShort) {
                 const uint32_t qi = atomicAdd(&qn, 1u);
-                if (qi < jmp::kQ) {
+                if (qi < kQ) {
                     qrec[qi] = r;
                     qpos[qi] = o;
                     o += ll + ml;
@@ -1600,54 +1602,69 @@ __global__ __launch_bounds__(fst::kTT) void k_djump(const uint8_t* __restrict__ 
             o += ll + ml;
         }
         __syncthreads();
-        const uint32_t nq = umin_(qn, jmp::kQ);
+        const uint32_t nq = umin_(qn, kQ);
         for (uint32_t e = 0; e < nq; ++e) {
             const uint2 v = rec[qrec[e]];
             const uint32_t o0 = qpos[e], ll = v.x >> 15, lit = v.x & 0x7FFFu, off = v.y & 0xFFFFu;
             const uint32_t ml = off ? (v.y >> 16) + 4u : 0u;
-            for (uint32_t i = t; i < ll; i += kTT) {
+            for (uint32_t i = t; i < ll; i += kT) {
                 out[o0 + i] = in[lit + i];
                 P[o0 + i] = (uint16_t)(o0 + i);
             }
             const uint32_t md = o0 + ll, ms = md - off;
-            for (uint32_t i = t; i < ml; i += kTT) P[md + i] = (uint16_t)(ms + (off >= ml ? i : i % off));
+            for (uint32_t i = t; i < ml; i += kT) P[md + i] = (uint16_t)(ms + (off >= ml ? i : i % off));
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // literal bytes in memory before the gathers below
         __syncthreads();
+        [[maybe_unused]] const uint64_t tj1 = FP_NOW();
         // ---- pointer jumping (pairs of u16 per dword; in place: a pointer read mid-update is an
-        // older or newer point of the same chain)
+        // older or newer point of the same chain). kJ pairs per thread at a time: every pair read
+        // and every gather of the batch in flight before the first use
         const uint32_t Up = (U + 1u) >> 1;
+        [[maybe_unused]] uint32_t nround = 0;
         for (;;) {
             int ch = 0;
-            for (uint32_t k = t; k < Up; k += kTT) {
-                const uint32_t pr = P32[k], b0 = 2u * k, b1 = b0 + 1u;
-                uint32_t lo = pr & 0xFFFFu, hi = pr >> 16;
-                bool c = false;
-                if (lo != b0) {
-                    const uint32_t q = P[lo];
-                    if (q != lo) { lo = q; c = true; }
+            constexpr uint32_t kJ = 8;
+            for (uint32_t k0 = t; k0 < Up; k0 += kT * kJ) {
+                uint32_t pr[kJ], q[kJ][2];
+#pragma unroll
+                for (uint32_t e = 0; e < kJ; ++e) {
+                    const uint32_t k = k0 + kT * e;
+                    pr[e] = k < Up ? P32[k] : 0u;  // (beyond U: pair 0 -> 0, a root)
                 }
-                if (b1 < U && hi != b1) {
-                    const uint32_t q = P[hi];
-                    if (q != hi) { hi = q; c = true; }
+#pragma unroll
+                for (uint32_t e = 0; e < kJ; ++e) {
+                    q[e][0] = P[pr[e] & 0xFFFFu];
+                    q[e][1] = P[pr[e] >> 16];
                 }
-                if (c) {
-                    P32[k] = lo | (hi << 16);
-                    ch = 1;
+#pragma unroll
+                for (uint32_t e = 0; e < kJ; ++e) {
+                    const uint32_t k = k0 + kT * e;
+                    const uint32_t lo = pr[e] & 0xFFFFu, hi = pr[e] >> 16;
+                    // a root points to itself (its gather returns it: no change); the odd tail
+                    // entry past U is kept as read
+                    const uint32_t nlo = q[e][0];
+                    const uint32_t nhi = 2u * k + 1u < U ? q[e][1] : hi;
+                    if (k < Up && (nlo != lo || nhi != hi)) {
+                        P32[k] = nlo | (nhi << 16);
+                        ch = 1;
+                    }
                 }
             }
+            ++nround;
             if (!__syncthreads_or(ch)) break;
         }
-        // ---- every dword with a match byte: its bytes from their literals, eight dwords per thread
+        [[maybe_unused]] const uint64_t tj2 = FP_NOW();
+        // ---- every dword with a match byte: its bytes from their literals, kE dwords per thread
         // at a time (every gather of a batch in flight before its stores)
         const bool al = ((uintptr_t)out & 3u) == 0u;
-        constexpr uint32_t kE = 8;
-        for (uint32_t b0 = 4u * t; b0 < U; b0 += 4u * kTT * kE) {
+        constexpr uint32_t kE = 4;
+        for (uint32_t b0 = 4u * t; b0 < U; b0 += 4u * kT * kE) {
             uint32_t v[kE], pp[kE][4];
             bool need[kE];
 #pragma unroll
             for (uint32_t e = 0; e < kE; ++e) {
-                const uint32_t b = b0 + 4u * kTT * e;
+                const uint32_t b = b0 + 4u * kT * e;
                 const uint32_t n = b < U ? umin_(4u, U - b) : 0u;
                 const uint32_t w0 = n ? P32[b >> 1] : 0u, w1 = n ? P32[(b >> 1) + 1u] : 0u;
                 pp[e][0] = w0 & 0xFFFFu;
@@ -1658,7 +1675,7 @@ __global__ __launch_bounds__(fst::kTT) void k_djump(const uint8_t* __restrict__ 
             }
 #pragma unroll
             for (uint32_t e = 0; e < kE; ++e) {
-                const uint32_t b = b0 + 4u * kTT * e;
+                const uint32_t b = b0 + 4u * kT * e;
                 v[e] = 0u;
                 if (!need[e]) continue;
                 const uint32_t n = umin_(4u, U - b);
@@ -1674,7 +1691,7 @@ __global__ __launch_bounds__(fst::kTT) void k_djump(const uint8_t* __restrict__ 
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (every gather of the batch before its stores)
 #pragma unroll
             for (uint32_t e = 0; e < kE; ++e) {
-                const uint32_t b = b0 + 4u * kTT * e;
+                const uint32_t b = b0 + 4u * kT * e;
                 if (!need[e]) continue;
                 const uint32_t n = umin_(4u, U - b);
                 if (n == 4u && al) {
@@ -1686,12 +1703,22 @@ __global__ __launch_bounds__(fst::kTT) void k_djump(const uint8_t* __restrict__ 
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (t < 16u) {
-            const uint32_t h = xxh32_row0(out, U);
+        [[maybe_unused]] const uint64_t tj3 = FP_NOW();
+        if (t < 4u) {
+            const uint32_t h = xxh32_lane4(out, U);
             if (t == 0) {
                 if (a.bh) a.bh[Un.first] = (1ull << 32) | h;
                 blk_out[Un.first] = U;
                 blk_status[Un.first] = S3HC_OK;
+#ifdef FPROF
+                const uint64_t tj4 = FP_NOW();
+                FP_ADD(25, tj1 - tj0);
+                FP_ADD(26, tj2 - tj1);
+                FP_ADD(27, tj3 - tj2);
+                FP_ADD(28, tj4 - tj3);
+                FP_ADD(29, nround);
+                FP_ADD(30, 1);
+#endif
             }
         }
         __syncthreads();
@@ -1852,10 +1879,10 @@ hipError_t launch_fast_small(const uint8_t* src, uint8_t* dst, const DecBlock* b
     const uint32_t maxc = a.maxc < kFastMaxC ? a.maxc : kFastMaxC;
 #if S3HC_SMALL_JUMP
     static const hipError_t attr = hipFuncSetAttribute((const void*)k_djump, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)djump_lds_bytes(kFastMaxC));  // (> 64 KiB of dynamic LDS)
+                                                       (int)jmp::kLds);  // (> 64 KiB of dynamic LDS)
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL(k_djump, dim3(nunits), dim3(fst::kTT), djump_lds_bytes(maxc), st, src, dst, blk, units, nunits,
-                       unit_lb, a, maxc, blk_out, blk_status);
+    hipLaunchKernelGGL(k_djump, dim3(nunits), dim3(jmp::kT), jmp::kLds, st, src, dst, blk, units, nunits, unit_lb, a,
+                       maxc, blk_out, blk_status);
 #else
     hipLaunchKernelGGL(k_dsmall, dim3(nunits), dim3(fst::kTT), fast_lds_bytes(maxc), st, src, dst, blk, units, nunits,
                        unit_lb, a, maxc, blk_out, blk_status);

@@ -2381,6 +2381,10 @@ __global__ void k_dframe_verify(const uint8_t* __restrict__ src, const uint64_t*
     if ((flg & 0x04) && got_hash[f] != fwant[f]) fstatus[f] = S3HC_CHECKSUM;
 }
 
+#ifndef S3HC_CLOSE_ROW16  // 1: 16 lanes per frame (xxh32_row16), 0: 4 lanes per frame (xxh32_lanes)
+#define S3HC_CLOSE_ROW16 0
+#endif
+constexpr uint32_t kCloseLanes = S3HC_CLOSE_ROW16 ? 16u : 4u;
 // k_dframe_finish + k_xxh32_ranges + k_dframe_verify in one launch (same rules, same results):
 // the 16 lanes of a DPP row own frame f; each sums the frame's block results (frames hold few
 // blocks), the row hashes the frame's output (xxh32_row16: four frames per wave, a 4096-frame
@@ -2396,7 +2400,7 @@ __global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__
                                                      const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ fwant,
                                                      uint32_t n, const int32_t* fstat_in, int32_t* fstatus,
                                                      uint32_t* __restrict__ out_len, uint32_t* __restrict__ got_hash) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, f = gid >> 4, j = gid & 15;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, f = gid / kCloseLanes, j = gid % kCloseLanes;
     const bool act = f < n;
     int st = S3HC_OK;
     uint64_t tot = 0;
@@ -2417,7 +2421,11 @@ __global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__
     }
     const uint32_t L = st == S3HC_OK ? (uint32_t)tot : 0u;
     const bool have = (pre >> 32) != 0;
+#if S3HC_CLOSE_ROW16
     uint32_t h = xxh32_row16<8>(out + (act ? out_off[f] : 0), have ? 0u : L, act, j);
+#else
+    uint32_t h = xxh32_lanes<32, true>(out + (act ? out_off[f] : 0), have ? 0u : L, act, j);
+#endif
     if (!act || j != 0) return;
     if (have) h = (uint32_t)pre;
     out_len[f] = L;
@@ -2531,7 +2539,7 @@ hipError_t launch_dframe_close(const uint8_t* src, const uint64_t* frame_off, co
                                const uint64_t* out_off, const uint32_t* fwant, uint32_t n, const int32_t* fstat_in,
                                int32_t* fstatus, uint32_t* out_len, uint32_t* got_hash, hipStream_t st) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_dframe_close, dim3(cdiv((uint64_t)n * 16, 64)), dim3(64), 0, st, src, frame_off, blk_base, nblk,
+    hipLaunchKernelGGL(k_dframe_close, dim3(cdiv((uint64_t)n * kCloseLanes, 64)), dim3(64), 0, st, src, frame_off, blk_base, nblk,
                        blocks, blk_out, blk_status, blk_hash, out, out_off, fwant, n, fstat_in, fstatus, out_len,
                        got_hash);
     return hipGetLastError();

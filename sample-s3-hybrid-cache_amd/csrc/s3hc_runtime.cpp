@@ -121,14 +121,22 @@ static inline uint32_t rd32h(const uint8_t* p) {
 }
 
 // ------------------------------------------------------------ device memory
+// Size for a buffer of capacity cap that must hold n > cap bytes: a regrowth of a small buffer
+// (< 256 MiB) takes 1.5x its old capacity, so batches whose sizes vary do not reallocate (host
+// pinned frees cost ~0.6 ms each); first allocations and large buffers are exact.
+static inline size_t regrow(size_t n, size_t cap) {
+    return cap && n < ((size_t)256 << 20) ? std::max<size_t>(n, cap + cap / 2) : n;
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
     ~DevBuf() { if (p) (void)hipFree(p); }
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
+        // a buffer that grows again (per-batch sizes vary) takes 1.5x: no realloc churn
+        size_t want = std::max<size_t>(regrow(n, cap), 256);
         if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
-        size_t want = std::max<size_t>(n, 256);
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
         return e;
@@ -149,8 +157,8 @@ struct PinnedBuf {
     ~PinnedBuf() { if (p) (void)hipHostFree(p); }
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
+        const size_t want = std::max<size_t>(regrow(n, cap), 1 << 16);
         if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
-        const size_t want = std::max<size_t>(n, 1 << 16);
         hipError_t e = hipHostMalloc((void**)&p, want, hipHostMallocDefault);
         if (e == hipSuccess) cap = want;
         return e;
@@ -159,7 +167,7 @@ struct PinnedBuf {
     hipError_t ensure_keep(size_t n, size_t keep) {
         if (n <= cap) return hipSuccess;
         uint8_t* q = nullptr;
-        const size_t want = std::max<size_t>(n, 1 << 16);
+        const size_t want = std::max<size_t>(regrow(n, cap), 1 << 16);
         hipError_t e = hipHostMalloc((void**)&q, want, hipHostMallocDefault);
         if (e != hipSuccess) return e;
         if (p) {

@@ -2,7 +2,7 @@
 """Phase timers of k_dsmall (the range reader's fused small-launch decode) in a diagnostic build
 (S3HC_DIAG_LEVEL=10): `nb` 64 KiB log-text frames (default 11, one 256 KiB reader batch) decoded
 through the host-walked path `steps` times. Prints the token-index phases (per wave, cycles) and
-the executor phases (per block, cycles) of one launch, and the wall time per call.
+the executor phases (k_dsmall) or the pointer-jumping phases (k_djump) per block, cycles, and the wall time per call.
 Usage: S3HC_LIB_PATH=.../build/diag/lib_prof.so python tools/fprof_small.py [nb]"""
 import ctypes
 import json
@@ -18,6 +18,7 @@ import synth  # noqa: E402
 TOK = {0: "stage", 1: "walk1", 2: "walk2", 3: "chain", 4: "count_alloc", 5: "emit", 6: "total"}
 EXE = {16: "decode_next", 17: "literals", 18: "round0", 19: "pending", 20: "flush_or_slow", 21: "total",
        22: "windows", 23: "rounds"}
+JMP = {25: "positions_pointers", 26: "jumping", 27: "gather", 28: "hash", 29: "rounds"}
 
 
 def main():
@@ -42,7 +43,8 @@ def main():
     units = v[24] or 1
     out = {"frames": nb, "compressed": len(frames), "call_us": round(dt * 1e6, 1),
            "dtok_per_wave_cycles": {n: round(v[i] / (4 * wg), 1) for i, n in TOK.items()},
-           "dexec_per_block": {n: round(v[i] / units, 1) for i, n in EXE.items()}}
+           "dexec_per_block": {n: round(v[i] / units, 1) for i, n in EXE.items()},
+           "djump_per_block": {n: round(v[i] / (v[30] or 1), 1) for i, n in JMP.items()}}
     print(json.dumps(out, indent=1))
 
 

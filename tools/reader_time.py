@@ -50,6 +50,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, default=512)
     ap.add_argument("--only", default="")
+    ap.add_argument("--depths", default="3,4")
     a = ap.parse_args()
     eng = S.Engine(0)
     data = synth.log_text(a.mib << 20, 7)
@@ -61,7 +62,7 @@ def main():
         h_fr = eng.host_alloc(len(fr))
         h_fr.view()[:] = np.frombuffer(fr, dtype=np.uint8)
         h_out = eng.host_alloc(len(data))
-        for depth in (3, 4):
+        for depth in [int(x) for x in a.depths.split(",")]:
             r = run(eng, h_fr, len(fr), len(data), h_out, 256 << 10, depth)
             assert bytes(h_out.view()[-item:]) == data[-item:]
             res[f"{name}_depth{depth}"] = r
