@@ -54,7 +54,7 @@ constexpr uint32_t kMaxC = kFastMaxC;
 #else
 #define S3HC_HOPF hop
 #endif
-#ifndef S3HC_DTOK_BAL  // 1: records by sequence rank, 2: coalesced wave-interleaved rounds, 0: by bitmap words
+#ifndef S3HC_DTOK_BAL  // 1: records by sequence rank, 0: by bitmap words
 #define S3HC_DTOK_BAL 1
 #endif
 constexpr uint32_t kTT = S3HC_DTOK_TT;         // k_dtok threads = speculative segments per block
@@ -481,93 +481,6 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
                 emit(q, k);
             }
         }
-    }
-#elif S3HC_DTOK_BAL == 2
-    // wave-interleaved: wave wq takes the sequences [wq Q, wq Q + Q) (Q a multiple of 64) in
-    // rounds of 64 consecutive ones, lane l the round's l-th; its token position comes from a
-    // 64-entry LDS list the wave expands from the bitmap words at its cursor, and the round's
-    // records are stored coalesced (one 512-byte store per round)
-    static_assert(TT == 256, "the interleaved record pass: four waves");
-    uint16_t* base = J[0];
-    base[g] = (uint16_t)r0;
-    if (g == 0) base[TT] = (uint16_t)N;
-    __syncthreads();
-    {
-        const uint32_t wq = g >> 6, ln = g & 63u;
-        uint16_t* lst = &J[1][0] + 64u * wq;  // (J[1]: TT + 2 >= 4 x 64 entries)
-        auto wscan = [&](uint32_t x) {        // inclusive scan over the wave
-#pragma unroll
-            for (uint32_t d = 1; d < 64; d <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-                if (ln >= d) x += y;
-            }
-            return x;
-        };
-        const uint32_t Q = ((N + 255u) / 256u) * 64u;
-        const uint32_t R0 = umin_(N, wq * Q), R1 = umin_(N, R0 + Q);
-        uint32_t carry = 0;
-        if (R0 < R1) {
-            uint32_t t = 0;
-#pragma unroll
-            for (uint32_t step = TT / 2; step; step >>= 1)
-                if (base[t + step] <= R0) t += step;
-            uint32_t w = 4u * t, xb = bits[w], skip = R0 - base[t];
-            for (uint32_t pc = (uint32_t)__builtin_popcount(xb); skip >= pc; pc = (uint32_t)__builtin_popcount(xb)) {
-                skip -= pc;
-                xb = bits[++w];
-            }
-            for (; skip; --skip) xb &= xb - 1u;
-            for (uint32_t R = R0; R < R1;) {
-                const uint32_t wl = ln == 0 ? xb : (w + ln < nbw ? bits[w + ln] : 0u);
-                const uint32_t c = (uint32_t)__builtin_popcount(wl);
-                const uint32_t inc = wscan(c), ex = inc - c;
-                {
-                    uint32_t x = wl, idx = ex;
-                    while (x && idx < 64u) {
-                        lst[idx++] = (uint16_t)(((w + ln) << 5) + (uint32_t)__builtin_ctz(x));
-                        x &= x - 1u;
-                    }
-                }
-                wsync_blk();
-                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-                const uint32_t got = umin_(umin_(tot, 64u), R1 - R);
-                const bool mine = ln < got;
-                const uint32_t q = mine ? lst[ln] : 0u;
-                Tok T;
-                T.ll = T.ml = T.off = 0;
-                T.nxt = END;
-                if (mine) T = S3HC_HOPF(stage, mis, q, C);
-                const uint32_t len = T.ll + T.ml;
-                const uint32_t li = wscan(len);
-                if (mine) {
-                    const uint32_t lit = T.ll == 0 ? 0u : q + 1u + (T.ll >= 15u ? (T.ll - 15u) / 255u + 1u : 0u);
-                    uint32_t y = 0;
-                    if (T.nxt != END) {
-                        bad |= T.off == 0u;
-                        minsl = min(minsl, (int32_t)(carry + li - len + T.ll) - (int32_t)T.off);
-                        y = T.off | ((T.ml - 4u) << 16);
-                    }
-                    rec[R + ln] = make_uint2(lit | (T.ll << 15), y);
-                }
-                carry += (uint32_t)__builtin_amdgcn_readlane((int)li, 63);
-                // the cursor past the round's last sequence
-                if (got >= tot) {
-                    w += 64u;
-                    xb = w < nbw ? bits[w] : 0u;
-                } else {
-                    const uint64_t hit = __ballot(ex <= got && got < inc);
-                    const uint32_t L = (uint32_t)__builtin_ctzll(hit);
-                    uint32_t x = wl;
-                    if (ln == L)
-                        for (uint32_t k = got - ex; k; --k) x &= x - 1u;
-                    w += L;
-                    xb = (uint32_t)__builtin_amdgcn_readlane((int)x, (int)L);
-                }
-                R += got;
-                wsync_blk();  // (the next round rewrites the list)
-            }
-        }
-        o = ln == 63u ? carry : 0u;  // (the scan below: earlier waves' bytes at every lane of mine)
     }
 #else
     // each thread decodes the true tokens of its four bitmap words (positions [128 g, 128 g + 128))
@@ -1726,108 +1639,6 @@ __global__ __launch_bounds__(jmp::kT) void k_djump(const uint8_t* __restrict__ s
 }
 
 // ------------------------------------------------------------------ k_dexec
-// The hashing wave of k_dexec: xxh32 (seed 0) of the output of up to four executor waves, one
-// 16-lane group per executor g (its LDS ring at rings + g kORW, its progress words hs[2g] bytes
-// final / hs[2g + 1] bytes hashed: the dexec_unit protocol), Ug bytes (a group without a unit:
-// has = false). Lane 4s + a of a group loads dword a of the next four stripes' stripe s (times
-// P2); accumulator a runs over the four with DPP row shifts (no LDS round trip), so every lane of
-// the group holds its accumulator's value. Returns the unit's hash (every lane of its group).
-__device__ __forceinline__ uint32_t hash_rings(const uint32_t* rings, volatile uint32_t* hs, uint32_t Ug, bool has) {
-    using namespace fst;
-    const uint32_t lane = threadIdx.x & 63u, grp = lane >> 4, j = lane & 15u, ha = j & 3u, s = j >> 2;
-    const uint32_t* ring = rings + grp * kORW;
-    uint32_t hacc = ha == 0 ? XH1 + XH2 : (ha == 1 ? XH2 : (ha == 2 ? 0u : 0u - XH1));
-    const uint32_t hns = Ug >> 4;  // whole stripes
-    uint32_t hsn = 0;              // stripes hashed (group-uniform)
-    bool done = !has;
-    for (;;) {
-        const uint32_t avail = done ? 0u : hs[2u * grp];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint32_t lim = done ? 0u : umin_(avail >> 4, hns);
-        bool moved = false;
-        while (__ballot(hsn + 4u <= lim)) {
-            if (hsn + 4u <= lim) {
-                const uint32_t mv = ring[((16u * (hsn + s) + 4u * ha) & kORM) >> 2] * XH2;
-                hacc = xh_rotl(hacc + mv, 13) * XH1;
-                hacc = xh_rotl(hacc + fdpp<0x104, 0xF>(mv), 13) * XH1;
-                hacc = xh_rotl(hacc + fdpp<0x108, 0xF>(mv), 13) * XH1;
-                hacc = xh_rotl(hacc + fdpp<0x10C, 0xF>(mv), 13) * XH1;
-                hsn += 4u;
-                moved = true;
-            }
-        }
-        while (__ballot(hsn < lim)) {
-            if (hsn < lim) {
-                hacc = xh_round(hacc, ring[((16u * hsn + 4u * ha) & kORM) >> 2]);
-                ++hsn;
-                moved = true;
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (ring reads done before the slots are released)
-        if (!done && moved && j == 0) hs[2u * grp + 1u] = 16u * hsn;
-        if (!done && avail >= Ug && hsn == hns) done = true;
-        if (!__ballot(!done)) break;
-        if (!__ballot(moved)) __builtin_amdgcn_s_sleep(2);
-    }
-    // (lanes 16 grp + a hold accumulator a; row broadcasts within the group)
-    const uint32_t v1 = (uint32_t)__shfl((int)hacc, (int)(16u * grp), 64), v2 = (uint32_t)__shfl((int)hacc, (int)(16u * grp + 1u), 64);
-    const uint32_t v3 = (uint32_t)__shfl((int)hacc, (int)(16u * grp + 2u), 64), v4 = (uint32_t)__shfl((int)hacc, (int)(16u * grp + 3u), 64);
-    uint32_t h = Ug >= 16u ? xh_rotl(v1, 1) + xh_rotl(v2, 7) + xh_rotl(v3, 12) + xh_rotl(v4, 18) : XH5;
-    h += Ug;
-    const uint8_t* rb = (const uint8_t*)ring;
-    uint32_t p = hns * 16u;
-    for (; p + 4u <= Ug; p += 4u) {
-        const uint32_t w = (uint32_t)rb[p & kORM] | ((uint32_t)rb[(p + 1u) & kORM] << 8) |
-                           ((uint32_t)rb[(p + 2u) & kORM] << 16) | ((uint32_t)rb[(p + 3u) & kORM] << 24);
-        h = xh_rotl(h + w * XH3, 17) * XH4;
-    }
-    for (; p < Ug; ++p) h = xh_rotl(h + (uint32_t)rb[p & kORM] * XH5, 11) * XH1;
-    h ^= h >> 15;
-    h *= XH2;
-    h ^= h >> 13;
-    h *= XH3;
-    h ^= h >> 16;
-    return h;
-}
-
-#ifndef S3HC_DEXEC_HASH  // 1: k_dexec = four executors + a hashing wave per workgroup; 0: one executor per workgroup, the frame close hashes
-#define S3HC_DEXEC_HASH 0
-#endif
-#if S3HC_DEXEC_HASH
-// Four executor waves (one unit each, k_dtok's records) and, when the frame close takes hashes
-// (a.bh), a fifth wave hashing their output from the LDS rings while they run: the frame's
-// content xxh32 without a second pass over the output. The four units of a workgroup are
-// consecutive; the grid strides over groups of four.
-// (<= 128 VGPRs: four waves per SIMD, three workgroups per CU)
-__global__ __launch_bounds__(5 * 64) __attribute__((amdgpu_waves_per_eu(4))) void k_dexec(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                  const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
-                                                  uint32_t nunits, const uint64_t* __restrict__ ucount,
-                                                  uint32_t* __restrict__ blk_out, int32_t* __restrict__ blk_status,
-                                                  FastArgs a) {
-    const uint32_t nu = unit_count(ucount, nunits);
-    __shared__ __attribute__((aligned(16))) uint32_t ring[4 * fst::kORW];
-    __shared__ DexLds dl[4];
-    __shared__ uint32_t hs[8];
-    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // (wave-uniform: scalar ring base)
-    for (uint32_t b = 4u * blockIdx.x; b < nu; b += 4u * gridDim.x) {
-        if (threadIdx.x < 8u) hs[threadIdx.x] = 0u;
-        __syncthreads();
-        if (wv < 4u) {
-            const uint32_t u = b + wv;
-            if (u < nu && a.unit_fast[u])
-                dexec_unit(u, src, dst, blk, units, blk_out, blk_status, a, a.fu[u], ring + wv * fst::kORW,
-                           a.bh ? hs + 2u * wv : nullptr, dl + wv);
-        } else if (a.bh) {
-            const uint32_t u = b + ((threadIdx.x & 63u) >> 4);
-            const bool has = u < nu && a.unit_fast[u];
-            const uint32_t h = hash_rings(ring, hs, has ? a.fu[u].U : 0u, has);
-            if (has && (threadIdx.x & 15u) == 0u) a.bh[units[u].first] = (1ull << 32) | h;
-        }
-        __syncthreads();
-    }
-}
-constexpr uint32_t kDexecUnits = 4, kDexecThreads = 5 * 64;
-#else
 // One executor wave per workgroup (k_dtok's records); the frame close hashes the output.
 // (<= 128 VGPRs: 4 waves per SIMD, a 4096-block batch resident at once)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_dexec(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -1845,8 +1656,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     }
 }
 constexpr uint32_t kDexecUnits = 1, kDexecThreads = 64;
-#endif
-bool fast_exec_hashes() { return S3HC_DEXEC_HASH != 0; }
+// (the frame close hashes k_dexec's output: a hashing wave beside the executors costs a 4096-block
+// batch its one-pass residency)
+bool fast_exec_hashes() { return false; }
 
 // ================================================================ launchers
 static inline uint32_t fcdiv(uint64_t x, uint64_t y) { return (uint32_t)((x + y - 1) / y); }

@@ -241,75 +241,6 @@ __device__ __forceinline__ uint32_t xxh32_lanes(const uint8_t* __restrict__ p, u
     return h;
 }
 
-// xxh32 of [p, p + L) by the 16 lanes of a DPP row (one row per range: act row-uniform).
-// Lane 4s + a loads dword a of stripe 4g + s and multiplies it by P2 (off the chain, four stripes
-// per load instruction); lane a (s = 0) runs accumulator a over the four stripes, taking the
-// others' products by row shifts (no LDS round trip). Per 16 bytes the chain costs one add (its
-// DPP operand included), a rotate and a multiply instead of k_dframe_close's former load, two
-// multiplies, add and rotate in four lanes of a range. Valid in lane j == 0 of an active row.
-template <uint32_t kB>  // four-stripe groups per load batch (loads in flight: 2 kB per lane)
-__device__ __forceinline__ uint32_t xxh32_row16(const uint8_t* __restrict__ p, uint32_t L, bool act, uint32_t j) {
-    const uint32_t a = j & 3u, s = j >> 2;
-    const uint32_t ns = act ? L >> 4 : 0u, ng = ns >> 2;
-    uint32_t acc = a == 0 ? XP1 + XP2 : (a == 1 ? XP2 : (a == 2 ? 0u : 0u - XP1));
-    auto step4 = [&](uint32_t m) {
-        acc = rotl32(acc + m, 13) * XP1;
-        acc = rotl32(acc + dpp0<0x104, 0xF>(m), 13) * XP1;
-        acc = rotl32(acc + dpp0<0x108, 0xF>(m), 13) * XP1;
-        acc = rotl32(acc + dpp0<0x10C, 0xF>(m), 13) * XP1;
-    };
-    uint32_t g = 0;
-    if ((((uintptr_t)p) & 3) == 0) {
-        const uint32_t* w = (const uint32_t*)p + 4u * s + a;  // stripe 4 g + s, dword a: w[16 g]
-        uint32_t b0[kB], b1[kB];
-        const uint32_t nb = ng / kB;
-#define XRLD(buf, bi)                                                                              \
-    {                                                                                              \
-        const uint32_t bb_ = (bi) < nb ? (bi) : 0u;                                                \
-        _Pragma("unroll") for (uint32_t k = 0; k < kB; ++k) buf[k] = w[16u * (bb_ * kB + k)];      \
-    }
-        if (nb) XRLD(b0, 0u)  // (clamped reloads stay within the range's first batch)
-        for (uint32_t b = 0; b < nb; b += 2) {
-            XRLD(b1, b + 1)
-#pragma unroll
-            for (uint32_t k = 0; k < kB; ++k) step4(b0[k] * XP2);
-            XRLD(b0, b + 2)
-            if (b + 1 < nb) {
-#pragma unroll
-                for (uint32_t k = 0; k < kB; ++k) step4(b1[k] * XP2);
-            }
-        }
-#undef XRLD
-        for (g = nb * kB; g < ng; ++g) step4(w[16u * g] * XP2);
-        for (uint32_t t = 4u * ng; t < ns; ++t) acc = xround(acc, ((const uint32_t*)p)[4u * t + a]);
-    } else {
-        for (; g < ng; ++g) step4(gld32u(p + 16u * (4u * g + s) + 4u * a, 4u) * XP2);
-        for (uint32_t t = 4u * ng; t < ns; ++t) acc = xround(acc, gld32u(p + 16u * t + 4u * a, 4u));
-    }
-    const int rb = lane_id() & ~15;
-    const uint32_t v1 = __shfl(acc, rb), v2 = __shfl(acc, rb + 1), v3 = __shfl(acc, rb + 2), v4 = __shfl(acc, rb + 3);
-    if (!act || j != 0) return 0u;
-    uint32_t h = L >= 16 ? rotl32(v1, 1) + rotl32(v2, 7) + rotl32(v3, 12) + rotl32(v4, 18) : XP5;
-    h += L;
-    uint32_t t = ns * 16;
-    while (t + 4 <= L) {
-        h += gld32u(p + t, L - t) * XP3;
-        h = rotl32(h, 17) * XP4;
-        t += 4;
-    }
-    while (t < L) {
-        h += (uint32_t)p[t] * XP5;
-        h = rotl32(h, 11) * XP1;
-        t++;
-    }
-    h ^= h >> 15;
-    h *= XP2;
-    h ^= h >> 13;
-    h *= XP3;
-    h ^= h >> 16;
-    return h;
-}
-
 // out[r] = xxh32(base + off[r], len[r], seed 0). Lanes 4r..4r+3 run the 4 accumulator chains
 // (gid = global thread index of the calling grid's xxh32 threads).
 template <uint32_t kIF, bool kPipe>
@@ -2381,14 +2312,10 @@ __global__ void k_dframe_verify(const uint8_t* __restrict__ src, const uint64_t*
     if ((flg & 0x04) && got_hash[f] != fwant[f]) fstatus[f] = S3HC_CHECKSUM;
 }
 
-#ifndef S3HC_CLOSE_ROW16  // 1: 16 lanes per frame (xxh32_row16), 0: 4 lanes per frame (xxh32_lanes)
-#define S3HC_CLOSE_ROW16 0
-#endif
-constexpr uint32_t kCloseLanes = S3HC_CLOSE_ROW16 ? 16u : 4u;
+constexpr uint32_t kCloseLanes = 4;  // lanes per frame (16 per frame with DPP-shared P2 products measured slower)
 // k_dframe_finish + k_xxh32_ranges + k_dframe_verify in one launch (same rules, same results):
-// the 16 lanes of a DPP row own frame f; each sums the frame's block results (frames hold few
-// blocks), the row hashes the frame's output (xxh32_row16: four frames per wave, a 4096-frame
-// batch on every SIMD), its lane 0 checks the EndMark. fstat_in: statuses set before the
+// lanes 4f..4f+3 own frame f; each sums the frame's block results (frames hold few blocks), the
+// four hash the frame's output, lane 4f checks the EndMark. fstat_in: statuses set before the
 // decode (nullptr: none). blk_hash (nullable): hashes the large-block path computed while
 // decoding (1 << 32 | xxh32 per block); a frame of one such block skips its own pass.
 // got_hash (nullable): each frame's content xxh32.
@@ -2421,11 +2348,7 @@ __global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__
     }
     const uint32_t L = st == S3HC_OK ? (uint32_t)tot : 0u;
     const bool have = (pre >> 32) != 0;
-#if S3HC_CLOSE_ROW16
-    uint32_t h = xxh32_row16<8>(out + (act ? out_off[f] : 0), have ? 0u : L, act, j);
-#else
     uint32_t h = xxh32_lanes<32, true>(out + (act ? out_off[f] : 0), have ? 0u : L, act, j);
-#endif
     if (!act || j != 0) return;
     if (have) h = (uint32_t)pre;
     out_len[f] = L;

@@ -1996,8 +1996,24 @@ struct RSlot {
 };
 }  // namespace
 
+// Host-time accounting of the reader (S3HC_HOST_TRACE=1, diagnostics: printed at close)
+struct ReaderTrace {
+    enum { FEED, WALK, STAGE, SUBMIT, ISSUE, WAIT, DELIVER, N };
+    bool on = false;
+    double t[N] = {};
+    uint64_t batches = 0;
+};
+struct RTimer {
+    ReaderTrace& tr;
+    int k;
+    double t0;
+    RTimer(ReaderTrace& r, int kk) : tr(r), k(kk), t0(r.on ? host_us() : 0.0) {}
+    ~RTimer() { if (tr.on) tr.t[k] += host_us() - t0; }
+};
+
 struct s3hc_reader {
     s3hc_ctx* ctx;
+    ReaderTrace tr;
     size_t batch_bytes;
     size_t batch_max;           // batch limit while earlier batches are in flight (>= batch_bytes)
     std::vector<RSlot> slots;
@@ -2063,7 +2079,12 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     const uint64_t tok_entries = assign_tok_slots(mb, nbk);
     if (nu) memcpy(m + o_u, units.data(), sizeof(DecUnit) * nu);
     hipStream_t st = S.st;
-    par_memcpy(S.h_in.p, r->in.data() + r->in_head + F0.pos, nin);
+    {
+        RTimer T_(r->tr, ReaderTrace::STAGE);
+        par_memcpy(S.h_in.p, r->in.data() + r->in_head + F0.pos, nin);
+    }
+    RTimer T_(r->tr, ReaderTrace::SUBMIT);
+    ++r->tr.batches;
     HIPCHK(S.d_in.ensure(o_meta + nmeta + 64));
     // one device-to-host copy per batch: the frame results, then (256-byte aligned) the slots
     S.R = (8ull * n + 255) & ~255ull;
@@ -2118,15 +2139,19 @@ static int reader_pump(s3hc_reader* r) {
         const size_t want = r->inflight.empty() ? r->batch_bytes : r->batch_max;
         const size_t lim = std::min(avail, want + ((size_t)8 << 20));
         HWalk W;
-        // frames up to `want` bytes and one past it: the batch never takes more
-        walk_frames(r->in.data() + r->in_head, lim, W, true, false, want);
-        size_t nf = W.frames.size();
-        if (nf && W.last_incomplete) nf--;  // (stream mode leaves incomplete frames unwalked)
-        if (nf == 0 && lim < avail) {
-            W = HWalk();
-            walk_frames(r->in.data() + r->in_head, avail, W, true, false, want);
+        size_t nf;
+        {
+            RTimer T_(r->tr, ReaderTrace::WALK);
+            // frames up to `want` bytes and one past it: the batch never takes more
+            walk_frames(r->in.data() + r->in_head, lim, W, true, false, want);
             nf = W.frames.size();
-            if (nf && W.last_incomplete) nf--;
+            if (nf && W.last_incomplete) nf--;  // (stream mode leaves incomplete frames unwalked)
+            if (nf == 0 && lim < avail) {
+                W = HWalk();
+                walk_frames(r->in.data() + r->in_head, avail, W, true, false, want);
+                nf = W.frames.size();
+                if (nf && W.last_incomplete) nf--;
+            }
         }
         if (nf == 0) {
             if (W.tail_status != S3HC_OK && W.frames.empty() && !r->error) {  // bad header: nothing decodable
@@ -2158,7 +2183,8 @@ static int reader_pump(s3hc_reader* r) {
 
 // Decode of slot S finished: queue the D2H of its good frames' bytes (stream order) into its
 // pinned output buffer. A failing frame ends the stream after them (applied when S is the head).
-static int reader_issue_copy(RSlot& S) {
+static int reader_issue_copy(RSlot& S, ReaderTrace& tr) {
+    RTimer T_(tr, ReaderTrace::ISSUE);
     // (the results head h_out; olen is copied before h_out may be reallocated below)
     std::vector<uint32_t> olen((const uint32_t*)S.h_out.p, (const uint32_t*)S.h_out.p + S.n);
     const int32_t* st = (const int32_t*)(S.h_out.p + 4ull * S.n);
@@ -2206,7 +2232,7 @@ static int reader_advance(s3hc_reader* r) {
     for (int i : r->inflight) {
         RSlot& S = r->slots[i];
         if (S.state == 0 && hipEventQuery(S.ev) == hipSuccess) {
-            int rc = reader_issue_copy(S);
+            int rc = reader_issue_copy(S, r->tr);
             if (rc) return rc;
         }
     }
@@ -2217,11 +2243,17 @@ static int reader_advance(s3hc_reader* r) {
 static int reader_complete(s3hc_reader* r) {
     RSlot& S = r->slots[r->inflight.front()];
     if (S.state == 0) {
-        HIPCHK(hipEventSynchronize(S.ev));
-        int rc = reader_issue_copy(S);
+        {
+            RTimer T_(r->tr, ReaderTrace::WAIT);
+            HIPCHK(hipEventSynchronize(S.ev));
+        }
+        int rc = reader_issue_copy(S, r->tr);
         if (rc) return rc;
     }
-    if (!S.covered) HIPCHK(hipEventSynchronize(S.ev2));
+    if (!S.covered) {
+        RTimer T_(r->tr, ReaderTrace::WAIT);
+        HIPCHK(hipEventSynchronize(S.ev2));
+    }
     S.state = 2;
     S.ready = true;
     r->total += S.out_len;
@@ -2251,6 +2283,7 @@ extern "C" int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3
         r->batch_bytes = batch_bytes;
         r->batch_max = batch_bytes;
         r->slots.resize(depth);
+        r->tr.on = knob_on(KN_HOST_TRACE);
         for (auto& S : r->slots) {
             HIPCHK(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
             HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
@@ -2273,12 +2306,16 @@ extern "C" int s3hc_reader_feed(s3hc_reader* r, const uint8_t* src, size_t n) {
         if (r->finished) return fail(S3HC_INVALID_ARG, "reader already finished");
         if (r->error) return S3HC_OK;  // the stream has ended with an error; input is ignored
         if (r->in_head && r->in_head >= r->in.size() / 2) {  // drop consumed input (amortized)
+            RTimer T_(r->tr, ReaderTrace::FEED);
             r->in.erase(r->in.begin(), r->in.begin() + r->in_head);
             r->in_head = 0;
         }
-        const size_t old = r->in.size();
-        r->in.resize(old + n);
-        par_memcpy(r->in.data() + old, src, n);
+        {
+            RTimer T_(r->tr, ReaderTrace::FEED);
+            const size_t old = r->in.size();
+            r->in.resize(old + n);
+            par_memcpy(r->in.data() + old, src, n);
+        }
         std::lock_guard<std::mutex> g(r->ctx->mu);
         HIPCHK(hipSetDevice(r->ctx->device));
         int rc = reader_advance(r);
@@ -2303,6 +2340,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
         if (!r->inflight.empty() && r->slots[r->inflight.front()].ready) {
             RSlot& S = r->slots[r->inflight.front()];
             if (S.out_pos < S.out_len) {
+                RTimer T_(r->tr, ReaderTrace::DELIVER);
                 const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
                 if (k) par_memcpy(dst, S.h_out.p + S.R + S.out_pos, k);
                 S.out_pos += k;
@@ -2316,6 +2354,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
             if (!r->inflight.empty() && r->slots[r->inflight.front()].ready) {
                 RSlot& S = r->slots[r->inflight.front()];
                 if (*n == 0 && S.out_pos < S.out_len) {
+                    RTimer T_(r->tr, ReaderTrace::DELIVER);
                     const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
                     if (k) par_memcpy(dst, S.h_out.p + S.R + S.out_pos, k);
                     S.out_pos += k;
@@ -2361,6 +2400,13 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
 extern "C" uint64_t s3hc_reader_total(const s3hc_reader* r) { return r ? r->total : 0; }
 extern "C" void s3hc_reader_close(s3hc_reader* r) {
     if (!r) return;
+    if (r->tr.on) {
+        static const char* nm[] = {"feed", "walk", "stage", "submit", "issue", "wait", "deliver"};
+        fprintf(stderr, "[s3hc reader] batches %llu us/batch:", (unsigned long long)r->tr.batches);
+        for (int k = 0; k < ReaderTrace::N; ++k)
+            fprintf(stderr, " %s %.1f", nm[k], r->tr.t[k] / (double)std::max<uint64_t>(1, r->tr.batches));
+        fprintf(stderr, "\n");
+    }
     (void)hipSetDevice(r->ctx->device);
     for (auto& S : r->slots) {
         if (S.st) (void)hipStreamSynchronize(S.st);
