@@ -2319,15 +2319,17 @@ constexpr uint32_t kCloseLanes = 4;  // lanes per frame (16 per frame with DPP-s
 // decode (nullptr: none). blk_hash (nullable): hashes the large-block path computed while
 // decoding (1 << 32 | xxh32 per block); a frame of one such block skips its own pass.
 // got_hash (nullable): each frame's content xxh32.
-__global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__ src, const uint64_t* __restrict__ frame_off,
-                                                     const uint64_t* __restrict__ blk_base, const uint32_t* __restrict__ nblk,
-                                                     const DecBlock* __restrict__ blocks, const uint32_t* __restrict__ blk_out,
-                                                     const int32_t* __restrict__ blk_status,
-                                                     const uint64_t* __restrict__ blk_hash, const uint8_t* __restrict__ out,
-                                                     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ fwant,
-                                                     uint32_t n, const int32_t* fstat_in, int32_t* fstatus,
-                                                     uint32_t* __restrict__ out_len, uint32_t* __restrict__ got_hash) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x, f = gid / kCloseLanes, j = gid % kCloseLanes;
+// (lane gid of the close: frame gid / 4; callable by any workgroup shape whose lanes come in
+// aligned groups of four)
+__device__ __forceinline__ void dframe_close_lane(uint32_t gid, const uint8_t* __restrict__ src, const uint64_t* __restrict__ frame_off,
+                                                  const uint64_t* __restrict__ blk_base, const uint32_t* __restrict__ nblk,
+                                                  const DecBlock* __restrict__ blocks, const uint32_t* __restrict__ blk_out,
+                                                  const int32_t* __restrict__ blk_status,
+                                                  const uint64_t* __restrict__ blk_hash, const uint8_t* __restrict__ out,
+                                                  const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ fwant,
+                                                  uint32_t n, const int32_t* fstat_in, int32_t* fstatus,
+                                                  uint32_t* __restrict__ out_len, uint32_t* __restrict__ got_hash) {
+    const uint32_t f = gid / kCloseLanes, j = gid % kCloseLanes;
     const bool act = f < n;
     int st = S3HC_OK;
     uint64_t tot = 0;
@@ -2360,6 +2362,17 @@ __global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__
         else if ((flg & 0x04) && h != fwant[f]) st = S3HC_CHECKSUM;
     }
     fstatus[f] = st;
+}
+__global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__ src, const uint64_t* __restrict__ frame_off,
+                                                     const uint64_t* __restrict__ blk_base, const uint32_t* __restrict__ nblk,
+                                                     const DecBlock* __restrict__ blocks, const uint32_t* __restrict__ blk_out,
+                                                     const int32_t* __restrict__ blk_status,
+                                                     const uint64_t* __restrict__ blk_hash, const uint8_t* __restrict__ out,
+                                                     const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ fwant,
+                                                     uint32_t n, const int32_t* fstat_in, int32_t* fstatus,
+                                                     uint32_t* __restrict__ out_len, uint32_t* __restrict__ got_hash) {
+    dframe_close_lane(blockIdx.x * blockDim.x + threadIdx.x, src, frame_off, blk_base, nblk, blocks, blk_out, blk_status,
+                      blk_hash, out, out_off, fwant, n, fstat_in, fstatus, out_len, got_hash);
 }
 
 }  // namespace s3hc
@@ -2488,3 +2501,7 @@ extern "C" int s3hc_diag_prof(unsigned long long* out, int n, int reset) {
     return 0;
 }
 #endif
+
+// The 64 KiB-block fast path and the small-batch decoder (same translation unit: k_djump runs
+// decode_unit_pe for the blocks its token index does not take).
+#include "s3hc_fast.hip"

@@ -41,7 +41,7 @@ hipError_t launch_fast_exec(const uint8_t*, uint8_t*, const DecBlock*, const Dec
                             uint32_t, uint32_t*, int32_t*, const FastArgs&, hipStream_t);
 bool fast_exec_hashes();
 hipError_t launch_fast_small(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint8_t*,
-                             const FastArgs&, uint32_t*, int32_t*, hipStream_t);
+                             const FastArgs&, uint32_t*, int32_t*, hipStream_t, const CloseArgs*, bool*);
 hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*,
                            uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, uint32_t*, int32_t*, hipStream_t);
@@ -402,6 +402,7 @@ struct LbScratch {
     // 64 KiB-block fast path (s3hc_fast.hip): per-unit token bitmaps and results
     DevBuf f_bmp, f_fu, f_unit_fast;  // (f_bmp: sequence records)
     DevBuf f_hash;                     // launches without the large-block path: per-block hashes (FastArgs::bh)
+    DevBuf f_done;                     // k_djump's finished-workgroup count (CloseArgs::done; zero between launches)
     FastArgs fa{};
     bool fast_ready = false;
     // small launch (host-walked, <= kLbFewBlocks blocks): 64 KiB blocks run the fused k_dsmall
@@ -422,6 +423,10 @@ struct LbScratch {
         if ((e = f_fu.ensure((size_t)nunits * sizeof(FastUnit) + 64)) != hipSuccess) return e;
         if ((e = f_unit_fast.ensure((size_t)nunits + 64)) != hipSuccess) return e;
         if ((e = f_hash.ensure((size_t)std::max(nunits, nblocks) * 8 + 64)) != hipSuccess) return e;
+        if (!f_done.p) {
+            if ((e = f_done.ensure(64)) != hipSuccess) return e;
+            if ((e = hipMemset(f_done.p, 0, 64)) != hipSuccess) return e;
+        }
         fa.rec = f_bmp.as<uint2>();
         fa.fu = f_fu.as<FastUnit>();
         fa.unit_fast = f_unit_fast.as<uint8_t>();
@@ -539,10 +544,14 @@ static bool fast_path_enabled() { return !knob_on(KN_FAST_DISABLE); }
 // units: 1 << 32 | xxh32, or 0), nullptr when the path did not run.
 // Plans walked on the device pass ucount (the frame walk's block total: the units' count) and
 // size the per-unit grids to their frames; host-walked plans know their units exactly.
+// close (nullable): the batch's frame close; a small launch without large blocks then runs as one
+// kernel (k_djump: token index, block decode, the per-unit decoder for what it leaves, the frame
+// close) and *closed is set — the caller launches no frame close of its own.
 static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, const DecBlock* blk,
                                 const DecUnit* units, uint32_t nunits, uint32_t* blk_out, int32_t* blk_status,
                                 hipStream_t st, const uint64_t** blk_hash = nullptr, const uint64_t* ucount = nullptr,
-                                uint32_t grid = 0) {
+                                uint32_t grid = 0, const CloseArgs* close = nullptr, bool* closed = nullptr) {
+    if (closed) *closed = false;
     if (!grid || grid > nunits) grid = nunits;
     // S3HC_LB_DISABLE (tests, comparisons): every block goes to the one-wave decoder
     const bool lb = L && L->active && nunits && !knob_on(KN_LB_DISABLE);
@@ -562,10 +571,23 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
         L->fa.bh = nullptr;
     }
     if (fast && L->small) {
-        // small host-walked launch: token index + executor + content xxh32 in one launch
+        // small host-walked launch: token index + block decode + content xxh32 in one launch (and,
+        // without large blocks, the per-unit decoder and the frame close too)
+        CloseArgs c{};
+        const CloseArgs* cp = nullptr;
+        if (close && !lb) {
+            c = *close;
+            c.done = L->f_done.as<uint32_t>();
+            cp = &c;
+        }
+        bool fused = false;
         if ((e = launch_fast_small(src, dst, blk, units, nunits, lb ? L->a.unit_lb : nullptr, L->fa, blk_out,
-                                   blk_status, st)) != hipSuccess)
+                                   blk_status, st, cp, &fused)) != hipSuccess)
             return e;
+        if (fused) {
+            if (closed) *closed = true;
+            return hipSuccess;
+        }
     } else if (fast) {
         if ((e = launch_fast_tok(src, blk, units, nunits, ucount, grid, lb ? L->a.unit_lb : nullptr, L->fa, st)) !=
             hipSuccess)
@@ -2105,15 +2127,26 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     KTimer T(r->ctx, st);
     T.begin("decode");
     const uint64_t* bh = nullptr;
-    HIPCHK(decode_launch(&S.lb, src, d_slots, d_blk, (const DecUnit*)(dm + o_u), nu,
-                         S.d_blk_out.as<uint32_t>(), S.d_blk_status.as<int32_t>(), st, &bh));
+    CloseArgs ca{};
+    ca.frame_off = (const uint64_t*)(dm + o_fo);
+    ca.blk_base = (const uint64_t*)(dm + o_bb);
+    ca.nblk = (const uint32_t*)(dm + o_nb);
+    ca.out_off = (const uint64_t*)(dm + o_oo);
+    ca.fwant = (const uint32_t*)(dm + o_w);
+    ca.n = n;
+    ca.fstatus = d_st;
+    ca.out_len = d_olen;
+    bool closed = false;
+    HIPCHK(decode_launch(&S.lb, src, d_slots, d_blk, (const DecUnit*)(dm + o_u), nu, S.d_blk_out.as<uint32_t>(),
+                         S.d_blk_status.as<int32_t>(), st, &bh, nullptr, 0, &ca, &closed));
     T.end();
-    T.begin("dec_close");
-    HIPCHK(launch_dframe_close(src, (const uint64_t*)(dm + o_fo), (const uint64_t*)(dm + o_bb),
-                               (const uint32_t*)(dm + o_nb), d_blk, S.d_blk_out.as<uint32_t>(),
-                               S.d_blk_status.as<int32_t>(), bh, d_slots, (const uint64_t*)(dm + o_oo),
-                               (const uint32_t*)(dm + o_w), n, nullptr, d_st, d_olen, nullptr, st));
-    T.end();
+    if (!closed) {
+        T.begin("dec_close");
+        HIPCHK(launch_dframe_close(src, ca.frame_off, ca.blk_base, ca.nblk, d_blk, S.d_blk_out.as<uint32_t>(),
+                                   S.d_blk_status.as<int32_t>(), bh, d_slots, ca.out_off, ca.fwant, n, nullptr, d_st,
+                                   d_olen, nullptr, st));
+        T.end();
+    }
     // speculative copy of the decoded slots behind the decode, in the same round trip: frames of
     // 64 KiB blocks fill their slots, so the prefix is the batch's output; a frame whose slot is
     // its block capacity (BD 0x70: 4 MiB) only gets the prefix a 4:1 ratio can fill
