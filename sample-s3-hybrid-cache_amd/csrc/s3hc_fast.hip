@@ -56,6 +56,9 @@ constexpr uint32_t kMaxC = kFastMaxC;
 #else
 #define S3HC_HOPF hop
 #endif
+#ifndef S3HC_DTOK_SKIP  // diagnostic builds only (timing, output wrong): 1 no record stores, 2 no token parse in the record pass
+#define S3HC_DTOK_SKIP 0
+#endif
 #ifndef S3HC_DTOK_BAL  // 1: records by sequence rank, 0: by bitmap words
 #define S3HC_DTOK_BAL 1
 #endif
@@ -443,7 +446,15 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
     int32_t minsl = 0x7FFFFFFF;
     bool bad = false;
     auto emit = [&](uint32_t q, uint32_t k) {  // the token at q is sequence k
+#if S3HC_DTOK_SKIP & 2  // diagnostic builds (timing only, output wrong): no token parse in the record pass
+        Tok T;
+        T.ll = q & 7u;
+        T.ml = 4u + (q & 3u);
+        T.off = 1u + (q & 15u);
+        T.nxt = k + 1u == N ? END : q + 1u;
+#else
         const Tok T = S3HC_HOPF(stage, mis, q, C);
+#endif
         const uint32_t lit = T.ll == 0 ? 0u : q + 1u + (T.ll >= 15u ? (T.ll - 15u) / 255u + 1u : 0u);
         o += T.ll;
         uint32_t y = 0;
@@ -453,7 +464,11 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
             o += T.ml;
             y = T.off | ((T.ml - 4u) << 16);
         }
+#if S3HC_DTOK_SKIP & 1  // diagnostic builds: no record stores
+        if (y == 0xFFFFFFFFu) rec[k] = make_uint2(lit | (T.ll << 15), y);
+#else
         rec[k] = make_uint2(lit | (T.ll << 15), y);
+#endif
     };
 #if S3HC_DTOK_BAL == 1
     // balanced: thread g decodes sequences [g K, g K + K) (K = ceil(N / TT)), found from the
@@ -511,13 +526,13 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
     F.U = Utot;
     F.pad0 = F.pad1 = 0;
     *fo = F;
-    if (ok) {
+    if (ok && !S3HC_DTOK_SKIP) {
         if (g == 0) {
             a.fu[u] = F;
             a.unit_fast[u] = 1;
         }
     } else {
-        leave();
+        leave();  // (diagnostic skip builds: records are wrong, the per-unit decoder takes every block)
     }
 #ifdef FPROF
     if ((g & 63u) == 0) {

@@ -118,3 +118,42 @@ def test_reader_output_beyond_speculative_prefix(engine, oracle, item):
         out, r = _run(engine, frames, 4 * MiB, batch, depth)
         assert out == data, (batch, depth)
         assert r.total == len(data)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_reader_corrupt_block_payloads_one_launch_batches(engine, oracle, seed):
+    # batches of 64 KiB frames only: each is one launch (k_djump with the per-unit decoder for the
+    # blocks its token index leaves and the frame close in its last workgroup). Payload bytes of a
+    # few frames are flipped: the reader must deliver exactly the frames before the first failing
+    # one (the oracle decodes frame by frame) and then report that frame's status.
+    import random
+
+    import s3hc_lz4 as S
+
+    rng = random.Random(900 + seed)
+    data = synth.log_text(24 * 65536, 47 + seed)
+    fr = [bytearray(engine.compress_frame(data[i:i + 65536])) for i in range(0, len(data), 65536)]
+    for k in rng.sample(range(4, 24), 3):
+        f = fr[k]
+        for _ in range(rng.randint(1, 6)):
+            p = rng.randrange(11, len(f) - 8)  # inside the block payload (after header and block size)
+            f[p] ^= 1 << rng.randrange(8)
+    good, first_bad, want_st = bytearray(), None, 0
+    for k, f in enumerate(fr):
+        st, out = oracle.decompress_status(bytes(f))
+        if st != 0:
+            first_bad, want_st = k, st
+            break
+        good += out
+    r = S.RangeReader(engine, 256 << 10, 3)
+    r.feed(b"".join(bytes(f) for f in fr))
+    r.finish()
+    out = bytearray()
+    if first_bad is None:
+        _drain(r, out)
+        assert bytes(out) == data
+        return
+    with pytest.raises(S.CodecError) as e:
+        _drain(r, out)
+    assert e.value.status == want_st, (first_bad, want_st, e.value.status)
+    assert bytes(out) == bytes(good)
