@@ -56,7 +56,8 @@ const char* s3hc_version(void);
 
 /* Diagnostic / A-B switches (no reference counterpart: the reference has one codec). Read from
  * the environment (S3HC_FAST_DISABLE, S3HC_FAST, S3HC_LB_DISABLE, S3HC_LBW_DISABLE, S3HC_LBW_CAP,
- * S3HC_LBW_ROUNDS, S3HC_DEC_ONEWAVE, S3HC_FAST_TRACE, S3HC_LB_TRACE, S3HC_HOST_TRACE) once per
+ * S3HC_LBW_ROUNDS, S3HC_DEC_ONEWAVE, S3HC_FAST_TRACE, S3HC_LB_TRACE, S3HC_HOST_TRACE,
+ * S3HC_READER_SLOTS) once per
  * process at the first s3hc_create; this call changes one afterwards (value NULL = default; a
  * flag knob is on when its value is non-NULL, S3HC_FAST is on unless "0"). Process-wide. The
  * per-call decode path only reads the cached values. S3HC_INVALID_ARG for an unknown name. */
@@ -107,7 +108,8 @@ void s3hc_stream_close(s3hc_stream* s);
 
 /* ---- pipelined range reader (stream_range_data for throughput, config 4) --- */
 /* Complete frames are grouped into device batches of about batch_bytes compressed bytes that
- * run on `depth` HIP queues (pinned H2D of input + host-walked frame tables, decode, one
+ * run on `depth` HIP queues, S3HC_READER_SLOTS (default 1) batches in flight per queue (pinned
+ * H2D of input + host-walked frame tables, decode, one
  * frame-close launch = lengths + content xxh32 + EndMark checks, D2H), so batches overlap;
  * decoded bytes come back in stream order. Same semantics as s3hc_stream; the first failing
  * frame ends the stream after the bytes of every earlier frame.

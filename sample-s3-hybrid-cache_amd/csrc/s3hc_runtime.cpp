@@ -840,13 +840,13 @@ constexpr KnobName kKnobNames[] = {
     {"S3HC_LBW_DISABLE", KN_LBW_DISABLE, 0},   {"S3HC_LBW_CAP", KN_LBW_CAP, -1},
     {"S3HC_LBW_ROUNDS", KN_LBW_ROUNDS, -1},    {"S3HC_DEC_ONEWAVE", KN_DEC_ONEWAVE, 0},
     {"S3HC_FAST_TRACE", KN_FAST_TRACE, 0},     {"S3HC_LB_TRACE", KN_LB_TRACE, 0},
-    {"S3HC_HOST_TRACE", KN_HOST_TRACE, 0},
+    {"S3HC_HOST_TRACE", KN_HOST_TRACE, 0},     {"S3HC_READER_SLOTS", KN_READER_SLOTS, 1},
 };
 // a flag knob is on when its variable is set at all (the env convention of earlier rounds);
 // the numeric ones take the value
 long long knob_value(const KnobName& n, const char* v) {
     if (!v) return n.dflt;
-    if (n.k == KN_LBW_CAP || n.k == KN_LBW_ROUNDS) return strtoll(v, nullptr, 10);
+    if (n.k == KN_LBW_CAP || n.k == KN_LBW_ROUNDS || n.k == KN_READER_SLOTS) return strtoll(v, nullptr, 10);
     return 1;
 }
 int knob_set(const char* name, const char* v) {
@@ -1998,7 +1998,7 @@ extern "C" int s3hc_memcpy_async(s3hc_ctx* ctx, void* dst, const void* src, size
 // final size check (disk_cache.rs:3929-3934) against s3hc_reader_total.
 namespace {
 struct RSlot {
-    hipStream_t st = nullptr;
+    hipStream_t st = nullptr;  // one of the reader's queues (slot i: queue i % depth)
     hipEvent_t ev = nullptr;
     PinnedBuf h_in, h_out;  // h_in: input + tables; h_out: frame results + decoded slots
     DevBuf d_in, d_out, d_blk_out, d_blk_status;
@@ -2017,6 +2017,21 @@ struct RSlot {
     int32_t err = 0;        // status of the first failing frame (good < n)
 };
 }  // namespace
+
+// std::allocator that leaves bytes uninitialised on resize (the reader's input buffer is
+// overwritten by the feed copy right after growing)
+template <typename T>
+struct NoInitAlloc : std::allocator<T> {
+    template <typename U>
+    struct rebind { using other = NoInitAlloc<U>; };
+    NoInitAlloc() = default;
+    template <typename U>
+    NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <typename U>
+    void construct(U* p) noexcept { ::new ((void*)p) U; }
+    template <typename U, typename... A>
+    void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
 
 // Host-time accounting of the reader (S3HC_HOST_TRACE=1, diagnostics: printed at close)
 struct ReaderTrace {
@@ -2038,9 +2053,11 @@ struct s3hc_reader {
     ReaderTrace tr;
     size_t batch_bytes;
     size_t batch_max;           // batch limit while earlier batches are in flight (>= batch_bytes)
-    std::vector<RSlot> slots;
+    std::vector<hipStream_t> queues;  // `depth` HIP queues
+    std::vector<RSlot> slots;         // S3HC_READER_SLOTS batches per queue (default 1; more queue
+                                      // a queue's next batch behind its running one: measured slower)
     std::vector<int> inflight;  // slot indices in stream order (head may be ready / being read)
-    std::vector<uint8_t> in;    // buffered input; undecoded bytes start at in_head (a frame boundary)
+    std::vector<uint8_t, NoInitAlloc<uint8_t>> in;  // buffered input (grown without zero-fill); undecoded bytes start at in_head (a frame boundary)
     size_t in_head = 0;
     bool finished = false;
     int error = S3HC_OK;        // reported once every byte before it was read
@@ -2203,10 +2220,16 @@ static int reader_pump(s3hc_reader* r) {
         } else if (!r->inflight.empty()) {
             return S3HC_OK;  // wait for more input to fill the batch while others run
         }
+        // a free slot on the queue with the fewest batches in flight
         std::vector<bool> used(r->slots.size(), false);
-        for (int i : r->inflight) used[i] = true;
-        int s = 0;
-        while (used[s]) ++s;
+        std::vector<int> busy(r->queues.size(), 0);
+        for (int i : r->inflight) {
+            used[i] = true;
+            ++busy[(size_t)i % r->queues.size()];
+        }
+        int s = -1;
+        for (int i = 0; i < (int)r->slots.size(); ++i)
+            if (!used[i] && (s < 0 || busy[(size_t)i % r->queues.size()] < busy[(size_t)s % r->queues.size()])) s = i;
         int rc = reader_submit(r, r->slots[s], W, k);
         if (rc) return rc;
         r->inflight.push_back(s);
@@ -2315,10 +2338,14 @@ extern "C" int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3
         r->ctx = ctx;
         r->batch_bytes = batch_bytes;
         r->batch_max = batch_bytes;
-        r->slots.resize(depth);
+        const long long per = std::min<long long>(4, std::max<long long>(1, knob(KN_READER_SLOTS)));
+        r->queues.assign(depth, nullptr);
+        r->slots.resize((size_t)depth * (size_t)per);
         r->tr.on = knob_on(KN_HOST_TRACE);
-        for (auto& S : r->slots) {
-            HIPCHK(hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking));
+        for (auto& q : r->queues) HIPCHK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+        for (size_t i = 0; i < r->slots.size(); ++i) {
+            RSlot& S = r->slots[i];
+            S.st = r->queues[i % (size_t)depth];
             HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&S.ev2, hipEventDisableTiming));
         }
@@ -2441,11 +2468,13 @@ extern "C" void s3hc_reader_close(s3hc_reader* r) {
         fprintf(stderr, "\n");
     }
     (void)hipSetDevice(r->ctx->device);
+    for (auto q : r->queues)
+        if (q) (void)hipStreamSynchronize(q);
     for (auto& S : r->slots) {
-        if (S.st) (void)hipStreamSynchronize(S.st);
         if (S.ev) (void)hipEventDestroy(S.ev);
         if (S.ev2) (void)hipEventDestroy(S.ev2);
-        if (S.st) (void)hipStreamDestroy(S.st);
     }
+    for (auto q : r->queues)
+        if (q) (void)hipStreamDestroy(q);
     delete r;
 }

@@ -157,3 +157,29 @@ def test_reader_corrupt_block_payloads_one_launch_batches(engine, oracle, seed):
         _drain(r, out)
     assert e.value.status == want_st, (first_bad, want_st, e.value.status)
     assert bytes(out) == bytes(good)
+
+
+@pytest.mark.parametrize("slots", ["1", "3", "4"])
+def test_reader_batches_per_queue(engine, oracle, slots):
+    # S3HC_READER_SLOTS batches in flight per queue (default 1): small batches so that every slot
+    # holds one, a depth of 1..3 queues, and a corrupt frame late in the stream (the batches
+    # queued behind it are dropped, every earlier byte delivered)
+    import s3hc_lz4 as S
+
+    data = synth.log_text(3 * MiB + 4321, 43)
+    fr = [engine.compress_frame(data[i:i + 65536]) for i in range(0, len(data), 65536)]
+    with S.knobs({"S3HC_READER_SLOTS": slots}):
+        for depth in (1, 2, 3):
+            out, r = _run(engine, b"".join(fr), 200_000, 100_000, depth)
+            assert out == data, depth
+            assert r.total == len(data)
+        bad = bytearray(fr[40])
+        bad[-2] ^= 0x21  # content checksum of frame 40
+        r = S.RangeReader(engine, 70_000, 3)
+        r.feed(b"".join(fr[:40]) + bytes(bad) + b"".join(fr[41:]))
+        r.finish()
+        out = bytearray()
+        with pytest.raises(S.CodecError) as e:
+            _drain(r, out)
+        assert e.value.status == S.S3HC_CHECKSUM
+        assert bytes(out) == data[:40 * 65536]

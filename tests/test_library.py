@@ -101,7 +101,7 @@ def test_knobs_set_and_reject_unknown():
     import s3hc_lz4 as S
 
     for name, value in (("S3HC_FAST_DISABLE", "1"), ("S3HC_FAST", "0"), ("S3HC_LBW_CAP", "4096"),
-                        ("S3HC_LBW_ROUNDS", "2"), ("S3HC_HOST_TRACE", None)):
+                        ("S3HC_LBW_ROUNDS", "2"), ("S3HC_HOST_TRACE", None), ("S3HC_READER_SLOTS", "1")):
         S.set_knob(name, value)
         S.set_knob(name, None)
     with pytest.raises(S.CodecError):

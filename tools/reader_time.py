@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Config 4 reader, fixed 256 KiB batches: where the host's time goes (feed = submit side, read =
-wait + delivery), for 64 KiB frames and the reference's 1 MiB frames, depth 3 and 4.
-Usage: python tools/reader_time.py [--mib N]"""
+wait + delivery), for 64 KiB frames and the reference's 1 MiB frames, depth 3 and 4; --slots
+sweeps S3HC_READER_SLOTS (batches in flight per queue), --reps alternates the runs.
+Usage: python tools/reader_time.py [--mib N] [--depths 3] [--slots 1,2] [--reps 2]"""
 import argparse
 import json
 import os
@@ -51,6 +52,8 @@ def main():
     ap.add_argument("--mib", type=int, default=512)
     ap.add_argument("--only", default="")
     ap.add_argument("--depths", default="3,4")
+    ap.add_argument("--slots", default="")
+    ap.add_argument("--reps", type=int, default=1)
     a = ap.parse_args()
     eng = S.Engine(0)
     data = synth.log_text(a.mib << 20, 7)
@@ -62,10 +65,15 @@ def main():
         h_fr = eng.host_alloc(len(fr))
         h_fr.view()[:] = np.frombuffer(fr, dtype=np.uint8)
         h_out = eng.host_alloc(len(data))
-        for depth in [int(x) for x in a.depths.split(",")]:
-            r = run(eng, h_fr, len(fr), len(data), h_out, 256 << 10, depth)
-            assert bytes(h_out.view()[-item:]) == data[-item:]
-            res[f"{name}_depth{depth}"] = r
+        for rep in range(a.reps):
+            for depth in [int(x) for x in a.depths.split(",")]:
+                for sl in (a.slots.split(",") if a.slots else [None]):
+                    with S.knobs({"S3HC_READER_SLOTS": sl}):
+                        r = run(eng, h_fr, len(fr), len(data), h_out, 256 << 10, depth)
+                    assert bytes(h_out.view()[-item:]) == data[-item:]
+                    key = f"{name}_depth{depth}" + (f"_slots{sl}" if sl else "") + (f"_rep{rep}" if a.reps > 1 else "")
+                    res[key] = r
+                    print(key, r, flush=True)
         h_fr.free()
         h_out.free()
     print(json.dumps(res, indent=1))
