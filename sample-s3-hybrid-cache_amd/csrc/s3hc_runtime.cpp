@@ -425,7 +425,10 @@ struct LbScratch {
         if ((e = f_hash.ensure((size_t)std::max(nunits, nblocks) * 8 + 64)) != hipSuccess) return e;
         if (!f_done.p) {
             if ((e = f_done.ensure(64)) != hipSuccess) return e;
-            if ((e = hipMemset(f_done.p, 0, 64)) != hipSuccess) return e;
+            // zeroed before any launch reads it: the launches run on non-blocking queues, which do
+            // not wait for the null stream, so the clear is finished on the host side here
+            if ((e = hipMemsetAsync(f_done.p, 0, 64, nullptr)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(nullptr)) != hipSuccess) return e;
         }
         fa.rec = f_bmp.as<uint2>();
         fa.fu = f_fu.as<FastUnit>();
