@@ -1419,6 +1419,40 @@ static_assert(fast_lds_bytes(kFastMaxC) <= kLds, "the staged block fits P's LDS"
 
 // xxh32 (seed 0) of [p, p + L) in global memory by lanes 0..3 of the calling wave (lane a runs
 // accumulator a; 32 stripes of loads in flight ahead of the chain). Valid in lane 0.
+#ifndef S3HC_HASH_PRE  // k_djump's block checksum: stripe products (input * PRIME2) by the whole workgroup
+#define S3HC_HASH_PRE 1
+#endif
+// xxh32 of p[0, L) on lanes 0-3 (lane a: accumulator a), with pr[4 s + a] = the stripe words times
+// PRIME2 already computed (by the whole workgroup, into LDS): each lane's serial round is then an
+// add, a rotate and one multiply
+__device__ __forceinline__ uint32_t xxh32_lane4_pre(const uint8_t* __restrict__ p, uint32_t L, const uint32_t* pr) {
+    const uint32_t a = threadIdx.x & 3u;
+    const uint32_t ns = L >> 4;
+    uint32_t acc = a == 0 ? XH1 + XH2 : (a == 1 ? XH2 : (a == 2 ? 0u : 0u - XH1));
+    constexpr uint32_t kB = 32;
+    uint32_t s = 0;
+    for (; s + kB <= ns; s += kB) {
+        uint32_t m[kB];
+#pragma unroll
+        for (uint32_t k = 0; k < kB; ++k) m[k] = pr[4u * (s + k) + a];
+#pragma unroll
+        for (uint32_t k = 0; k < kB; ++k) acc = xh_rotl(acc + m[k], 13) * XH1;
+    }
+    for (; s < ns; ++s) acc = xh_rotl(acc + pr[4u * s + a], 13) * XH1;
+    const uint32_t v1 = (uint32_t)__shfl((int)acc, 0, 4), v2 = (uint32_t)__shfl((int)acc, 1, 4);
+    const uint32_t v3 = (uint32_t)__shfl((int)acc, 2, 4), v4 = (uint32_t)__shfl((int)acc, 3, 4);
+    uint32_t h = L >= 16u ? xh_rotl(v1, 1) + xh_rotl(v2, 7) + xh_rotl(v3, 12) + xh_rotl(v4, 18) : XH5;
+    h += L;
+    uint32_t t = ns * 16u;
+    for (; t + 4u <= L; t += 4u) h = xh_rotl(h + gld4(p + t) * XH3, 17) * XH4;
+    for (; t < L; ++t) h = xh_rotl(h + (uint32_t)p[t] * XH5, 11) * XH1;
+    h ^= h >> 15;
+    h *= XH2;
+    h ^= h >> 13;
+    h *= XH3;
+    h ^= h >> 16;
+    return h;
+}
 __device__ __forceinline__ uint32_t xxh32_lane4(const uint8_t* __restrict__ p, uint32_t L) {
     const uint32_t a = threadIdx.x & 3u;
     const uint32_t ns = L >> 4;
@@ -1638,8 +1672,16 @@ __global__ __launch_bounds__(jmp::kT) void k_djump(const uint8_t* __restrict__ s
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         [[maybe_unused]] const uint64_t tj3 = FP_NOW();
+#if S3HC_HASH_PRE
+        // the stripes' words times PRIME2, by every thread, into LDS over P (no longer needed)
+        for (uint32_t i = t; i < (U >> 4) * 4u; i += kT) P32[i] = gld4(out + 4u * i) * XH2;
+        __syncthreads();
+        if (t < 4u) {
+            const uint32_t h = xxh32_lane4_pre(out, U, P32);
+#else
         if (t < 4u) {
             const uint32_t h = xxh32_lane4(out, U);
+#endif
             if (t == 0) {
                 if (a.bh) a.bh[Un.first] = (1ull << 32) | h;
                 blk_out[Un.first] = U;
