@@ -1483,15 +1483,16 @@ __device__ __forceinline__ uint32_t xxh32_lane4(const uint8_t* __restrict__ p, u
     return h;
 }
 
-// c.done != nullptr (a launch without the large-block path): the workgroups also run the per-unit
-// decoder for the blocks the token index leaves (exact statuses, waves 0-1, its LDS over P) and
-// the last workgroup to finish closes the batch's frames (k_dframe_close's lanes): the batch is
-// one launch.
+// Blocks the token index leaves (stored, malformed, linked, > kFastMaxC compressed) keep bh 0 and
+// unit_fast 0: the per-unit decoder (k_decode_pe, next launch on the queue) gives them their exact
+// statuses, and k_dframe_close closes the frames. (Round 4 ran both inside this kernel; the
+// per-unit decoder's barriers on two of the sixteen waves then paired with the other waves' own,
+// which is the fault of GPUTEST_r04 — every barrier here is reached by all 1024 threads.)
 __global__ __launch_bounds__(jmp::kT) void k_djump(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                    const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
                                                    uint32_t nunits, const uint8_t* __restrict__ unit_lb, FastArgs a,
                                                    uint32_t maxc, uint32_t* __restrict__ blk_out,
-                                                   int32_t* __restrict__ blk_status, CloseArgs c) {
+                                                   int32_t* __restrict__ blk_status) {
     using namespace jmp;
     extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];  // (dtok_unit's staged block, then P)
     uint16_t* P = (uint16_t*)dsm;
@@ -1504,10 +1505,6 @@ __global__ __launch_bounds__(jmp::kT) void k_djump(const uint8_t* __restrict__ s
         FastUnit F;
         // token index and records with all 16 waves (1024 speculative segments)
         if (!dtok_unit<kT>(u, src, blk, units, unit_lb, a, maxc, &F)) {  // (a unit it leaves: bh 0)
-            __syncthreads();
-            // (no large-block path in such a launch: every unit left here is the per-unit
-            // decoder's, so it is told nothing about the fast path's flags)
-            if (c.done && threadIdx.x < 128u) decode_unit_pe(u, dsm, src, dst, blk, units, blk_out, blk_status, nullptr, nullptr);
             __syncthreads();
             continue;
         }
@@ -1699,22 +1696,6 @@ __global__ __launch_bounds__(jmp::kT) void k_djump(const uint8_t* __restrict__ s
         }
         __syncthreads();
     }
-    if (c.done) {
-        // the last workgroup closes the frames: every workgroup's output, lengths, statuses and
-        // hashes released device-wide before it counts itself
-        __shared__ uint32_t last;
-        __threadfence();
-        __syncthreads();
-        if (t == 0) last = atomicAdd(c.done, 1u) == gridDim.x - 1u ? 1u : 0u;
-        __syncthreads();
-        if (last) {
-            __threadfence();
-            for (uint32_t g0 = 0; g0 < kCloseLanes * c.n; g0 += kT)
-                dframe_close_lane(g0 + t, src, c.frame_off, c.blk_base, c.nblk, blk, blk_out, blk_status, a.bh, dst,
-                                  c.out_off, c.fwant, c.n, c.fstat_in, c.fstatus, c.out_len, c.got_hash);
-            if (t == 0) *c.done = 0u;  // (ready for the next launch)
-        }
-    }
 }
 
 // ------------------------------------------------------------------ k_dexec
@@ -1763,25 +1744,17 @@ extern "C" int s3hc_diag_fprof(unsigned long long* out, int n, int reset) {
     return 0;
 }
 #endif
-// close (nullable, k_djump only): the launch also runs the per-unit decoder and closes the frames;
-// *fused says whether it did
 hipError_t launch_fast_small(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
                              uint32_t nunits, const uint8_t* unit_lb, const FastArgs& a, uint32_t* blk_out,
-                             int32_t* blk_status, hipStream_t st, const CloseArgs* close, bool* fused) {
-    *fused = false;
+                             int32_t* blk_status, hipStream_t st) {
     if (!nunits || !a.maxc) return hipSuccess;
     const uint32_t maxc = a.maxc < kFastMaxC ? a.maxc : kFastMaxC;
 #if S3HC_SMALL_JUMP
     static const hipError_t attr = hipFuncSetAttribute((const void*)k_djump, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (int)jmp::kLds);  // (> 64 KiB of dynamic LDS)
     if (attr != hipSuccess) return attr;
-    CloseArgs c{};
-    if (close && close->done) {
-        c = *close;
-        *fused = true;
-    }
     hipLaunchKernelGGL(k_djump, dim3(nunits), dim3(jmp::kT), jmp::kLds, st, src, dst, blk, units, nunits, unit_lb, a,
-                       maxc, blk_out, blk_status, c);
+                       maxc, blk_out, blk_status);
 #else
     hipLaunchKernelGGL(k_dsmall, dim3(nunits), dim3(fst::kTT), fast_lds_bytes(maxc), st, src, dst, blk, units, nunits,
                        unit_lb, a, maxc, blk_out, blk_status);

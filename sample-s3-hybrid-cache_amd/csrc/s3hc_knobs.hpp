@@ -20,6 +20,7 @@ enum Knob : int {
     KN_LB_TRACE,          // S3HC_LB_TRACE=1: stderr line per large-block launch (serialises the stream)
     KN_HOST_TRACE,        // S3HC_HOST_TRACE=1: host-call stage times on stderr
     KN_READER_SLOTS,      // S3HC_READER_SLOTS=<n>: range-reader batches in flight per HIP queue (1..4)
+    KN_POISON,            // S3HC_POISON=1: device scratch filled with 0xFF on (re)allocation
     KN_COUNT
 };
 

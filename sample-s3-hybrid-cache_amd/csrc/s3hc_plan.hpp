@@ -211,23 +211,6 @@ struct FastUnit {        // 16 bytes, written by k_dtok for every unit it takes
 constexpr uint32_t fast_stage_bytes(uint32_t maxc) { return (maxc + 64u + 15u) & ~15u; }
 constexpr uint32_t fast_lds_bytes(uint32_t maxc) { return fast_stage_bytes(maxc) + 4u * ((maxc + 31u) / 32u + 1u); }
 
-// Frame close of a batch (k_dframe_close's arguments), for a decode launch that closes its frames
-// itself (k_djump: its last workgroup). done: a u32 the launch counts its finished workgroups in
-// (zero before, reset by the last one).
-struct CloseArgs {
-    const uint64_t* frame_off;
-    const uint64_t* blk_base;
-    const uint32_t* nblk;
-    const uint64_t* out_off;
-    const uint32_t* fwant;
-    uint32_t n;
-    const int32_t* fstat_in;
-    int32_t* fstatus;
-    uint32_t* out_len;
-    uint32_t* got_hash;
-    uint32_t* done;
-};
-
 struct FastArgs {
     uint2* rec;          // per block, at DecBlock::tok: the block's sequence records in stream order,
                          // {lit | ll << 15, off | (ml - 4) << 16} (off = 0: the last, match-less one)

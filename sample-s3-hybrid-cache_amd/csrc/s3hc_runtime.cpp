@@ -41,7 +41,7 @@ hipError_t launch_fast_exec(const uint8_t*, uint8_t*, const DecBlock*, const Dec
                             uint32_t, uint32_t*, int32_t*, const FastArgs&, hipStream_t);
 bool fast_exec_hashes();
 hipError_t launch_fast_small(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint8_t*,
-                             const FastArgs&, uint32_t*, int32_t*, hipStream_t, const CloseArgs*, bool*);
+                             const FastArgs&, uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*,
                            uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, uint32_t*, int32_t*, hipStream_t);
@@ -139,6 +139,9 @@ struct DevBuf {
         if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
+        if (e == hipSuccess && knob_on(KN_POISON)) {  // diagnostics: unwritten bytes read as 0xFF everywhere
+            if ((e = hipMemset(p, 0xFF, want)) == hipSuccess) e = hipDeviceSynchronize();
+        }
         return e;
     }
     template <class T> T* as() const { return (T*)p; }
@@ -402,7 +405,6 @@ struct LbScratch {
     // 64 KiB-block fast path (s3hc_fast.hip): per-unit token bitmaps and results
     DevBuf f_bmp, f_fu, f_unit_fast;  // (f_bmp: sequence records)
     DevBuf f_hash;                     // launches without the large-block path: per-block hashes (FastArgs::bh)
-    DevBuf f_done;                     // k_djump's finished-workgroup count (CloseArgs::done; zero between launches)
     FastArgs fa{};
     bool fast_ready = false;
     // small launch (host-walked, <= kLbFewBlocks blocks): 64 KiB blocks run the fused k_dsmall
@@ -423,13 +425,6 @@ struct LbScratch {
         if ((e = f_fu.ensure((size_t)nunits * sizeof(FastUnit) + 64)) != hipSuccess) return e;
         if ((e = f_unit_fast.ensure((size_t)nunits + 64)) != hipSuccess) return e;
         if ((e = f_hash.ensure((size_t)std::max(nunits, nblocks) * 8 + 64)) != hipSuccess) return e;
-        if (!f_done.p) {
-            if ((e = f_done.ensure(64)) != hipSuccess) return e;
-            // zeroed before any launch reads it: the launches run on non-blocking queues, which do
-            // not wait for the null stream, so the clear is finished on the host side here
-            if ((e = hipMemsetAsync(f_done.p, 0, 64, nullptr)) != hipSuccess) return e;
-            if ((e = hipStreamSynchronize(nullptr)) != hipSuccess) return e;
-        }
         fa.rec = f_bmp.as<uint2>();
         fa.fu = f_fu.as<FastUnit>();
         fa.unit_fast = f_unit_fast.as<uint8_t>();
@@ -547,14 +542,11 @@ static bool fast_path_enabled() { return !knob_on(KN_FAST_DISABLE); }
 // units: 1 << 32 | xxh32, or 0), nullptr when the path did not run.
 // Plans walked on the device pass ucount (the frame walk's block total: the units' count) and
 // size the per-unit grids to their frames; host-walked plans know their units exactly.
-// close (nullable): the batch's frame close; a small launch without large blocks then runs as one
-// kernel (k_djump: token index, block decode, the per-unit decoder for what it leaves, the frame
-// close) and *closed is set — the caller launches no frame close of its own.
+// The caller closes the frames (k_dframe_close) after it.
 static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, const DecBlock* blk,
                                 const DecUnit* units, uint32_t nunits, uint32_t* blk_out, int32_t* blk_status,
                                 hipStream_t st, const uint64_t** blk_hash = nullptr, const uint64_t* ucount = nullptr,
-                                uint32_t grid = 0, const CloseArgs* close = nullptr, bool* closed = nullptr) {
-    if (closed) *closed = false;
+                                uint32_t grid = 0) {
     if (!grid || grid > nunits) grid = nunits;
     // S3HC_LB_DISABLE (tests, comparisons): every block goes to the one-wave decoder
     const bool lb = L && L->active && nunits && !knob_on(KN_LB_DISABLE);
@@ -574,23 +566,11 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
         L->fa.bh = nullptr;
     }
     if (fast && L->small) {
-        // small host-walked launch: token index + block decode + content xxh32 in one launch (and,
-        // without large blocks, the per-unit decoder and the frame close too)
-        CloseArgs c{};
-        const CloseArgs* cp = nullptr;
-        if (close && !lb) {
-            c = *close;
-            c.done = L->f_done.as<uint32_t>();
-            cp = &c;
-        }
-        bool fused = false;
+        // small host-walked launch: token index + block decode + content xxh32 in one launch; the
+        // per-unit decoder below takes the blocks it leaves
         if ((e = launch_fast_small(src, dst, blk, units, nunits, lb ? L->a.unit_lb : nullptr, L->fa, blk_out,
-                                   blk_status, st, cp, &fused)) != hipSuccess)
+                                   blk_status, st)) != hipSuccess)
             return e;
-        if (fused) {
-            if (closed) *closed = true;
-            return hipSuccess;
-        }
     } else if (fast) {
         if ((e = launch_fast_tok(src, blk, units, nunits, ucount, grid, lb ? L->a.unit_lb : nullptr, L->fa, st)) !=
             hipSuccess)
@@ -844,7 +824,15 @@ constexpr KnobName kKnobNames[] = {
     {"S3HC_LBW_ROUNDS", KN_LBW_ROUNDS, -1},    {"S3HC_DEC_ONEWAVE", KN_DEC_ONEWAVE, 0},
     {"S3HC_FAST_TRACE", KN_FAST_TRACE, 0},     {"S3HC_LB_TRACE", KN_LB_TRACE, 0},
     {"S3HC_HOST_TRACE", KN_HOST_TRACE, 0},     {"S3HC_READER_SLOTS", KN_READER_SLOTS, 1},
+    {"S3HC_POISON", KN_POISON, 0},
 };
+// the slot a name reads and writes (S3HC_FAST: the other spelling of S3HC_FAST_DISABLE)
+int knob_slot(const char* name) {
+    if (!strcmp(name, "S3HC_FAST")) return KN_FAST_DISABLE;
+    for (const auto& n : kKnobNames)
+        if (!strcmp(n.name, name)) return n.k;
+    return -1;
+}
 // a flag knob is on when its variable is set at all (the env convention of earlier rounds);
 // the numeric ones take the value
 long long knob_value(const KnobName& n, const char* v) {
@@ -879,6 +867,22 @@ extern "C" int s3hc_set_knob(const char* name, const char* value) {
     if (!name) return fail(S3HC_INVALID_ARG, "name is NULL");
     knobs_load_env_once();  // (a knob set before the first context keeps its value)
     if (knob_set(name, value) != S3HC_OK) return fail(S3HC_INVALID_ARG, "unknown knob");
+    return S3HC_OK;
+}
+extern "C" int s3hc_get_knob(const char* name, long long* value) {
+    if (!name || !value) return fail(S3HC_INVALID_ARG, "bad arguments");
+    knobs_load_env_once();
+    const int k = knob_slot(name);
+    if (k < 0) return fail(S3HC_INVALID_ARG, "unknown knob");
+    *value = g_knob[k].load(std::memory_order_relaxed);
+    return S3HC_OK;
+}
+extern "C" int s3hc_set_knob_value(const char* name, long long value) {
+    if (!name) return fail(S3HC_INVALID_ARG, "name is NULL");
+    knobs_load_env_once();
+    const int k = knob_slot(name);
+    if (k < 0) return fail(S3HC_INVALID_ARG, "unknown knob");
+    g_knob[k].store(value, std::memory_order_relaxed);
     return S3HC_OK;
 }
 
@@ -1545,6 +1549,10 @@ static int decode_walk(s3hc_ctx* ctx, const uint8_t* src, size_t n, HWalk& W, bo
         int fs = S3HC_OK;
         for (uint32_t k = 0; k < F.nblk; ++k) {
             const uint32_t b = F.blk0 + k;
+            // device-written results drive the copies below: a status no decoder assigns or a block
+            // longer than its frame allows is not a decode's result
+            if (bs[b] < S3HC_OK || bs[b] > S3HC_INVALID_ARG || (bs[b] == S3HC_OK && bo[b] > W.blocks[b].limit))
+                return fail(S3HC_DEVICE, "decode results out of range");
             if (W.blk_has_cs[b] && cs_got[b] != W.blk_cs_want[b]) { fs = S3HC_CHECKSUM; break; }
             if (bs[b] != S3HC_OK) { fs = bs[b]; break; }
             if ((F.flg & 0x20) && k + 1 < F.nblk && bo[b] != W.blocks[b].cap) need_compact = true;
@@ -2017,9 +2025,41 @@ struct RSlot {
     uint64_t spec = 0;      // decoded-slot prefix copied to h_out right behind the decode (one round trip)
     bool covered = false;   // the good frames' bytes lie in that prefix: no second copy
     uint64_t R = 0;         // d_out / h_out: frame results (u32 lengths, i32 statuses) in [0, R), slots after
+    uint64_t slot = 0;      // decoded-slot bytes of the batch (frame f's slot: [dst_off[f], dst_off[f + 1]))
     int32_t err = 0;        // status of the first failing frame (good < n)
 };
 }  // namespace
+
+// The frame results a batch's decode wrote (lengths, statuses) decide the copies out of device
+// memory, so they are checked before any copy: every status must be one the decoders assign, every
+// good frame's length must fit its slot (slot f = [dst_off[f], dst_off[f + 1]), the last one up
+// to slot_total), the failing frame's status must be an error. Returns S3HC_OK with *good (frames
+// before the first failing one) and *bytes (their decoded bytes), or S3HC_DEVICE: the results are
+// not a decode's (the reference's contract turns every problem into an error chunk,
+// disk_cache.rs:3873-3934, never a copy of memory no decode wrote).
+static int check_batch_results(uint32_t n, const uint32_t* olen, const int32_t* st, const uint64_t* dst_off,
+                               uint64_t slot_total, uint32_t* good, uint64_t* bytes) {
+    uint32_t g = 0;
+    uint64_t b = 0;
+    for (; g < n; ++g) {
+        const int32_t s = st[g];
+        if (s < S3HC_OK || s > S3HC_INVALID_ARG) return fail(S3HC_DEVICE, "decode results: status out of range");
+        if (s != S3HC_OK) break;
+        const uint64_t lo = dst_off[g], hi = g + 1 < n ? dst_off[g + 1] : slot_total;
+        if (lo > hi || hi > slot_total || olen[g] > hi - lo)
+            return fail(S3HC_DEVICE, "decode results: frame length beyond its slot");
+        b += olen[g];
+    }
+    *good = g;
+    *bytes = b;
+    return S3HC_OK;
+}
+extern "C" int s3hc_diag_check_batch_results(uint32_t n, const uint32_t* olen, const int32_t* status,
+                                             const uint64_t* dst_off, uint64_t slot_total, uint32_t* good,
+                                             uint64_t* bytes) {
+    if ((n && (!olen || !status || !dst_off)) || !good || !bytes) return fail(S3HC_INVALID_ARG, "bad arguments");
+    return check_batch_results(n, olen, status, dst_off, slot_total, good, bytes);
+}
 
 // std::allocator that leaves bytes uninitialised on resize (the reader's input buffer is
 // overwritten by the feed copy right after growing)
@@ -2080,6 +2120,7 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     const uint32_t nbk = (all ? (uint32_t)W.blocks.size() : W.frames[nf].blk0) - F0.blk0;
     const uint64_t slot = (all ? W.slot_total : W.frames[nf].out_off) - F0.out_off;
     S.n = n;
+    S.slot = slot;
     S.dst_off.resize(n);
     std::vector<DecUnit> units;
     for (uint32_t f = 0; f < n; ++f) {
@@ -2147,26 +2188,15 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     KTimer T(r->ctx, st);
     T.begin("decode");
     const uint64_t* bh = nullptr;
-    CloseArgs ca{};
-    ca.frame_off = (const uint64_t*)(dm + o_fo);
-    ca.blk_base = (const uint64_t*)(dm + o_bb);
-    ca.nblk = (const uint32_t*)(dm + o_nb);
-    ca.out_off = (const uint64_t*)(dm + o_oo);
-    ca.fwant = (const uint32_t*)(dm + o_w);
-    ca.n = n;
-    ca.fstatus = d_st;
-    ca.out_len = d_olen;
-    bool closed = false;
     HIPCHK(decode_launch(&S.lb, src, d_slots, d_blk, (const DecUnit*)(dm + o_u), nu, S.d_blk_out.as<uint32_t>(),
-                         S.d_blk_status.as<int32_t>(), st, &bh, nullptr, 0, &ca, &closed));
+                         S.d_blk_status.as<int32_t>(), st, &bh, nullptr, 0));
     T.end();
-    if (!closed) {
-        T.begin("dec_close");
-        HIPCHK(launch_dframe_close(src, ca.frame_off, ca.blk_base, ca.nblk, d_blk, S.d_blk_out.as<uint32_t>(),
-                                   S.d_blk_status.as<int32_t>(), bh, d_slots, ca.out_off, ca.fwant, n, nullptr, d_st,
-                                   d_olen, nullptr, st));
-        T.end();
-    }
+    T.begin("dec_close");
+    HIPCHK(launch_dframe_close(src, (const uint64_t*)(dm + o_fo), (const uint64_t*)(dm + o_bb),
+                               (const uint32_t*)(dm + o_nb), d_blk, S.d_blk_out.as<uint32_t>(),
+                               S.d_blk_status.as<int32_t>(), bh, d_slots, (const uint64_t*)(dm + o_oo),
+                               (const uint32_t*)(dm + o_w), n, nullptr, d_st, d_olen, nullptr, st));
+    T.end();
     // speculative copy of the decoded slots behind the decode, in the same round trip: frames of
     // 64 KiB blocks fill their slots, so the prefix is the batch's output; a frame whose slot is
     // its block capacity (BD 0x70: 4 MiB) only gets the prefix a 4:1 ratio can fill
@@ -2249,7 +2279,8 @@ static int reader_issue_copy(RSlot& S, ReaderTrace& tr) {
     const int32_t* st = (const int32_t*)(S.h_out.p + 4ull * S.n);
     uint32_t good = 0;
     uint64_t bytes = 0;
-    while (good < S.n && st[good] == S3HC_OK) bytes += olen[good++];
+    if (int rc = check_batch_results(S.n, olen.data(), st, S.dst_off.data(), S.slot, &good, &bytes)) return rc;
+    if (bytes > S.slot) return fail(S3HC_DEVICE, "decode results: batch output beyond its slots");
     S.err = good < S.n ? st[good] : 0;
     // frames decode into slots of their block capacity; when every frame but the last filled
     // its slot (the normal case) the good output is already contiguous: one copy, or none when

@@ -58,6 +58,9 @@ def _load():
         "s3hc_last_error": (ctypes.c_char_p, []),
         "s3hc_version": (ctypes.c_char_p, []),
         "s3hc_set_knob": (i32, [ctypes.c_char_p, ctypes.c_char_p]),
+        "s3hc_get_knob": (i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong)]),
+        "s3hc_set_knob_value": (i32, [ctypes.c_char_p, ctypes.c_longlong]),
+        "s3hc_diag_check_batch_results": (i32, [u32, vp, vp, vp, u64, ctypes.POINTER(u32), ctypes.POINTER(u64)]),
         "s3hc_frame_bound": (sz, [sz]),
         "s3hc_compat_encode_dev": (i32, [vp, vp, vp, vp, u32, vp, vp, vp, vp]),
         "s3hc_compress_frame": (i32, [vp, u8p, sz, i32, u8p, sz, szp, ip]),
@@ -192,22 +195,45 @@ def set_knob(name: str, value=None) -> None:
     _check(lib.s3hc_set_knob(name.encode(), None if value is None else str(value).encode()))
 
 
+def get_knob(name: str) -> int:
+    """The knob's raw value (S3HC_FAST reads S3HC_FAST_DISABLE's slot)."""
+    v = ctypes.c_longlong()
+    _check(lib.s3hc_get_knob(name.encode(), ctypes.byref(v)))
+    return v.value
+
+
 class knobs:
-    """Context manager: set knobs (name -> value) for the block, then restore their defaults.
-    Replaces the environment toggles of earlier rounds (the library reads the environment once)."""
+    """Context manager: set knobs (name -> value) for the block, then restore the values they had
+    on entry (raw slot values, so alias names such as S3HC_FAST / S3HC_FAST_DISABLE restore
+    exactly). Replaces the environment toggles of earlier rounds (the library reads the
+    environment once)."""
 
     def __init__(self, env: dict):
         self.env = dict(env)
+        self.saved = []
 
     def __enter__(self):
+        self.saved = [(k, get_knob(k)) for k in self.env]
         for k, v in self.env.items():
             set_knob(k, v)
         return self
 
     def __exit__(self, *exc):
-        for k in self.env:
-            set_knob(k, os.environ.get(k))
+        for k, v in reversed(self.saved):
+            _check(lib.s3hc_set_knob_value(k.encode(), v))
         return False
+
+
+def check_batch_results(olen, status, dst_off, slot_total):
+    """s3hc_diag_check_batch_results: (good, bytes) or CodecError(S3HC_DEVICE) (the reader's
+    check of device-written frame results before any copy)."""
+    n = len(olen)
+    a = (ctypes.c_uint32 * max(n, 1))(*olen)
+    b = (ctypes.c_int32 * max(n, 1))(*status)
+    c = (ctypes.c_uint64 * max(n, 1))(*dst_off)
+    g, by = ctypes.c_uint32(), ctypes.c_uint64()
+    _check(lib.s3hc_diag_check_batch_results(n, a, b, c, slot_total, ctypes.byref(g), ctypes.byref(by)))
+    return g.value, by.value
 
 
 def frame_bound(n: int) -> int:

@@ -122,9 +122,8 @@ def test_reader_output_beyond_speculative_prefix(engine, oracle, item):
 
 @pytest.mark.parametrize("seed", [0, 1, 2, 3])
 def test_reader_corrupt_block_payloads_one_launch_batches(engine, oracle, seed):
-    # batches of 64 KiB frames only: each is one launch (k_djump with the per-unit decoder for the
-    # blocks its token index leaves and the frame close in its last workgroup). Payload bytes of a
-    # few frames are flipped: the reader must deliver exactly the frames before the first failing
+    # batches of 64 KiB frames only: k_djump decodes them, the per-unit decoder takes the blocks its
+    # token index leaves, k_dframe_close closes the frames. Payload bytes of a few frames are flipped: the reader must deliver exactly the frames before the first failing
     # one (the oracle decodes frame by frame) and then report that frame's status.
     import random
 
@@ -183,3 +182,51 @@ def test_reader_batches_per_queue(engine, oracle, slots):
             _drain(r, out)
         assert e.value.status == S.S3HC_CHECKSUM
         assert bytes(out) == data[:40 * 65536]
+
+
+@pytest.mark.parametrize("poison", [None, "1"])
+@pytest.mark.parametrize("corrupt_at", [None, 150, 187])
+def test_reader_many_small_frames_stored_and_corrupt(engine, oracle, poison, corrupt_at):
+    # batches of far more than 32 small frames, with stored (incompressible)
+    # frames the token index leaves to the per-unit decoder, and a corrupt frame late in a batch.
+    # Every delivered byte and the status must be the oracle's, frame by frame. S3HC_POISON=1 fills
+    # every device scratch buffer with 0xFF when allocated: a read of anything no launch wrote
+    # would fail the same way on every box (the GPUTEST_r04 fault: results of the fused close).
+    import random
+
+    import s3hc_lz4 as S
+
+    rng = random.Random(77 if corrupt_at is None else corrupt_at)
+    items = []
+    for k in range(192):
+        n = rng.choice((4096, 6000, 1500, 13, 5, 65536 // 8))
+        if k % 17 == 5:
+            items.append(rng.randbytes(n))             # stored block
+        elif k % 11 == 3:
+            items.append(bytes([k & 0xFF]) * n)        # one long overlapping match
+        else:
+            items.append(synth.log_text(n, 300 + k))
+    fr = [bytearray(oracle.lz4flex_compress_frame(x)) for x in items]
+    if corrupt_at is not None:
+        fr[corrupt_at][-1] ^= 0x44  # content checksum
+    good, want_st = bytearray(), 0
+    for f in fr:
+        st, out = oracle.decompress_status(bytes(f))
+        if st != 0:
+            want_st = st
+            break
+        good += out
+    with S.knobs({"S3HC_POISON": poison}):
+        for batch, depth in ((256 << 10, 3), (64 << 10, 2)):
+            r = S.RangeReader(engine, batch, depth)
+            r.feed(b"".join(bytes(f) for f in fr))
+            r.finish()
+            out = bytearray()
+            if want_st == 0:
+                _drain(r, out)
+                assert bytes(out) == b"".join(items), (batch, depth)
+            else:
+                with pytest.raises(S.CodecError) as e:
+                    _drain(r, out)
+                assert e.value.status == want_st
+                assert bytes(out) == bytes(good), (batch, depth)

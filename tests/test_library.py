@@ -108,3 +108,46 @@ def test_knobs_set_and_reject_unknown():
         S.set_knob("S3HC_NO_SUCH_KNOB", "1")
     with S.knobs({"S3HC_LB_DISABLE": "1", "S3HC_FAST": "1"}):
         pass
+
+
+def test_knobs_restore_exact_values_with_aliases():
+    # S3HC_FAST and S3HC_FAST_DISABLE share one slot; the context manager restores the
+    # values on entry, whatever the order and the environment
+    import s3hc_lz4 as S
+
+    S.set_knob("S3HC_FAST", "0")  # fast path off (S3HC_FAST_DISABLE's slot = 1)
+    try:
+        assert S.get_knob("S3HC_FAST_DISABLE") == 1 and S.get_knob("S3HC_FAST") == 1
+        with S.knobs({"S3HC_FAST": "1", "S3HC_FAST_DISABLE": None, "S3HC_POISON": "1"}):
+            assert S.get_knob("S3HC_FAST_DISABLE") == 0
+            assert S.get_knob("S3HC_POISON") == 1
+        assert S.get_knob("S3HC_FAST_DISABLE") == 1
+        assert S.get_knob("S3HC_POISON") == 0
+    finally:
+        S.set_knob("S3HC_FAST_DISABLE", None)
+    assert S.get_knob("S3HC_FAST_DISABLE") == 0
+    with pytest.raises(S.CodecError):
+        S.get_knob("S3HC_NO_SUCH_KNOB")
+
+
+def test_reader_result_check_rejects_forged_results():
+    # device-written frame lengths and statuses are checked on the host before
+    # they drive a device-to-host copy (the reader's s3hc_reader_* path; pure host code)
+    import s3hc_lz4 as S
+
+    off = [0, 65536, 131072, 196608]
+    slot = 262144
+    assert S.check_batch_results([65536, 65536, 65536, 100], [0, 0, 0, 0], off, slot) == (4, 196708)
+    assert S.check_batch_results([65536, 7, 0, 0], [0, 2, 0, 0], off, slot) == (1, 65536)  # CHECKSUM at frame 1
+    assert S.check_batch_results([], [], [], 0) == (0, 0)
+    assert S.check_batch_results([65536, 65536, 65536, 65536], [0] * 4, off, slot) == (4, slot)
+    for olen, st in (([65537, 0, 0, 0], [0] * 4),              # longer than its slot
+                     ([0, 0, 0, 65537], [0] * 4),              # the last frame past the batch's slots
+                     ([0xFFFFFFFF, 0, 0, 0], [0] * 4),         # poison-filled length
+                     ([0, 0, 0, 0], [0, -1, 0, 0]),            # poison-filled status (0xFFFFFFFF)
+                     ([0, 0, 0, 0], [0, 0, 7, 0])):            # a status no decoder assigns
+        with pytest.raises(S.CodecError) as e:
+            S.check_batch_results(olen, st, off, slot)
+        assert e.value.status == S.S3HC_DEVICE
+    # lengths after the first failing frame are not the decode's business: never read
+    assert S.check_batch_results([10, 0xFFFFFFFF, 0xFFFFFFFF, 0], [0, 1, -1, 9], off, slot) == (1, 10)

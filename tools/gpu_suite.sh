@@ -1,6 +1,7 @@
-# Round-3 GPU suite: every -m gpu test (one process, per-test timeouts), then the default bench line
+# Whole GPU suite (one process, per-test timeouts), then the default bench line without the CPU leg.
+# usage: bash tools/gpu_suite.sh [extra pytest args]
 mkdir -p gpurun_out
-timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x --timeout 900 --timeout-method thread --durations=12 -p no:cacheprovider > gpurun_out/suite.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread --durations=12 -p no:cacheprovider "$@" > gpurun_out/suite.log 2>&1
 rc=$?
 tail -18 gpurun_out/suite.log
 if [ $rc -ne 0 ]; then exit $rc; fi
