@@ -133,6 +133,12 @@ void s3hc_stream_close(s3hc_stream* s);
  * pipeline stays at batch_bytes, so time to first byte is unchanged). */
 typedef struct s3hc_reader s3hc_reader;
 int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3hc_reader** out);
+/* The same reader over nctx devices of one process (no reference counterpart: the proxy runs
+ * every range read on the one host, http_proxy.rs:11608-11622): `depth` queues per context,
+ * queue q on ctxs[q % nctx]; each batch goes to the least busy queue, so consecutive batches
+ * alternate devices. Batches are independent (no collective); the output is the one-device
+ * reader's, in stream order. Duplicate context pointers are refused. */
+int s3hc_reader_open_multi(s3hc_ctx* const* ctxs, int nctx, size_t batch_bytes, int depth, s3hc_reader** out);
 int s3hc_reader_set_batch_max(s3hc_reader* r, size_t max_bytes);
 int s3hc_reader_feed(s3hc_reader* r, const uint8_t* src, size_t n);
 int s3hc_reader_finish(s3hc_reader* r);
@@ -279,6 +285,17 @@ typedef int (*s3hc_frame_sink)(void* user, const uint8_t* frame, size_t n);
  * record_object per committed range (:1865-1867, :2053). */
 int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t flush_bytes, uint32_t flush_batches,
                            s3hc_handler* stats, s3hc_aggregator** out);
+/* The same aggregator over nctx devices of one process (the proxy's concurrent writers,
+ * http_proxy.rs:11608-11622, spread over a node's GPUs): each flush splits the queued batches
+ * into contiguous shards of about equal bytes (s3hc_shard_items), encodes shard d on ctxs[d]
+ * (concurrently, no collective), and delivers every frame in queue order, byte-identical to the
+ * one-device aggregator. Duplicate context pointers are refused. */
+int s3hc_aggregator_create_multi(s3hc_ctx* const* ctxs, int nctx, size_t batch_size, size_t flush_bytes,
+                                 uint32_t flush_batches, s3hc_handler* stats, s3hc_aggregator** out);
+/* Contiguous shards of n items of byte sizes len[] over ndev devices: item i goes to the shard
+ * holding its byte midpoint (about equal bytes per shard, order kept), and every shard gets at
+ * least one item when n >= ndev. first[d] = first item of shard d, first[ndev] = n. Host only. */
+int s3hc_shard_items(const uint64_t* len, uint32_t n, int ndev, uint32_t* first);
 int s3hc_aggregator_flush(s3hc_aggregator* a);
 /* Layout of compressed batches: S3HC_BLK_AUTO_LZ4FLEX (default, one frame per batch as
  * flush_batch writes it) or S3HC_BLK_64K_PER_FRAME (64 KiB frames: a reference reader decodes

@@ -162,7 +162,7 @@ struct PinnedBuf {
         if (n <= cap) return hipSuccess;
         const size_t want = std::max<size_t>(regrow(n, cap), 1 << 16);
         if (p) { (void)hipHostFree(p); p = nullptr; cap = 0; }
-        hipError_t e = hipHostMalloc((void**)&p, want, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc((void**)&p, want, hipHostMallocPortable);
         if (e == hipSuccess) cap = want;
         return e;
     }
@@ -171,7 +171,7 @@ struct PinnedBuf {
         if (n <= cap) return hipSuccess;
         uint8_t* q = nullptr;
         const size_t want = std::max<size_t>(regrow(n, cap), 1 << 16);
-        hipError_t e = hipHostMalloc((void**)&q, want, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc((void**)&q, want, hipHostMallocPortable);
         if (e != hipSuccess) return e;
         if (p) {
             memcpy(q, p, std::min(keep, cap));
@@ -1924,7 +1924,7 @@ extern "C" int s3hc_host_alloc(s3hc_ctx* ctx, size_t n, void** out) {
     return guarded([&]() -> int {
         if (!ctx || !out) return fail(S3HC_INVALID_ARG, "bad arguments");
         HIPCHK(hipSetDevice(ctx->device));
-        HIPCHK(hipHostMalloc(out, n ? n : 16, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(out, n ? n : 16, hipHostMallocPortable));
         return S3HC_OK;
     });
 }
@@ -2009,7 +2009,8 @@ extern "C" int s3hc_memcpy_async(s3hc_ctx* ctx, void* dst, const void* src, size
 // final size check (disk_cache.rs:3929-3934) against s3hc_reader_total.
 namespace {
 struct RSlot {
-    hipStream_t st = nullptr;  // one of the reader's queues (slot i: queue i % depth)
+    s3hc_ctx* ctx = nullptr;   // the device of the slot's queue
+    hipStream_t st = nullptr;  // one of the reader's queues (slot i: queue i % queues)
     hipEvent_t ev = nullptr;
     PinnedBuf h_in, h_out;  // h_in: input + tables; h_out: frame results + decoded slots
     DevBuf d_in, d_out, d_blk_out, d_blk_status;
@@ -2092,11 +2093,12 @@ struct RTimer {
 };
 
 struct s3hc_reader {
-    s3hc_ctx* ctx;
+    s3hc_ctx* ctx;                  // ctxs[0]
+    std::vector<s3hc_ctx*> ctxs;    // the reader's devices (queue q on ctxs[q % ctxs.size()])
     ReaderTrace tr;
     size_t batch_bytes;
     size_t batch_max;           // batch limit while earlier batches are in flight (>= batch_bytes)
-    std::vector<hipStream_t> queues;  // `depth` HIP queues
+    std::vector<hipStream_t> queues;  // `depth` HIP queues per device
     std::vector<RSlot> slots;         // S3HC_READER_SLOTS batches per queue (default 1; more queue
                                       // a queue's next batch behind its running one: measured slower)
     std::vector<int> inflight;  // slot indices in stream order (head may be ready / being read)
@@ -2162,6 +2164,7 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     const uint64_t tok_entries = assign_tok_slots(mb, nbk);
     if (nu) memcpy(m + o_u, units.data(), sizeof(DecUnit) * nu);
     hipStream_t st = S.st;
+    HIPCHK(hipSetDevice(S.ctx->device));
     {
         RTimer T_(r->tr, ReaderTrace::STAGE);
         par_memcpy(S.h_in.p, r->in.data() + r->in_head + F0.pos, nin);
@@ -2185,7 +2188,7 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     uint32_t* d_olen = S.d_out.as<uint32_t>();
     int32_t* d_st = (int32_t*)(S.d_out.as<uint8_t>() + 4ull * n);
     uint8_t* d_slots = S.d_out.as<uint8_t>() + S.R;
-    KTimer T(r->ctx, st);
+    KTimer T(S.ctx, st);
     T.begin("decode");
     const uint64_t* bh = nullptr;
     HIPCHK(decode_launch(&S.lb, src, d_slots, d_blk, (const DecUnit*)(dm + o_u), nu, S.d_blk_out.as<uint32_t>(),
@@ -2274,6 +2277,7 @@ static int reader_pump(s3hc_reader* r) {
 // pinned output buffer. A failing frame ends the stream after them (applied when S is the head).
 static int reader_issue_copy(RSlot& S, ReaderTrace& tr) {
     RTimer T_(tr, ReaderTrace::ISSUE);
+    HIPCHK(hipSetDevice(S.ctx->device));
     // (the results head h_out; olen is copied before h_out may be reallocated below)
     std::vector<uint32_t> olen((const uint32_t*)S.h_out.p, (const uint32_t*)S.h_out.p + S.n);
     const int32_t* st = (const int32_t*)(S.h_out.p + 4ull * S.n);
@@ -2321,7 +2325,7 @@ static bool reader_copy_done(RSlot& S) { return S.state == 1 && (S.covered || hi
 static int reader_advance(s3hc_reader* r) {
     for (int i : r->inflight) {
         RSlot& S = r->slots[i];
-        if (S.state == 0 && hipEventQuery(S.ev) == hipSuccess) {
+        if (S.state == 0 && hipSetDevice(S.ctx->device) == hipSuccess && hipEventQuery(S.ev) == hipSuccess) {
             int rc = reader_issue_copy(S, r->tr);
             if (rc) return rc;
         }
@@ -2332,6 +2336,7 @@ static int reader_advance(s3hc_reader* r) {
 // Wait until the oldest batch's decoded bytes are in its pinned output buffer.
 static int reader_complete(s3hc_reader* r) {
     RSlot& S = r->slots[r->inflight.front()];
+    HIPCHK(hipSetDevice(S.ctx->device));
     if (S.state == 0) {
         {
             RTimer T_(r->tr, ReaderTrace::WAIT);
@@ -2342,6 +2347,7 @@ static int reader_complete(s3hc_reader* r) {
     }
     if (!S.covered) {
         RTimer T_(r->tr, ReaderTrace::WAIT);
+        HIPCHK(hipSetDevice(S.ctx->device));
         HIPCHK(hipEventSynchronize(S.ev2));
     }
     S.state = 2;
@@ -2352,6 +2358,7 @@ static int reader_complete(s3hc_reader* r) {
         r->error_msg = "frame decode failed";
         for (size_t k = 1; k < r->inflight.size(); ++k) {
             RSlot& L = r->slots[r->inflight[k]];
+            (void)hipSetDevice(L.ctx->device);
             (void)hipStreamSynchronize(L.st);
             L.state = 0;
             L.ready = false;
@@ -2363,29 +2370,53 @@ static int reader_complete(s3hc_reader* r) {
     return S3HC_OK;
 }
 
+// Every context of a reader locked in list order (the same order on every path: no deadlock);
+// the reader's per-slot scratch and the contexts' timing state are used under them.
+struct ReaderLock {
+    std::vector<std::unique_lock<std::mutex>> g;
+    explicit ReaderLock(s3hc_reader* r) {
+        g.reserve(r->ctxs.size());
+        for (auto* c : r->ctxs) g.emplace_back(c->mu);
+    }
+};
+static int reader_new(s3hc_ctx* const* ctxs, int nctx, size_t batch_bytes, int depth, s3hc_reader** out) {
+    if (!ctxs || nctx < 1 || !out || depth < 1 || depth > 16 || batch_bytes == 0) return fail(S3HC_INVALID_ARG, "bad arguments");
+    for (int i = 0; i < nctx; ++i) {
+        if (!ctxs[i]) return fail(S3HC_INVALID_ARG, "NULL context");
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i]) return fail(S3HC_INVALID_ARG, "a context is listed twice");
+    }
+    std::unique_ptr<s3hc_reader> r(new s3hc_reader);
+    r->ctx = ctxs[0];
+    r->ctxs.assign(ctxs, ctxs + nctx);
+    ReaderLock lk(r.get());
+    r->batch_bytes = batch_bytes;
+    r->batch_max = batch_bytes;
+    const long long per = std::min<long long>(4, std::max<long long>(1, knob(KN_READER_SLOTS)));
+    const size_t nq = (size_t)depth * (size_t)nctx;
+    r->queues.assign(nq, nullptr);
+    r->slots.resize(nq * (size_t)per);
+    r->tr.on = knob_on(KN_HOST_TRACE);
+    for (size_t q = 0; q < nq; ++q) {
+        HIPCHK(hipSetDevice(ctxs[q % (size_t)nctx]->device));
+        HIPCHK(hipStreamCreateWithFlags(&r->queues[q], hipStreamNonBlocking));
+    }
+    for (size_t i = 0; i < r->slots.size(); ++i) {
+        RSlot& S = r->slots[i];
+        S.ctx = ctxs[(i % nq) % (size_t)nctx];
+        S.st = r->queues[i % nq];
+        HIPCHK(hipSetDevice(S.ctx->device));
+        HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&S.ev2, hipEventDisableTiming));
+    }
+    *out = r.release();
+    return S3HC_OK;
+}
 extern "C" int s3hc_reader_open(s3hc_ctx* ctx, size_t batch_bytes, int depth, s3hc_reader** out) {
-    return guarded([&]() -> int {
-        if (!ctx || !out || depth < 1 || depth > 16 || batch_bytes == 0) return fail(S3HC_INVALID_ARG, "bad arguments");
-        std::lock_guard<std::mutex> g(ctx->mu);
-        HIPCHK(hipSetDevice(ctx->device));
-        std::unique_ptr<s3hc_reader> r(new s3hc_reader);
-        r->ctx = ctx;
-        r->batch_bytes = batch_bytes;
-        r->batch_max = batch_bytes;
-        const long long per = std::min<long long>(4, std::max<long long>(1, knob(KN_READER_SLOTS)));
-        r->queues.assign(depth, nullptr);
-        r->slots.resize((size_t)depth * (size_t)per);
-        r->tr.on = knob_on(KN_HOST_TRACE);
-        for (auto& q : r->queues) HIPCHK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
-        for (size_t i = 0; i < r->slots.size(); ++i) {
-            RSlot& S = r->slots[i];
-            S.st = r->queues[i % (size_t)depth];
-            HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&S.ev2, hipEventDisableTiming));
-        }
-        *out = r.release();
-        return S3HC_OK;
-    });
+    return guarded([&]() -> int { return reader_new(&ctx, 1, batch_bytes, depth, out); });
+}
+extern "C" int s3hc_reader_open_multi(s3hc_ctx* const* ctxs, int nctx, size_t batch_bytes, int depth, s3hc_reader** out) {
+    return guarded([&]() -> int { return reader_new(ctxs, nctx, batch_bytes, depth, out); });
 }
 extern "C" int s3hc_reader_set_batch_max(s3hc_reader* r, size_t max_bytes) {
     return guarded([&]() -> int {
@@ -2410,8 +2441,7 @@ extern "C" int s3hc_reader_feed(s3hc_reader* r, const uint8_t* src, size_t n) {
             r->in.resize(old + n);
             par_memcpy(r->in.data() + old, src, n);
         }
-        std::lock_guard<std::mutex> g(r->ctx->mu);
-        HIPCHK(hipSetDevice(r->ctx->device));
+        ReaderLock g(r);
         int rc = reader_advance(r);
         if (rc) return rc;
         return reader_pump(r);
@@ -2442,8 +2472,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
                 if (S.out_pos < S.out_len) return S3HC_OK;
             }
         }
-        std::lock_guard<std::mutex> g(r->ctx->mu);
-        HIPCHK(hipSetDevice(r->ctx->device));
+        ReaderLock g(r);
         for (;;) {
             if (!r->inflight.empty() && r->slots[r->inflight.front()].ready) {
                 RSlot& S = r->slots[r->inflight.front()];
@@ -2501,14 +2530,21 @@ extern "C" void s3hc_reader_close(s3hc_reader* r) {
             fprintf(stderr, " %s %.1f", nm[k], r->tr.t[k] / (double)std::max<uint64_t>(1, r->tr.batches));
         fprintf(stderr, "\n");
     }
-    (void)hipSetDevice(r->ctx->device);
-    for (auto q : r->queues)
-        if (q) (void)hipStreamSynchronize(q);
+    const size_t nc = r->ctxs.size();
+    for (size_t q = 0; q < r->queues.size(); ++q)
+        if (r->queues[q]) {
+            (void)hipSetDevice(r->ctxs[q % nc]->device);
+            (void)hipStreamSynchronize(r->queues[q]);
+        }
     for (auto& S : r->slots) {
+        if (S.ctx) (void)hipSetDevice(S.ctx->device);
         if (S.ev) (void)hipEventDestroy(S.ev);
         if (S.ev2) (void)hipEventDestroy(S.ev2);
     }
-    for (auto q : r->queues)
-        if (q) (void)hipStreamDestroy(q);
+    for (size_t q = 0; q < r->queues.size(); ++q)
+        if (r->queues[q]) {
+            (void)hipSetDevice(r->ctxs[q % nc]->device);
+            (void)hipStreamDestroy(r->queues[q]);
+        }
     delete r;
 }

@@ -28,8 +28,10 @@
 #include <atomic>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "s3hc_guard.hpp"
@@ -90,21 +92,27 @@ int grow_dev(s3hc_ctx* ctx, void** p, size_t* cap, size_t n) {
 
 }  // namespace
 
+// One device of an aggregator: its context, HIP queue and staging (s3hc_aggregator_create_multi
+// gives one per device; a flush encodes one contiguous shard of the queued batches on each).
+struct Lane {
+    s3hc_ctx* ctx = nullptr;
+    void* queue = nullptr;   // the lane's HIP queue
+    Staging stg;
+};
+
 struct s3hc_aggregator {
-    s3hc_ctx* ctx;
+    std::vector<Lane> lanes;  // lanes[0]: the context of s3hc_aggregator_create
     size_t batch_size;
     size_t flush_bytes;
     uint32_t flush_batches;
     s3hc_handler* stats;     // optional shared counters (the writers' Arc<CompressionStatsAtomic>)
     uint8_t compress_mode = 0;  // compressed batches: 0 lz4_flex Auto, 2 64 KiB frames, kModeCompat
-    void* queue = nullptr;   // the aggregator's HIP queue
     std::mutex mu;           // guards pending / pending_bytes / counters
     std::mutex flush_mu;     // one aggregated flush at a time (keeps per-writer frame order)
     std::deque<Batch> pending;
     size_t pending_bytes = 0;
     uint64_t launches = 0;
     uint64_t batches_encoded = 0;
-    Staging stg;
 };
 
 struct s3hc_writer {
@@ -144,49 +152,61 @@ static void set_writer_error(s3hc_writer* w, int rc, const std::string& msg) {  
     }
 }
 
-// Encode every queued batch in one launch and deliver the frames in queue order.
-// Caller holds flush_mu.
-static int aggregated_flush(s3hc_aggregator* a) {
-    std::deque<Batch> work;
-    {
-        std::lock_guard<std::mutex> g(a->mu);
-        work.swap(a->pending);
-        a->pending_bytes = 0;
+// Contiguous shards by byte midpoint (s3hc_shard_items in s3hc_lz4.h).
+extern "C" int s3hc_shard_items(const uint64_t* len, uint32_t n, int ndev, uint32_t* first) {
+    if ((!len && n) || !first || ndev < 1) return werr(S3HC_INVALID_ARG, "bad arguments");
+    unsigned __int128 total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += len[i];
+    first[0] = 0;
+    first[ndev] = n;
+    uint32_t i = 0;
+    unsigned __int128 acc = 0;  // bytes of items [0, i)
+    for (int d = 1; d < ndev; ++d) {
+        // first item whose midpoint lies at or beyond d / ndev of the bytes
+        while (i < n && (2 * acc + len[i]) * (unsigned __int128)ndev < 2 * total * (unsigned __int128)d) acc += len[i++];
+        uint32_t f = i;
+        if (n >= (uint32_t)ndev) {  // every shard non-empty
+            f = std::max<uint32_t>(f, first[d - 1] + 1);
+            f = std::min<uint32_t>(f, n - (uint32_t)(ndev - d));
+        } else {
+            f = std::max<uint32_t>(f, first[d - 1]);
+        }
+        first[d] = f;
     }
-    if (work.empty()) return S3HC_OK;
-    const uint32_t n = (uint32_t)work.size();
+    return S3HC_OK;
+}
+
+// Encode batches [i0, i1) of `work` on one lane: frame[i] / flen[i] point into the lane's pinned
+// staging afterwards. On failure returns the status and sets *msg (the C ABI's message is
+// thread-local, so it is read on this thread).
+static int encode_shard(const s3hc_aggregator* a, Lane& Ln, const std::deque<Batch>& work, uint32_t i0, uint32_t i1,
+                        std::vector<const uint8_t*>& frame, std::vector<uint32_t>& flen, std::string* msg) {
+    const uint32_t n = i1 - i0;
     std::vector<uint64_t> off(n);
     std::vector<uint32_t> len(n);
     std::vector<uint8_t> mode(n);
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; ++i) {
         off[i] = total;
-        len[i] = (uint32_t)work[i].data.size();
-        mode[i] = work[i].mode;
+        len[i] = (uint32_t)work[i0 + i].data.size();
+        mode[i] = work[i0 + i].mode;
         total += len[i];
     }
-    auto fail_all = [&](int rc, const char* what) {
-        const std::string msg = std::string(what) + ": " + s3hc_last_error();
-        std::lock_guard<std::mutex> g(a->mu);
-        for (auto& b : work) {
-            set_writer_error(b.w, rc, msg);
-            b.w->queued--;
-        }
-        return werr(rc, msg);
+    auto failed = [&](int rc, const char* what) {
+        *msg = std::string(what) + ": " + s3hc_last_error();
+        return rc;
     };
-    s3hc_ctx* ctx = a->ctx;
-    Staging& S = a->stg;
+    s3hc_ctx* ctx = Ln.ctx;
+    Staging& S = Ln.stg;
     int rc = grow_host(ctx, &S.h_in, &S.h_in_cap, total + 64);
     if (!rc) rc = grow_dev(ctx, &S.d_in, &S.d_in_cap, total + 64);
-    if (rc) return fail_all(rc, "staging allocation");
-    for (uint32_t i = 0; i < n; ++i) memcpy((uint8_t*)S.h_in + off[i], work[i].data.data(), len[i]);
+    if (rc) return failed(rc, "staging allocation");
+    for (uint32_t i = 0; i < n; ++i) memcpy((uint8_t*)S.h_in + off[i], work[i0 + i].data.data(), len[i]);
     // plan-encoded batches (Auto / 64 KiB frames / store-mode) and compat batches
     std::vector<uint32_t> ia, ic;
     for (uint32_t i = 0; i < n; ++i) (mode[i] == kModeCompat ? ic : ia).push_back(i);
-    if (!rc && total) rc = s3hc_memcpy_async(ctx, S.d_in, S.h_in, total, 1, a->queue);
-    if (rc) return fail_all(rc, "staging copy");
-    std::vector<const uint8_t*> frame(n);
-    std::vector<uint32_t> flen(n);
+    if (total) rc = s3hc_memcpy_async(ctx, S.d_in, S.h_in, total, 1, Ln.queue);
+    if (rc) return failed(rc, "staging copy");
     if (!ia.empty()) {
         const uint32_t na = (uint32_t)ia.size();
         std::vector<uint64_t> offa(na);
@@ -195,7 +215,7 @@ static int aggregated_flush(s3hc_aggregator* a) {
         for (uint32_t j = 0; j < na; ++j) { offa[j] = off[ia[j]]; lena[j] = len[ia[j]]; modea[j] = mode[ia[j]]; }
         s3hc_plan* plan = nullptr;
         rc = s3hc_plan_encode(ctx, offa.data(), lena.data(), modea.data(), na, &plan);
-        if (rc) return fail_all(rc, "plan");
+        if (rc) return failed(rc, "plan");
         const uint64_t bound = s3hc_plan_dst_bound(plan);
         rc = grow_dev(ctx, &S.d_out, &S.d_out_cap, bound + 64);
         if (!rc) rc = grow_host(ctx, &S.h_out, &S.h_out_cap, bound + 64);
@@ -203,18 +223,18 @@ static int aggregated_flush(s3hc_aggregator* a) {
         if (!rc) rc = grow_host(ctx, &S.h_meta, &S.h_meta_cap, 12ull * na + 64);
         uint64_t* d_ioff = (uint64_t*)S.d_meta;
         uint32_t* d_ilen = (uint32_t*)((uint8_t*)S.d_meta + 8ull * na);
-        if (!rc) rc = s3hc_encode_dev(ctx, plan, (const uint8_t*)S.d_in, (uint8_t*)S.d_out, S.d_out_cap, d_ioff, d_ilen, a->queue);
-        if (!rc) rc = s3hc_memcpy_async(ctx, S.h_meta, S.d_meta, 12ull * na, 2, a->queue);
-        if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
+        if (!rc) rc = s3hc_encode_dev(ctx, plan, (const uint8_t*)S.d_in, (uint8_t*)S.d_out, S.d_out_cap, d_ioff, d_ilen, Ln.queue);
+        if (!rc) rc = s3hc_memcpy_async(ctx, S.h_meta, S.d_meta, 12ull * na, 2, Ln.queue);
+        if (!rc) rc = s3hc_queue_sync(ctx, Ln.queue);
         s3hc_plan_free(plan);
-        if (rc) return fail_all(rc, "encode");
+        if (rc) return failed(rc, "encode");
         const uint64_t* io = (const uint64_t*)S.h_meta;
         const uint32_t* il = (const uint32_t*)((const uint8_t*)S.h_meta + 8ull * na);
         const uint64_t bytes = io[na - 1] + il[na - 1];  // frames are packed in item order
-        rc = s3hc_memcpy_async(ctx, S.h_out, S.d_out, bytes, 2, a->queue);
-        if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
-        if (rc) return fail_all(rc, "frame copy");
-        for (uint32_t j = 0; j < na; ++j) { frame[ia[j]] = (const uint8_t*)S.h_out + io[j]; flen[ia[j]] = il[j]; }
+        rc = s3hc_memcpy_async(ctx, S.h_out, S.d_out, bytes, 2, Ln.queue);
+        if (!rc) rc = s3hc_queue_sync(ctx, Ln.queue);
+        if (rc) return failed(rc, "frame copy");
+        for (uint32_t j = 0; j < na; ++j) { frame[i0 + ia[j]] = (const uint8_t*)S.h_out + io[j]; flen[i0 + ia[j]] = il[j]; }
     }
     if (!ic.empty()) {
         const uint32_t nc = (uint32_t)ic.size();
@@ -232,42 +252,93 @@ static int aggregated_flush(s3hc_aggregator* a) {
         if (!rc) rc = grow_host(ctx, &S.h_cout, &S.h_cout_cap, lens_at + 4ull * nc + 64);
         uint32_t* d_clen = (uint32_t*)((uint8_t*)S.d_cout + lens_at);
         if (!rc) rc = s3hc_compat_encode_dev(ctx, (const uint8_t*)S.d_in, offc.data(), lenc.data(), nc,
-                                             (uint8_t*)S.d_cout, dof.data(), d_clen, a->queue);
+                                             (uint8_t*)S.d_cout, dof.data(), d_clen, Ln.queue);
         // frame lengths first
-        if (!rc) rc = s3hc_memcpy_async(ctx, (uint8_t*)S.h_cout + lens_at, d_clen, 4ull * nc, 2, a->queue);
-        if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
-        if (rc) return fail_all(rc, "compat encode");
+        if (!rc) rc = s3hc_memcpy_async(ctx, (uint8_t*)S.h_cout + lens_at, d_clen, 4ull * nc, 2, Ln.queue);
+        if (!rc) rc = s3hc_queue_sync(ctx, Ln.queue);
+        if (rc) return failed(rc, "compat encode");
         const uint32_t* cl = (const uint32_t*)((const uint8_t*)S.h_cout + lens_at);
-        for (uint32_t j = 0; j < nc; ++j) { frame[ic[j]] = (const uint8_t*)S.h_cout + dof[j]; flen[ic[j]] = cl[j]; }
+        for (uint32_t j = 0; j < nc; ++j) { frame[i0 + ic[j]] = (const uint8_t*)S.h_cout + dof[j]; flen[i0 + ic[j]] = cl[j]; }
         // then only each frame's own bytes (not its whole s3hc_frame_bound slot)
         for (uint32_t j = 0; j < nc && !rc; ++j)
-            if (cl[j]) rc = s3hc_memcpy_async(ctx, (uint8_t*)S.h_cout + dof[j], (const uint8_t*)S.d_cout + dof[j], cl[j], 2, a->queue);
-        if (!rc) rc = s3hc_queue_sync(ctx, a->queue);
-        if (rc) return fail_all(rc, "compat frame copy");
+            if (cl[j]) rc = s3hc_memcpy_async(ctx, (uint8_t*)S.h_cout + dof[j], (const uint8_t*)S.d_cout + dof[j], cl[j], 2, Ln.queue);
+        if (!rc) rc = s3hc_queue_sync(ctx, Ln.queue);
+        if (rc) return failed(rc, "compat frame copy");
     }
+    (void)a;
+    return S3HC_OK;
+}
+
+// Encode every queued batch (one launch per device: contiguous shards over the aggregator's
+// lanes, run concurrently) and deliver the frames in queue order. Caller holds flush_mu.
+static int aggregated_flush(s3hc_aggregator* a) {
+    std::deque<Batch> work;
     {
         std::lock_guard<std::mutex> g(a->mu);
-        a->launches++;
+        work.swap(a->pending);
+        a->pending_bytes = 0;
+    }
+    if (work.empty()) return S3HC_OK;
+    const uint32_t n = (uint32_t)work.size();
+    const int nl = (int)std::min<size_t>(a->lanes.size(), n);
+    std::vector<uint64_t> blen(n);
+    for (uint32_t i = 0; i < n; ++i) blen[i] = work[i].data.size();
+    std::vector<uint32_t> first(nl + 1);
+    (void)s3hc_shard_items(blen.data(), n, nl, first.data());
+    std::vector<const uint8_t*> frame(n, nullptr);
+    std::vector<uint32_t> flen(n, 0);
+    std::vector<int> rc(nl, S3HC_OK);
+    std::vector<std::string> msg(nl);
+    auto run = [&](int d) {
+        try {
+            if (first[d] < first[d + 1]) rc[d] = encode_shard(a, a->lanes[d], work, first[d], first[d + 1], frame, flen, &msg[d]);
+        } catch (const std::bad_alloc&) {
+            rc[d] = S3HC_NO_MEMORY;
+            msg[d] = "out of memory";
+        } catch (...) {
+            rc[d] = S3HC_DEVICE;
+            msg[d] = "internal error";
+        }
+    };
+    if (nl == 1) {
+        run(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int d = 1; d < nl; ++d) th.emplace_back(run, d);
+        run(0);
+        for (auto& t : th) t.join();
+    }
+    int first_rc = S3HC_OK;
+    std::string first_msg;
+    {
+        std::lock_guard<std::mutex> g(a->mu);
+        for (int d = 0; d < nl; ++d) {
+            if (rc[d] == S3HC_OK) continue;
+            if (!first_rc) { first_rc = rc[d]; first_msg = msg[d]; }
+            for (uint32_t i = first[d]; i < first[d + 1]; ++i) set_writer_error(work[i].w, rc[d], msg[d]);
+        }
+        for (int d = 0; d < nl; ++d) a->launches += rc[d] == S3HC_OK && first[d] < first[d + 1];
         a->batches_encoded += n;
     }
-    // deliver in queue order: each writer's frames keep their batch order
+    // deliver in queue order: each writer's frames keep their batch order (a writer with a
+    // failed batch gets none of its later frames)
     for (uint32_t i = 0; i < n; ++i) {
         s3hc_writer* w = work[i].w;
         const uint8_t* fr = frame[i];
         int src = S3HC_OK;
-        if (!w->error.load(std::memory_order_acquire)) {
+        if (!w->error.load(std::memory_order_acquire) && fr) {
             if (w->sink && w->sink(w->user, fr, flen[i]) != 0) {
                 src = S3HC_INVALID_ARG;
             } else {
                 w->compressed_bytes_written += flen[i];
-                if (a->stats) s3hc_handler_record_batch_bytes(a->stats, len[i], flen[i]);
+                if (a->stats) s3hc_handler_record_batch_bytes(a->stats, blen[i], flen[i]);
             }
         }
         std::lock_guard<std::mutex> g(a->mu);
         if (src) set_writer_error(w, src, "frame sink failed (write_all)");
         w->queued--;
     }
-    return S3HC_OK;
+    return first_rc ? werr(first_rc, first_msg) : S3HC_OK;
 }
 
 static int maybe_flush(s3hc_aggregator* a, bool force) {
@@ -300,6 +371,47 @@ static void queue_batch(s3hc_writer* w) {
     a->pending.push_back(std::move(b));
 }
 
+static void free_lane(Lane& L) {
+    s3hc_ctx* ctx = L.ctx;
+    Staging& S = L.stg;
+    if (S.h_in) s3hc_host_free(ctx, S.h_in);
+    if (S.h_out) s3hc_host_free(ctx, S.h_out);
+    if (S.h_meta) s3hc_host_free(ctx, S.h_meta);
+    if (S.d_in) s3hc_dev_free(ctx, S.d_in);
+    if (S.d_out) s3hc_dev_free(ctx, S.d_out);
+    if (S.d_meta) s3hc_dev_free(ctx, S.d_meta);
+    if (S.h_cout) s3hc_host_free(ctx, S.h_cout);
+    if (S.d_cout) s3hc_dev_free(ctx, S.d_cout);
+    if (L.queue) s3hc_queue_destroy(ctx, L.queue);
+    L = Lane();
+}
+
+static int aggregator_new(s3hc_ctx* const* ctxs, int nctx, size_t batch_size, size_t flush_bytes,
+                          uint32_t flush_batches, s3hc_handler* stats, s3hc_aggregator** out) {
+    for (int i = 0; i < nctx; ++i) {
+        if (!ctxs[i]) return werr(S3HC_INVALID_ARG, "NULL context");
+        for (int j = 0; j < i; ++j)
+            if (ctxs[j] == ctxs[i]) return werr(S3HC_INVALID_ARG, "a context is listed twice");
+    }
+    std::unique_ptr<s3hc_aggregator> a(new s3hc_aggregator);
+    a->batch_size = batch_size;
+    a->flush_bytes = flush_bytes;
+    a->flush_batches = flush_batches;
+    a->stats = stats;
+    a->lanes.resize(nctx);
+    for (int i = 0; i < nctx; ++i) {
+        a->lanes[i].ctx = ctxs[i];
+        int rc = s3hc_queue_create(ctxs[i], &a->lanes[i].queue);
+        if (rc) {
+            const std::string m = std::string("queue: ") + s3hc_last_error();
+            for (auto& L : a->lanes) if (L.ctx) free_lane(L);
+            return werr(rc, m);
+        }
+    }
+    *out = a.release();
+    return S3HC_OK;
+}
+
 extern "C" int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t flush_bytes, uint32_t flush_batches,
                                       s3hc_handler* stats, s3hc_aggregator** out) {
     return guarded([&]() -> int {
@@ -308,19 +420,16 @@ extern "C" int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t f
         // DiskCacheManager takes any batch size (its tests use 4-8 KiB); the 64 KiB..16 MiB bounds
         // belong to Config::validate (config.rs:1617-1627), the caller's configuration layer.
         if (batch_size == 0 || batch_size > 0xFFFFFFFFull / 2) return werr(S3HC_INVALID_ARG, "batch_size out of range");
-        s3hc_aggregator* a = new s3hc_aggregator;
-        a->ctx = ctx;
-        a->batch_size = batch_size;
-        a->flush_bytes = flush_bytes;
-        a->flush_batches = flush_batches;
-        a->stats = stats;
-        int rc = s3hc_queue_create(ctx, &a->queue);
-        if (rc) {
-            delete a;
-            return werr(rc, std::string("queue: ") + s3hc_last_error());
-        }
-        *out = a;
-        return S3HC_OK;
+        return aggregator_new(&ctx, 1, batch_size, flush_bytes, flush_batches, stats, out);
+    });
+}
+extern "C" int s3hc_aggregator_create_multi(s3hc_ctx* const* ctxs, int nctx, size_t batch_size, size_t flush_bytes,
+                                            uint32_t flush_batches, s3hc_handler* stats, s3hc_aggregator** out) {
+    return guarded([&]() -> int {
+        if (!ctxs || nctx < 1 || !out) return werr(S3HC_INVALID_ARG, "bad arguments");
+        *out = nullptr;
+        if (batch_size == 0 || batch_size > 0xFFFFFFFFull / 2) return werr(S3HC_INVALID_ARG, "batch_size out of range");
+        return aggregator_new(ctxs, nctx, batch_size, flush_bytes, flush_batches, stats, out);
     });
 }
 
@@ -355,17 +464,7 @@ extern "C" void s3hc_aggregator_destroy(s3hc_aggregator* a) {
         std::lock_guard<std::mutex> f(a->flush_mu);
         (void)aggregated_flush(a);
     }
-    s3hc_ctx* ctx = a->ctx;
-    Staging& S = a->stg;
-    if (S.h_in) s3hc_host_free(ctx, S.h_in);
-    if (S.h_out) s3hc_host_free(ctx, S.h_out);
-    if (S.h_meta) s3hc_host_free(ctx, S.h_meta);
-    if (S.d_in) s3hc_dev_free(ctx, S.d_in);
-    if (S.d_out) s3hc_dev_free(ctx, S.d_out);
-    if (S.d_meta) s3hc_dev_free(ctx, S.d_meta);
-    if (S.h_cout) s3hc_host_free(ctx, S.h_cout);
-    if (S.d_cout) s3hc_dev_free(ctx, S.d_cout);
-    if (a->queue) s3hc_queue_destroy(ctx, a->queue);
+    for (auto& L : a->lanes) free_lane(L);
     delete a;
 }
 

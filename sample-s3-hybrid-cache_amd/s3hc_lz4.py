@@ -124,6 +124,9 @@ def _load():
         "s3hc_reader_total": (u64, [vp]),
         "s3hc_reader_close": (None, [vp]),
         "s3hc_aggregator_create": (i32, [vp, sz, sz, u32, vp, ctypes.POINTER(vp)]),
+        "s3hc_aggregator_create_multi": (i32, [ctypes.POINTER(vp), i32, sz, sz, u32, vp, ctypes.POINTER(vp)]),
+        "s3hc_shard_items": (i32, [ctypes.POINTER(u64), u32, i32, ctypes.POINTER(u32)]),
+        "s3hc_reader_open_multi": (i32, [ctypes.POINTER(vp), i32, sz, i32, ctypes.POINTER(vp)]),
         "s3hc_aggregator_flush": (i32, [vp]),
         "s3hc_aggregator_set_frame_policy": (i32, [vp, i32]),
         "s3hc_aggregator_counters": (None, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
@@ -222,6 +225,15 @@ class knobs:
         for k, v in reversed(self.saved):
             _check(lib.s3hc_set_knob_value(k.encode(), v))
         return False
+
+
+def shard_items(lens, ndev: int) -> list[int]:
+    """s3hc_shard_items: first item of each of ndev contiguous shards (about equal bytes) + [n]."""
+    n = len(lens)
+    a = (ctypes.c_uint64 * max(n, 1))(*lens)
+    f = (ctypes.c_uint32 * (ndev + 1))()
+    _check(lib.s3hc_shard_items(a, n, ndev, f))
+    return list(f)
 
 
 def check_batch_results(olen, status, dst_off, slot_total):
@@ -569,9 +581,14 @@ class RangeReader:
     batches of ~batch_bytes run on `depth` HIP queues. batch_max (optional): batches queued behind
     running ones may take up to batch_max bytes of buffered frames (s3hc_reader_set_batch_max)."""
 
-    def __init__(self, eng: Engine, batch_bytes: int = 256 << 10, depth: int = 3, batch_max: int | None = None):
+    def __init__(self, eng, batch_bytes: int = 256 << 10, depth: int = 3, batch_max: int | None = None):
+        """eng: an Engine, or a list of Engines (s3hc_reader_open_multi: depth queues per device)."""
         h = ctypes.c_void_p()
-        _check(lib.s3hc_reader_open(eng.h, batch_bytes, depth, ctypes.byref(h)))
+        if isinstance(eng, (list, tuple)):
+            arr = (ctypes.c_void_p * len(eng))(*[e.h for e in eng])
+            _check(lib.s3hc_reader_open_multi(arr, len(eng), batch_bytes, depth, ctypes.byref(h)))
+        else:
+            _check(lib.s3hc_reader_open(eng.h, batch_bytes, depth, ctypes.byref(h)))
         self.h = h
         if batch_max is not None:
             _check(lib.s3hc_reader_set_batch_max(h, batch_max))
@@ -746,11 +763,18 @@ class RangeSpec:  # cache_types.rs:472-508 (codec fields)
 class BatchAggregator:
     """Coalesces the flush_batch calls of many writers into one encode launch."""
 
-    def __init__(self, eng: Engine, batch_size: int = 1 << 20, flush_bytes: int = 0, flush_batches: int = 0,
+    def __init__(self, eng, batch_size: int = 1 << 20, flush_bytes: int = 0, flush_batches: int = 0,
                  stats: "CompressionHandler | None" = None, frame_policy: int = BLK_AUTO_LZ4FLEX):
+        """eng: an Engine, or a list of Engines (s3hc_aggregator_create_multi: each flush is
+        split into contiguous shards, one per device)."""
         h = ctypes.c_void_p()
-        _wcheck(lib.s3hc_aggregator_create(eng.h, batch_size, flush_bytes, flush_batches,
-                                           stats.h if stats is not None else None, ctypes.byref(h)))
+        st = stats.h if stats is not None else None
+        if isinstance(eng, (list, tuple)):
+            arr = (ctypes.c_void_p * len(eng))(*[e.h for e in eng])
+            _wcheck(lib.s3hc_aggregator_create_multi(arr, len(eng), batch_size, flush_bytes, flush_batches, st,
+                                                     ctypes.byref(h)))
+        else:
+            _wcheck(lib.s3hc_aggregator_create(eng.h, batch_size, flush_bytes, flush_batches, st, ctypes.byref(h)))
         self.h, self.eng, self.stats = h, eng, stats
         if frame_policy != BLK_AUTO_LZ4FLEX:
             _wcheck(lib.s3hc_aggregator_set_frame_policy(h, frame_policy))

@@ -1,0 +1,134 @@
+"""Multi-device fan-out inside one process (the proxy's concurrent writers and
+range reads, /root/reference/src/http_proxy.rs:11608-11622): an aggregator and a range reader over
+several contexts. On a one-GPU box the contexts share device 0 (the --share-gpu rehearsal): the
+shard / dispatch logic and every copy between devices' queues run as on a multi-GPU node, and
+the output must be byte-identical to the one-context path. No collective is involved."""
+import threading
+
+import pytest
+
+import synth
+
+pytestmark = pytest.mark.gpu
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def engines():
+    import s3hc_lz4 as S
+
+    n = max(2, min(S.device_count(), 4))
+    return [S.Engine(i % S.device_count()) for i in range(n)]
+
+
+def _write_all(agg, datas, comp, chunk=16_384):
+    files, errs = [None] * len(datas), []
+
+    def run(k):
+        try:
+            d = datas[k]
+            w = agg.begin(0, len(d) - 1, comp[k])
+            for i in range(0, len(d), chunk):
+                w.write(d[i:i + chunk])
+            files[k] = w.file
+            w.commit()
+        except Exception as ex:  # pragma: no cover
+            errs.append(ex)
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(len(datas))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    return [bytes(f) for f in files]
+
+
+@pytest.mark.parametrize("policy", [0, 1, 2])
+def test_multi_device_aggregator_byte_identical(engine, engines, oracle, policy):
+    import s3hc_lz4 as S
+
+    nw = 20
+    datas = [synth.log_text(65536 * 3 + 999 * k, 500 + k) if k % 4 else synth.json_records(65536 * 2 + 17 * k, k)
+             for k in range(nw)]
+    comp = [k % 6 != 2 for k in range(nw)]
+    one = S.BatchAggregator(engine, 65536, flush_batches=12, frame_policy=policy)
+    many = S.BatchAggregator(engines, 65536, flush_batches=12, frame_policy=policy)
+    f1 = _write_all(one, datas, comp)
+    fm = _write_all(many, datas, comp)
+    assert fm == f1
+    for k in range(nw):
+        assert oracle.decompress_data(fm[k]) == datas[k]
+    assert one.counters()[1] == many.counters()[1]
+    one.close()
+    many.close()
+
+
+def test_multi_device_aggregator_splits_each_flush(engines, oracle):
+    # one writer, 8 full batches, one flush of all 8: one launch per device, frames in order
+    import s3hc_lz4 as S
+
+    data = synth.log_text(8 * 65536, 77)
+    agg = S.BatchAggregator(engines, 65536, flush_batches=8)
+    w = agg.begin(0, len(data) - 1, True)
+    for i in range(0, len(data), 65536):
+        w.write(data[i:i + 65536])
+    f = bytes(w.file)
+    w.commit()
+    launches, batches = agg.counters()
+    assert batches == 8 and launches == len(engines)
+    assert f == b"".join(engines[0].compress_frame(data[i:i + 65536]) for i in range(0, len(data), 65536))
+    assert oracle.decompress_data(f) == data
+    agg.close()
+
+
+def test_multi_device_aggregator_refuses_duplicate_context(engine):
+    import s3hc_lz4 as S
+
+    with pytest.raises(S.CodecError):
+        S.BatchAggregator([engine, engine], 65536)
+
+
+@pytest.mark.parametrize("batch,depth", [(256 << 10, 2), (4 * MiB, 1), (64 << 10, 3)])
+def test_multi_device_reader_matches(engines, oracle, batch, depth):
+    import s3hc_lz4 as S
+
+    data = synth.log_text(9 * MiB + 4321, 61)
+    frames = b"".join(oracle.lz4flex_compress_frame(data[i:i + 65536]) for i in range(0, len(data), 65536))
+    frames += oracle.lz4flex_compress_frame(data[:MiB])  # a reference-style 1 MiB frame
+    r = S.RangeReader(engines, batch, depth)
+    out = bytearray()
+    for i in range(0, len(frames), 3 * MiB):
+        r.feed(frames[i:i + 3 * MiB])
+        while True:
+            c = r.read(MiB)
+            if not c:
+                break
+            out += c
+    r.finish()
+    while True:
+        c = r.read(MiB)
+        if not c:
+            break
+        out += c
+    assert bytes(out) == data + data[:MiB]
+
+
+def test_multi_device_reader_corrupt_frame(engines, oracle):
+    import s3hc_lz4 as S
+
+    data = synth.log_text(40 * 65536, 62)
+    fr = [bytearray(oracle.lz4flex_compress_frame(data[i:i + 65536])) for i in range(0, len(data), 65536)]
+    fr[29][-1] ^= 0x10
+    r = S.RangeReader(engines, 100_000, 2)
+    r.feed(b"".join(bytes(f) for f in fr))
+    r.finish()
+    out = bytearray()
+    with pytest.raises(S.CodecError) as e:
+        while True:
+            c = r.read(MiB)
+            if not c:
+                break
+            out += c
+    assert e.value.status == S.S3HC_CHECKSUM
+    assert bytes(out) == data[:29 * 65536]

@@ -151,3 +151,33 @@ def test_reader_result_check_rejects_forged_results():
         assert e.value.status == S.S3HC_DEVICE
     # lengths after the first failing frame are not the decode's business: never read
     assert S.check_batch_results([10, 0xFFFFFFFF, 0xFFFFFFFF, 0], [0, 1, -1, 9], off, slot) == (1, 10)
+
+
+@pytest.mark.parametrize("ndev", [1, 2, 3, 8])
+def test_shard_items_contiguous_balanced(ndev):
+    # the multi-device aggregator's shards (host logic, no GPU)
+    import random
+
+    import s3hc_lz4 as S
+
+    rng = random.Random(ndev)
+    for n in (0, 1, ndev - 1, ndev, ndev + 1, 17, 300):
+        if n < 0:
+            continue
+        lens = [rng.choice((0, 1, 65536, 1 << 20, rng.randrange(1, 3 << 20))) for _ in range(n)]
+        f = S.shard_items(lens, ndev)
+        assert len(f) == ndev + 1 and f[0] == 0 and f[-1] == n
+        assert all(a <= b for a, b in zip(f, f[1:]))  # contiguous, in order
+        if n >= ndev:
+            assert all(a < b for a, b in zip(f, f[1:]))  # every device gets work
+        total = sum(lens)
+        if n >= ndev and total:
+            big = max(lens)
+            for d in range(ndev):
+                assert sum(lens[f[d]:f[d + 1]]) <= total / ndev + 2 * big  # about equal bytes
+    # equal items split evenly
+    assert S.shard_items([10] * 8, 4) == [0, 2, 4, 6, 8]
+    f = S.shard_items([10] * 3, 4)  # fewer items than devices: one item per used device
+    assert sum(b - a for a, b in zip(f, f[1:])) == 3 and all(b - a <= 1 for a, b in zip(f, f[1:]))
+    with pytest.raises(S.CodecError):
+        S.shard_items([1, 2], 0)
