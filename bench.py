@@ -281,9 +281,14 @@ def roofline_obj(kt, name, alg_bytes, profiled_shape: bool):
     }
     if tsrc:
         roof["traffic_source"] = tsrc + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same bench command)"
+        roof["traffic_bound"] = TRAFFIC_BOUND
     return roof
 
 
+# FETCH_SIZE is doubled for every kernel: the guide's halving applies to wide (16-B/lane) coalesced
+# streaming reads; for narrow gathers (k_dexec's sources, k_enc_parse's staged-input reads are LDS)
+# the doubled figure over-counts, so `traffic` is an upper bound of the HBM bytes
+TRAFFIC_BOUND = "upper: FETCH_SIZE x2 for every kernel (exact only for 16-B/lane streaming reads)"
 DECODE_PHASES = ("dec_plan", "decode", "dec_close")
 KERNEL_SYMBOL["dec_plan"] = "k_dframe_count+k_scan_u32_u64+k_dframe_fill"
 
@@ -311,6 +316,7 @@ def roofline_whole_decode(kt, alg_bytes, profiled_shape: bool):
     }
     if traffic is not None and tsrc:
         roof["traffic_source"] = tsrc + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same bench command)"
+        roof["traffic_bound"] = TRAFFIC_BOUND
     return roof
 
 
