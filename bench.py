@@ -52,6 +52,10 @@ def parse_args(argv=None):
     ap.add_argument("--total-blocks", type=int, default=0,
                     help="strong scaling instead: split this many blocks over the ranks (config 5: 1048576)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=3,
+                    help="extra steps after the timed region, every phase timed (kernel_ms_per_step)")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="diagnostics: no HIP events in the timed steps (no roofline; measures the events' cost)")
     ap.add_argument("--skip-check", action="store_true", help="diagnostic builds only: skip output checks")
     ap.add_argument("--cpu-seconds", type=float, default=1.0, help="wall seconds of each of the 5 CPU baseline runs")
     ap.add_argument("--selftest", action="store_true",
@@ -293,11 +297,12 @@ DECODE_PHASES = ("dec_plan", "decode", "dec_close")
 KERNEL_SYMBOL["dec_plan"] = "k_dframe_count+k_scan_u32_u64+k_dframe_fill"
 
 
-def roofline_whole_decode(kt, alg_bytes, profiled_shape: bool):
-    """(C + U) per step over the summed average time of the decode's three phases (frame walk,
-    block decode, verify), one event pair each on the launch stream."""
+def roofline_whole_decode(kt, alg_bytes, profiled_shape: bool, whole=None):
+    """(C + U) per step over the average time of the whole decode: `whole` = (ms, launches) of the
+    timed steps' single span over the three phases (frame walk, block decode, verify); without it
+    the summed averages of the phases' own event pairs."""
     parts = [p for p in DECODE_PHASES if p in kt]
-    ms = sum(kt[p][0] / kt[p][1] for p in parts)
+    ms = whole[0] / whole[1] if whole else sum(kt[p][0] / kt[p][1] for p in parts)
     achieved = alg_bytes / (ms / 1e3) / 1e9
     traffic, tsrc = None, None
     if profiled_shape:
@@ -314,6 +319,8 @@ def roofline_whole_decode(kt, alg_bytes, profiled_shape: bool):
         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
         "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(ms, 4),
     }
+    if whole:
+        roof["timed_in"] = "timed steps: one event pair over the three phases"
     if traffic is not None and tsrc:
         roof["traffic_source"] = tsrc + " (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same bench command)"
         roof["traffic_bound"] = TRAFFIC_BOUND
@@ -384,8 +391,11 @@ def run_rank(args):
         assert st == [0] * nb, f"decode status {set(st)}"
         assert d_out.read(2 * block) == first_chunk[: 2 * block]
 
+    # timed steps: HIP events only around the dominant kernel (k_enc_parse) and the whole decode
+    # (coarse spans: every event record is a dispatch boundary, so fewer of them perturb the
+    # timed region less); the per-phase breakdown comes from --profile-steps extra steps after it
     eng.timing_reset()
-    eng.set_timing(True)
+    eng.set_timing(not args.no_kernel_timing, coarse=True)
     g.barrier()
     eng.sync()
     t0 = time.perf_counter()
@@ -396,7 +406,16 @@ def run_rank(args):
     g.barrier()
     eng.set_timing(False)
     elapsed = g.max(t1 - t0)
-    kt = eng.timing()
+    kt_timed = eng.timing()
+    kt = {}
+    if not args.no_kernel_timing and args.profile_steps:
+        eng.timing_reset()
+        eng.set_timing(True)
+        for _ in range(args.profile_steps):
+            step()
+        eng.sync()
+        eng.set_timing(False)
+        kt = eng.timing()
 
     # full-output check after the timed steps: every block, every byte, chunk by chunk
     checked = 0
@@ -422,15 +441,21 @@ def run_rank(args):
         "decode": comp_bytes + nb * block,        # C read + U written
         "dec_close": nb * block,                  # U read (content xxh32 of every frame)
     }
-    dom = max(excl, key=lambda k: excl[k][0]) if excl else None
+    dom = max(excl, key=lambda k: excl[k][0] / excl[k][1]) if excl else None
     prof = nb == 4096 and not args.total_blocks
-    roof = roofline_obj(kt, dom, alg.get(dom, nb * block), prof) if dom else None
+    # the dominant kernel's launch duration: from the timed steps' own events (enc_parse is timed
+    # there), else from the profiled steps
+    kdom = kt_timed if dom in kt_timed else kt
+    roof = roofline_obj(kdom, dom, alg.get(dom, nb * block), prof) if dom else None
+    if roof:
+        roof["timed_in"] = "timed steps" if kdom is kt_timed else f"{args.profile_steps} profiled steps after the timed ones"
     # north_star decode figure over the whole decode the reference does in one FrameDecoder pass
     # (compression.rs:479-480): the plan's device frame walk, the block decode and the content
-    # xxh32 verify + EndMark checks; the block-decode kernels alone are the extra key
-    roof_dec = roofline_whole_decode(kt, alg["decode"], prof) if "decode" in kt else None
+    # xxh32 verify + EndMark checks, timed as one span in the timed steps ("dec_all"); the phase
+    # breakdown and the block-decode kernels alone come from the profiled steps
+    roof_dec = roofline_whole_decode(kt, alg["decode"], prof, kt_timed.get("dec_all")) if "decode" in kt else None
     roof_dec_k = roofline_obj(kt, "decode", alg["decode"], prof) if "decode" in kt else None
-    per_kernel = {k: round(v[0] / args.steps, 4) for k, v in kt.items()}
+    per_kernel = {k: round(v[0] / v[1], 4) for k, v in kt.items()}
     rank_rate = nb * block * args.steps / (t1 - t0) / GiB
     rates, devs = [rank_rate], [dev]
     if g.dist is not None:
@@ -471,6 +496,7 @@ def run_rank(args):
             "devices": {"visible": ndev, "rank_device": devs, "shared": len(set(devs)) < len(devs)},
             "blocks_checked": int(checked_all),
             "kernel_ms_per_step": per_kernel,
+            "kernel_ms_source": f"{args.profile_steps} steps after the timed ones, every phase its own event pair",
             "roofline": roof,
             "roofline_decode": roof_dec,
             "roofline_decode_kernels": roof_dec_k,

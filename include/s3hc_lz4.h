@@ -183,10 +183,12 @@ int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* plan, const uint8_t* d_src, uint8_
                     uint32_t* d_out_len, int32_t* d_status, void* stream);
 void s3hc_plan_free(s3hc_plan* plan);
 
-/* Per-kernel timing for roofline accounting: with timing on, every *_dev launch is bracketed
- * by HIP events on its stream (no host sync). s3hc_timing_collect resolves them into per-name
- * totals: s3hc_last_kernel_ms = summed ms, s3hc_kernel_count = launches.
- * Names: "xxh32", "enc_parse", "enc_sizes", "enc_emit", "dec_plan", "decode", "dec_finish". */
+/* Per-kernel timing for roofline accounting: with timing on, the phases of every *_dev launch are
+ * bracketed by HIP events on its stream (no host sync; adjacent phases share their boundary
+ * event). s3hc_timing_collect resolves them into per-name totals: s3hc_last_kernel_ms = summed
+ * ms, s3hc_kernel_count = launches. enabled: 0 off; 1 every phase ("xxh32", "enc_parse",
+ * "enc_sizes", "enc_emit", "dec_plan", "decode", "dec_close", ...); 2 coarse: "enc_parse" and one
+ * "dec_all" span over the whole device decode (fewest events in a timed region). */
 void s3hc_set_timing(s3hc_ctx* ctx, int enabled);
 int s3hc_timing_collect(s3hc_ctx* ctx);
 void s3hc_timing_reset(s3hc_ctx* ctx);

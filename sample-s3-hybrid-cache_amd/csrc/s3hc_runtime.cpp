@@ -617,12 +617,13 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
 struct TimedSpan {
     std::string name;
     hipEvent_t a, b;
+    bool shared_a;  // a is the previous span's b (returned to the pool once, with that span)
 };
 struct s3hc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
-    bool timing = false;
+    int timing = 0;  // 0 off, 1 every phase, 2 coarse (enc_parse, dec_all)
     std::map<std::string, float> kernel_ms;
     std::map<std::string, int> kernel_n;
     std::vector<TimedSpan> pending;
@@ -650,10 +651,15 @@ struct s3hc_ctx {
 
 // Per-kernel event timing (s3hc_set_timing). Events come from a pool and are only resolved
 // by s3hc_timing_collect(), so timing adds no host synchronisation inside a timed region.
+// Adjacent phases of one call share their boundary event (a phase that begins right where the
+// previous one ended reuses its end event): every event record on the stream is a dispatch
+// boundary the command processor waits at, so fewer records perturb the timed region less.
 struct KTimer {
     s3hc_ctx* ctx;
     hipStream_t st;
+    bool adjacent = false;  // the last call was end(): nothing was enqueued since
     explicit KTimer(s3hc_ctx* c, hipStream_t s) : ctx(c), st(s) {}
+    bool fine() const;      // every phase its own span (s3hc_set_timing 1), else the coarse spans (2)
     void begin(const char* name);
     void end();
 };
@@ -680,19 +686,32 @@ struct s3hc_plan {
     LbScratch lb;                        // large-block path scratch (frames allowing > 64 KiB blocks)
 };
 
+bool KTimer::fine() const { return ctx->timing != 2; }
 void KTimer::begin(const char* name) {
     if (!ctx->timing) return;
-    TimedSpan t{name, ctx->take_event(), ctx->take_event()};
-    (void)hipEventRecord(t.a, st);
-    ctx->pending.push_back(t);
+    if (adjacent && !ctx->pending.empty()) {
+        // this phase starts where the previous one ended: its start is that end event (a shared
+        // event is never handed back to the pool twice: the span marks it as borrowed)
+        TimedSpan t{name, ctx->pending.back().b, ctx->take_event(), true};
+        ctx->pending.push_back(t);
+    } else {
+        TimedSpan t{name, ctx->take_event(), ctx->take_event(), false};
+        (void)hipEventRecord(t.a, st);
+        ctx->pending.push_back(t);
+    }
+    adjacent = false;
 }
 void KTimer::end() {
     if (!ctx->timing || ctx->pending.empty()) return;
     (void)hipEventRecord(ctx->pending.back().b, st);
+    adjacent = true;
 }
 
 s3hc_ctx::~s3hc_ctx() {
-    for (auto& t : pending) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
+    for (auto& t : pending) {
+        if (!t.shared_a) (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
     for (auto e : event_pool) (void)hipEventDestroy(e);
     delete host_plan;
     if (stream) (void)hipStreamDestroy(stream);
@@ -792,20 +811,23 @@ static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t
                             P->d_frame_src_off.as<uint64_t>(), P->d_frame_src_len.as<uint32_t>(), nf,
                             P->d_frame_hash.as<uint32_t>(), P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), st));
     T.end();
-    T.begin("enc_sizes");
+    const bool fine = T.fine();
+    if (fine) T.begin("enc_sizes");
     HIPCHK(launch_enc_sizes(P->d_blocks.as<EncBlock>(), nb, P->d_summ.as<SegSummary>(), P->d_place.as<SegPlace>(),
                             P->d_blk_payload.as<uint32_t>(), P->d_blk_size.as<uint32_t>(),
                             P->d_blk_carry.as<uint32_t>(), st));
     HIPCHK(launch_scan(P->d_blk_size.as<uint32_t>(), nb, P->d_blk_off.as<uint64_t>(), P->d_total.as<uint64_t>(), st));
-    T.end();
-    T.begin("enc_emit");
+    if (fine) {
+        T.end();
+        T.begin("enc_emit");
+    }
     HIPCHK(launch_enc_emit(d_src, P->d_blocks.as<EncBlock>(), P->d_seg_block.as<uint32_t>(), nseg,
                            P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), P->d_place.as<SegPlace>(),
                            P->d_blk_payload.as<uint32_t>(), P->d_blk_carry.as<uint32_t>(),
                            P->d_blk_off.as<uint64_t>(), P->d_frame_hash.as<uint32_t>(), d_dst, st));
     HIPCHK(launch_enc_groups(P->d_item_blk0.as<uint32_t>(), P->d_item_nblk.as<uint32_t>(), ni,
                              P->d_blk_off.as<uint64_t>(), P->d_blk_size.as<uint32_t>(), d_item_off, d_item_len, st));
-    T.end();
+    if (fine) T.end();
     return S3HC_OK;
 }
 
@@ -914,7 +936,9 @@ extern "C" void s3hc_destroy(s3hc_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     delete ctx;
 }
-extern "C" void s3hc_set_timing(s3hc_ctx* ctx, int enabled) { if (ctx) ctx->timing = enabled != 0; }
+extern "C" void s3hc_set_timing(s3hc_ctx* ctx, int enabled) {
+    if (ctx) ctx->timing = enabled == 2 ? 2 : (enabled != 0 ? 1 : 0);
+}
 // Resolve recorded spans into per-name totals (ms) and launch counts; clears the spans.
 extern "C" int s3hc_timing_collect(s3hc_ctx* ctx) {
     return guarded([&]() -> int {
@@ -927,7 +951,7 @@ extern "C" int s3hc_timing_collect(s3hc_ctx* ctx) {
             HIPCHK(hipEventElapsedTime(&ms, t.a, t.b));
             ctx->kernel_ms[t.name] += ms;
             ctx->kernel_n[t.name] += 1;
-            ctx->event_pool.push_back(t.a);
+            if (!t.shared_a) ctx->event_pool.push_back(t.a);
             ctx->event_pool.push_back(t.b);
         }
         ctx->pending.clear();
@@ -1077,7 +1101,8 @@ extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src
         const uint32_t n = P->nframes;
         if (!n) return S3HC_OK;
         KTimer T(ctx, st);
-        T.begin("dec_plan");
+        const bool fine = T.fine();
+        T.begin(fine ? "dec_plan" : "dec_all");  // (coarse timing: the whole decode, one span)
         HIPCHK(launch_dframe_count(d_src, P->d_frame_off.as<uint64_t>(), P->d_frame_len.as<uint32_t>(),
                                    P->d_dst_cap.as<uint32_t>(), n, P->d_nblk.as<uint32_t>(), d_status, st));
         HIPCHK(launch_scan(P->d_nblk.as<uint32_t>(), n, P->d_blk_base.as<uint64_t>(), P->d_total.as<uint64_t>(), st));
@@ -1086,17 +1111,21 @@ extern "C" int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src
                                   P->d_dst_off.as<uint64_t>(), P->d_dst_cap.as<uint32_t>(), P->d_blk_base.as<uint64_t>(),
                                   d_status, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(),
                                   P->d_fwant.as<uint32_t>(), P->d_ftok.as<uint64_t>(), st));
-        T.end();
-        T.begin("decode");
+        if (fine) {
+            T.end();
+            T.begin("decode");
+        }
         const uint64_t* bh = nullptr;
         // one workgroup per frame (the common one block per frame: the exact unit count); frames of
         // several independent blocks have their extra units taken by a stride of the grid
         HIPCHK(decode_launch(&P->lb, d_src, d_dst, P->d_dblocks.as<DecBlock>(), P->d_units.as<DecUnit>(), P->blk_cap,
                              P->d_blk_out.as<uint32_t>(), P->d_blk_status.as<int32_t>(), st, &bh,
                              P->d_total.as<uint64_t>(), P->dec_grid));
-        T.end();
-        // frame results, content xxh32 and EndMark checks (one launch)
-        T.begin("dec_close");
+        if (fine) {
+            T.end();
+            // frame results, content xxh32 and EndMark checks (one launch)
+            T.begin("dec_close");
+        }
         HIPCHK(launch_dframe_close(d_src, P->d_frame_off.as<uint64_t>(), P->d_blk_base.as<uint64_t>(),
                                    P->d_nblk.as<uint32_t>(), P->d_dblocks.as<DecBlock>(), P->d_blk_out.as<uint32_t>(),
                                    P->d_blk_status.as<int32_t>(), bh, d_dst, P->d_dst_off.as<uint64_t>(),

@@ -312,8 +312,9 @@ class Engine:
         return FrameStream(self)
 
     # ---- timing of the last *_dev call
-    def set_timing(self, on: bool):
-        lib.s3hc_set_timing(self.h, 1 if on else 0)
+    def set_timing(self, on, coarse: bool = False):
+        """on: every phase its own span; coarse: only "enc_parse" and "dec_all" (fewest events)."""
+        lib.s3hc_set_timing(self.h, (2 if coarse else 1) if on else 0)
 
     def timing_reset(self):
         lib.s3hc_timing_reset(self.h)
@@ -323,7 +324,7 @@ class Engine:
         _check(lib.s3hc_timing_collect(self.h))
         out = {}
         for name in ("xxh32_side", "xxh32", "enc_parse", "enc_sizes", "enc_emit", "dec_plan", "decode", "dec_finish", "dec_close",
-                     "compat"):
+                     "dec_all", "compat"):
             n = lib.s3hc_kernel_count(self.h, name.encode())
             if n:
                 out[name] = (lib.s3hc_last_kernel_ms(self.h, name.encode()), n)
