@@ -52,6 +52,8 @@ def parse_args(argv=None):
     ap.add_argument("--total-blocks", type=int, default=0,
                     help="strong scaling instead: split this many blocks over the ranks (config 5: 1048576)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="two queues: step k's decode overlaps step k+1's encode (rooflines then include overlap)")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="extra steps after the timed region, every phase timed (kernel_ms_per_step)")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -378,13 +380,51 @@ def run_rank(args):
     dplan = eng.plan_decode(fo, fl, offs, [block] * nb)
     comp_bytes = fo[-1] + fl[-1]
 
+    # --pipeline: steps over two HIP queues, step k's decode (queue D) overlapping step k+1's
+    # encode (queue E), which writes the other of two frame buffers; marks order enc(k) -> dec(k)
+    # and dec(k) -> enc(k + 2). Every step still encodes and decodes its whole batch; the tail of
+    # one kernel and the head of the next share the chip (+2.7 % per step), but the
+    # kernels' own event spans then include the other queue's work, so the roofline durations are
+    # not a kernel's own: the default stays one queue (serial), whose spans are.
+    args.serial = not args.pipeline
+    q_enc, q_dec = (None, None) if args.serial else (eng.queue(), eng.queue())
+    frames = [d_frames] if args.serial else [d_frames, eng.alloc(plan.dst_bound)]
+    ioffs = [d_ioff] if args.serial else [d_ioff, eng.alloc(8 * nb)]
+    ilens = [d_ilen] if args.serial else [d_ilen, eng.alloc(4 * nb)]
+    after_dec = {}
+    nstep = [0]
+
     def step():
-        eng.encode_dev(plan, d_src, d_frames, d_ioff, d_ilen)
-        eng.decode_dev(dplan, d_frames, d_out, d_olen, d_ost)
+        i = nstep[0]
+        nstep[0] += 1
+        if args.serial:
+            eng.encode_dev(plan, d_src, d_frames, d_ioff, d_ilen)
+            eng.decode_dev(dplan, d_frames, d_out, d_olen, d_ost)
+            return
+        b = i & 1
+        if i - 2 in after_dec:  # the decode that read this frame buffer is done
+            m = after_dec.pop(i - 2)
+            eng.wait_mark(m, q_enc)
+            eng.free_mark(m)
+        eng.encode_dev(plan, d_src, frames[b], ioffs[b], ilens[b], q_enc)
+        m = eng.mark(q_enc)
+        eng.wait_mark(m, q_dec)
+        eng.free_mark(m)
+        eng.decode_dev(dplan, frames[b], d_out, d_olen, d_ost, q_dec)
+        after_dec[i] = eng.mark(q_dec)
+
+    def sync_all():
+        if not args.serial:
+            q_enc.sync()
+            q_dec.sync()
+            for k in list(after_dec):
+                if k < nstep[0] - 2:
+                    eng.free_mark(after_dec.pop(k))
+        eng.sync()
 
     for _ in range(args.warmup):
         step()
-    eng.sync()
+    sync_all()
     # correctness gate on the warmed-up state (outside the timed region)
     if not args.skip_check:
         st = d_ost.i32(nb)
@@ -401,7 +441,7 @@ def run_rank(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    eng.sync()
+    sync_all()
     t1 = time.perf_counter()
     g.barrier()
     eng.set_timing(False)
@@ -413,7 +453,7 @@ def run_rank(args):
         eng.set_timing(True)
         for _ in range(args.profile_steps):
             step()
-        eng.sync()
+        sync_all()
         eng.set_timing(False)
         kt = eng.timing()
 
@@ -488,6 +528,7 @@ def run_rank(args):
                              else f"config2: {nb} x 64 KiB log-text blocks per GPU") + ", LZ4 frame encode + decode, device-resident",
                 "blocks_per_gpu": nb, "block_bytes": block, "frame": "FLG 0x64 BD 0x40 (lz4_flex Auto), xxh32 content checksum",
                 "compression_ratio": round(comp_bytes / (nb * block), 4), "parallelism": f"shard{world}",
+                "queues": "pipelined (enc on E, dec on D)" if args.pipeline else "one queue, steps back to back",
                 "decode_plan": "built before timing from the frame offsets/lengths the encoder wrote (read back once: "
                                "they are the same every step); the plan's frame walk (headers, block table, units) "
                                "runs on the device inside every timed step",
