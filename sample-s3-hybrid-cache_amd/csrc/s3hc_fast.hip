@@ -1484,15 +1484,18 @@ __device__ __forceinline__ uint32_t xxh32_lane4(const uint8_t* __restrict__ p, u
 }
 
 // Blocks the token index leaves (stored, malformed, linked, > kFastMaxC compressed) keep bh 0 and
-// unit_fast 0: the per-unit decoder (k_decode_pe, next launch on the queue) gives them their exact
-// statuses, and k_dframe_close closes the frames. (Round 4 ran both inside this kernel; the
-// per-unit decoder's barriers on two of the sixteen waves then paired with the other waves' own,
-// which is the fault of GPUTEST_r04 — every barrier here is reached by all 1024 threads.)
+// unit_fast 0 and get their exact statuses from the per-unit decoder: with own_left (a launch of
+// one workgroup per unit and no large-block path) this workgroup runs it itself — waves 2-15
+// leave the kernel first, so decode_unit_pe's barriers count waves 0-1 only and no barrier of
+// this kernel follows; otherwise the per-unit decoder's own launch (k_decode_pe) takes them.
+// k_dframe_close closes the frames. (Round 4 also ran the frame close in the last workgroup and
+// let waves 2-15 wait at the close's barriers while waves 0-1 were inside the per-unit decoder:
+// the barriers paired across code locations, which is the fault of GPUTEST_r04.)
 __global__ __launch_bounds__(jmp::kT) void k_djump(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                    const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
                                                    uint32_t nunits, const uint8_t* __restrict__ unit_lb, FastArgs a,
                                                    uint32_t maxc, uint32_t* __restrict__ blk_out,
-                                                   int32_t* __restrict__ blk_status) {
+                                                   int32_t* __restrict__ blk_status, uint32_t own_left) {
     using namespace jmp;
     extern __shared__ __attribute__((aligned(16))) uint8_t dsm[];  // (dtok_unit's staged block, then P)
     uint16_t* P = (uint16_t*)dsm;
@@ -1505,7 +1508,12 @@ __global__ __launch_bounds__(jmp::kT) void k_djump(const uint8_t* __restrict__ s
         FastUnit F;
         // token index and records with all 16 waves (1024 speculative segments)
         if (!dtok_unit<kT>(u, src, blk, units, unit_lb, a, maxc, &F)) {  // (a unit it leaves: bh 0)
-            __syncthreads();
+            __syncthreads();  // (every thread is done with the staged block)
+            if (own_left && gridDim.x >= nunits) {  // (this workgroup's only unit)
+                if (t >= 128u) return;
+                decode_unit_pe(u, dsm, src, dst, blk, units, blk_out, blk_status, nullptr, nullptr);
+                return;
+            }
             continue;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the records are in memory before the barrier
@@ -1744,9 +1752,11 @@ extern "C" int s3hc_diag_fprof(unsigned long long* out, int n, int reset) {
     return 0;
 }
 #endif
+// own_left: the launch also decodes the units the fast path leaves (k_djump; no k_decode_pe needed)
 hipError_t launch_fast_small(const uint8_t* src, uint8_t* dst, const DecBlock* blk, const DecUnit* units,
                              uint32_t nunits, const uint8_t* unit_lb, const FastArgs& a, uint32_t* blk_out,
-                             int32_t* blk_status, hipStream_t st) {
+                             int32_t* blk_status, hipStream_t st, bool own_left, bool* owned) {
+    *owned = false;
     if (!nunits || !a.maxc) return hipSuccess;
     const uint32_t maxc = a.maxc < kFastMaxC ? a.maxc : kFastMaxC;
 #if S3HC_SMALL_JUMP
@@ -1754,7 +1764,8 @@ hipError_t launch_fast_small(const uint8_t* src, uint8_t* dst, const DecBlock* b
                                                        (int)jmp::kLds);  // (> 64 KiB of dynamic LDS)
     if (attr != hipSuccess) return attr;
     hipLaunchKernelGGL(k_djump, dim3(nunits), dim3(jmp::kT), jmp::kLds, st, src, dst, blk, units, nunits, unit_lb, a,
-                       maxc, blk_out, blk_status);
+                       maxc, blk_out, blk_status, own_left ? 1u : 0u);
+    *owned = own_left;
 #else
     hipLaunchKernelGGL(k_dsmall, dim3(nunits), dim3(fst::kTT), fast_lds_bytes(maxc), st, src, dst, blk, units, nunits,
                        unit_lb, a, maxc, blk_out, blk_status);

@@ -41,7 +41,7 @@ hipError_t launch_fast_exec(const uint8_t*, uint8_t*, const DecBlock*, const Dec
                             uint32_t, uint32_t*, int32_t*, const FastArgs&, hipStream_t);
 bool fast_exec_hashes();
 hipError_t launch_fast_small(const uint8_t*, uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint8_t*,
-                             const FastArgs&, uint32_t*, int32_t*, hipStream_t);
+                             const FastArgs&, uint32_t*, int32_t*, hipStream_t, bool, bool*);
 hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const DecUnit*, uint32_t, const uint64_t*,
                            uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, uint32_t*, int32_t*, hipStream_t);
@@ -566,11 +566,13 @@ static hipError_t decode_launch(LbScratch* L, const uint8_t* src, uint8_t* dst, 
         L->fa.bh = nullptr;
     }
     if (fast && L->small) {
-        // small host-walked launch: token index + block decode + content xxh32 in one launch; the
-        // per-unit decoder below takes the blocks it leaves
+        // small host-walked launch: token index + block decode + content xxh32 in one launch; without
+        // large blocks it also runs the per-unit decoder for the blocks it leaves (no second launch)
+        bool owned = false;
         if ((e = launch_fast_small(src, dst, blk, units, nunits, lb ? L->a.unit_lb : nullptr, L->fa, blk_out,
-                                   blk_status, st)) != hipSuccess)
+                                   blk_status, st, !lb, &owned)) != hipSuccess)
             return e;
+        if (owned) return hipSuccess;
     } else if (fast) {
         if ((e = launch_fast_tok(src, blk, units, nunits, ucount, grid, lb ? L->a.unit_lb : nullptr, L->fa, st)) !=
             hipSuccess)
@@ -646,8 +648,15 @@ struct s3hc_ctx {
     DevBuf d_ftab, d_fstat, d_flen, d_fhash;                  // per-frame tables of decode_walk
     HostStage hs;
     LbScratch lb;
+    // range-reader resources kept warm between the readers of this context (s3hc_reader_*): one
+    // reader per GET (stream_range_data) would otherwise allocate its pinned and device buffers,
+    // HIP queues and events on every open
+    std::mutex rpool_mu;
+    std::vector<void*> rslot_pool;         // RSlot* (reader section)
+    std::vector<hipStream_t> rqueue_pool;  // non-blocking queues of this device
     ~s3hc_ctx();
 };
+static void reader_pool_release(s3hc_ctx* ctx);
 
 // Per-kernel event timing (s3hc_set_timing). Events come from a pool and are only resolved
 // by s3hc_timing_collect(), so timing adds no host synchronisation inside a timed region.
@@ -934,6 +943,7 @@ extern "C" void s3hc_destroy(s3hc_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    reader_pool_release(ctx);
     delete ctx;
 }
 extern "C" void s3hc_set_timing(s3hc_ctx* ctx, int enabled) {
@@ -2057,8 +2067,79 @@ struct RSlot {
     uint64_t R = 0;         // d_out / h_out: frame results (u32 lengths, i32 statuses) in [0, R), slots after
     uint64_t slot = 0;      // decoded-slot bytes of the batch (frame f's slot: [dst_off[f], dst_off[f + 1]))
     int32_t err = 0;        // status of the first failing frame (good < n)
+    void reset() {          // (a slot taken from its context's pool: buffers kept, batch state cleared)
+        n = 0; state = 0; ready = false; good = 0; out_len = 0; out_pos = 0; spec = 0; covered = false;
+        R = 0; slot = 0; err = 0; dst_off.clear(); st = nullptr;
+    }
+    ~RSlot() {
+        if (ctx) (void)hipSetDevice(ctx->device);
+        if (ev) (void)hipEventDestroy(ev);
+        if (ev2) (void)hipEventDestroy(ev2);
+    }
 };
+constexpr size_t kReaderPoolMax = 64;  // pooled slots (and queues) per context
+// A slot of ctx (its device current): from the context's pool, else new with its two events.
+RSlot* rslot_take(s3hc_ctx* c) {
+    {
+        std::lock_guard<std::mutex> g(c->rpool_mu);
+        if (!c->rslot_pool.empty()) {
+            RSlot* S = (RSlot*)c->rslot_pool.back();
+            c->rslot_pool.pop_back();
+            S->reset();
+            return S;
+        }
+    }
+    std::unique_ptr<RSlot> S(new RSlot);
+    S->ctx = c;
+    if (hipEventCreateWithFlags(&S->ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&S->ev2, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return S.release();
+}
+void rslot_give(RSlot* S) {  // (nothing of the slot in flight)
+    if (!S) return;
+    s3hc_ctx* c = S->ctx;
+    {
+        std::lock_guard<std::mutex> g(c->rpool_mu);
+        if (c->rslot_pool.size() < kReaderPoolMax) {
+            c->rslot_pool.push_back(S);
+            return;
+        }
+    }
+    delete S;
+}
+hipStream_t rqueue_take(s3hc_ctx* c) {  // (device current)
+    {
+        std::lock_guard<std::mutex> g(c->rpool_mu);
+        if (!c->rqueue_pool.empty()) {
+            hipStream_t q = c->rqueue_pool.back();
+            c->rqueue_pool.pop_back();
+            return q;
+        }
+    }
+    hipStream_t q = nullptr;
+    return hipStreamCreateWithFlags(&q, hipStreamNonBlocking) == hipSuccess ? q : nullptr;
+}
+void rqueue_give(s3hc_ctx* c, hipStream_t q) {  // (q synchronised)
+    if (!q) return;
+    {
+        std::lock_guard<std::mutex> g(c->rpool_mu);
+        if (c->rqueue_pool.size() < kReaderPoolMax) {
+            c->rqueue_pool.push_back(q);
+            return;
+        }
+    }
+    (void)hipSetDevice(c->device);
+    (void)hipStreamDestroy(q);
+}
 }  // namespace
+static void reader_pool_release(s3hc_ctx* c) {
+    std::lock_guard<std::mutex> g(c->rpool_mu);
+    for (void* p : c->rslot_pool) delete (RSlot*)p;
+    c->rslot_pool.clear();
+    (void)hipSetDevice(c->device);
+    for (hipStream_t q : c->rqueue_pool) (void)hipStreamDestroy(q);
+    c->rqueue_pool.clear();
+}
 
 // The frame results a batch's decode wrote (lengths, statuses) decide the copies out of device
 // memory, so they are checked before any copy: every status must be one the decoders assign, every
@@ -2122,13 +2203,14 @@ struct RTimer {
 };
 
 struct s3hc_reader {
+    ~s3hc_reader();
     s3hc_ctx* ctx;                  // ctxs[0]
     std::vector<s3hc_ctx*> ctxs;    // the reader's devices (queue q on ctxs[q % ctxs.size()])
     ReaderTrace tr;
     size_t batch_bytes;
     size_t batch_max;           // batch limit while earlier batches are in flight (>= batch_bytes)
     std::vector<hipStream_t> queues;  // `depth` HIP queues per device
-    std::vector<RSlot> slots;         // S3HC_READER_SLOTS batches per queue (default 1; more queue
+    std::vector<RSlot*> slots;        // S3HC_READER_SLOTS batches per queue (default 1; more queue
                                       // a queue's next batch behind its running one: measured slower)
     std::vector<int> inflight;  // slot indices in stream order (head may be ready / being read)
     std::vector<uint8_t, NoInitAlloc<uint8_t>> in;  // buffered input (grown without zero-fill); undecoded bytes start at in_head (a frame boundary)
@@ -2295,7 +2377,7 @@ static int reader_pump(s3hc_reader* r) {
         int s = -1;
         for (int i = 0; i < (int)r->slots.size(); ++i)
             if (!used[i] && (s < 0 || busy[(size_t)i % r->queues.size()] < busy[(size_t)s % r->queues.size()])) s = i;
-        int rc = reader_submit(r, r->slots[s], W, k);
+        int rc = reader_submit(r, *r->slots[s], W, k);
         if (rc) return rc;
         r->inflight.push_back(s);
     }
@@ -2353,7 +2435,7 @@ static bool reader_copy_done(RSlot& S) { return S.state == 1 && (S.covered || hi
 // Queue the D2H of every batch whose decode has finished (any order: separate queues).
 static int reader_advance(s3hc_reader* r) {
     for (int i : r->inflight) {
-        RSlot& S = r->slots[i];
+        RSlot& S = *r->slots[i];
         if (S.state == 0 && hipSetDevice(S.ctx->device) == hipSuccess && hipEventQuery(S.ev) == hipSuccess) {
             int rc = reader_issue_copy(S, r->tr);
             if (rc) return rc;
@@ -2364,7 +2446,7 @@ static int reader_advance(s3hc_reader* r) {
 
 // Wait until the oldest batch's decoded bytes are in its pinned output buffer.
 static int reader_complete(s3hc_reader* r) {
-    RSlot& S = r->slots[r->inflight.front()];
+    RSlot& S = *r->slots[r->inflight.front()];
     HIPCHK(hipSetDevice(S.ctx->device));
     if (S.state == 0) {
         {
@@ -2386,7 +2468,7 @@ static int reader_complete(s3hc_reader* r) {
         r->error = S.err;
         r->error_msg = "frame decode failed";
         for (size_t k = 1; k < r->inflight.size(); ++k) {
-            RSlot& L = r->slots[r->inflight[k]];
+            RSlot& L = *r->slots[r->inflight[k]];
             (void)hipSetDevice(L.ctx->device);
             (void)hipStreamSynchronize(L.st);
             L.state = 0;
@@ -2424,19 +2506,18 @@ static int reader_new(s3hc_ctx* const* ctxs, int nctx, size_t batch_bytes, int d
     const long long per = std::min<long long>(4, std::max<long long>(1, knob(KN_READER_SLOTS)));
     const size_t nq = (size_t)depth * (size_t)nctx;
     r->queues.assign(nq, nullptr);
-    r->slots.resize(nq * (size_t)per);
+    r->slots.assign(nq * (size_t)per, nullptr);
     r->tr.on = knob_on(KN_HOST_TRACE);
     for (size_t q = 0; q < nq; ++q) {
-        HIPCHK(hipSetDevice(ctxs[q % (size_t)nctx]->device));
-        HIPCHK(hipStreamCreateWithFlags(&r->queues[q], hipStreamNonBlocking));
+        s3hc_ctx* c = ctxs[q % (size_t)nctx];
+        HIPCHK(hipSetDevice(c->device));
+        if (!(r->queues[q] = rqueue_take(c))) return fail(S3HC_DEVICE, "reader queue");
     }
     for (size_t i = 0; i < r->slots.size(); ++i) {
-        RSlot& S = r->slots[i];
-        S.ctx = ctxs[(i % nq) % (size_t)nctx];
-        S.st = r->queues[i % nq];
-        HIPCHK(hipSetDevice(S.ctx->device));
-        HIPCHK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&S.ev2, hipEventDisableTiming));
+        s3hc_ctx* c = ctxs[(i % nq) % (size_t)nctx];
+        HIPCHK(hipSetDevice(c->device));
+        if (!(r->slots[i] = rslot_take(c))) return fail(S3HC_DEVICE, "reader slot");
+        r->slots[i]->st = r->queues[i % nq];
     }
     *out = r.release();
     return S3HC_OK;
@@ -2490,8 +2571,8 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
         if (!cap) return S3HC_OK;
         // a ready head batch is delivered without the context lock (the copy is the caller's
         // Bytes::copy_from_slice; concurrent readers must not serialize on it)
-        if (!r->inflight.empty() && r->slots[r->inflight.front()].ready) {
-            RSlot& S = r->slots[r->inflight.front()];
+        if (!r->inflight.empty() && r->slots[r->inflight.front()]->ready) {
+            RSlot& S = *r->slots[r->inflight.front()];
             if (S.out_pos < S.out_len) {
                 RTimer T_(r->tr, ReaderTrace::DELIVER);
                 const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
@@ -2503,8 +2584,8 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
         }
         ReaderLock g(r);
         for (;;) {
-            if (!r->inflight.empty() && r->slots[r->inflight.front()].ready) {
-                RSlot& S = r->slots[r->inflight.front()];
+            if (!r->inflight.empty() && r->slots[r->inflight.front()]->ready) {
+                RSlot& S = *r->slots[r->inflight.front()];
                 if (*n == 0 && S.out_pos < S.out_len) {
                     RTimer T_(r->tr, ReaderTrace::DELIVER);
                     const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
@@ -2541,7 +2622,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
             }
             // the oldest batch is still running: wait for it only when the pipeline is full, the
             // input is finished or it is already done; otherwise ask the caller for more input
-            RSlot& H = r->slots[r->inflight.front()];
+            RSlot& H = *r->slots[r->inflight.front()];
             const bool done = reader_copy_done(H);
             if (!done && r->inflight.size() < r->slots.size() && !r->finished && !r->error) return S3HC_OK;
             int rc = reader_complete(r);
@@ -2550,6 +2631,18 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
     });
 }
 extern "C" uint64_t s3hc_reader_total(const s3hc_reader* r) { return r ? r->total : 0; }
+// Give the queues (synchronised) and slots back to their contexts' pools.
+s3hc_reader::~s3hc_reader() {
+    const size_t nc = ctxs.size();
+    for (size_t q = 0; q < queues.size(); ++q)
+        if (queues[q]) {
+            (void)hipSetDevice(ctxs[q % nc]->device);
+            (void)hipStreamSynchronize(queues[q]);
+        }
+    for (RSlot* S : slots) rslot_give(S);
+    for (size_t q = 0; q < queues.size(); ++q)
+        if (queues[q]) rqueue_give(ctxs[q % nc], queues[q]);
+}
 extern "C" void s3hc_reader_close(s3hc_reader* r) {
     if (!r) return;
     if (r->tr.on) {
@@ -2559,21 +2652,5 @@ extern "C" void s3hc_reader_close(s3hc_reader* r) {
             fprintf(stderr, " %s %.1f", nm[k], r->tr.t[k] / (double)std::max<uint64_t>(1, r->tr.batches));
         fprintf(stderr, "\n");
     }
-    const size_t nc = r->ctxs.size();
-    for (size_t q = 0; q < r->queues.size(); ++q)
-        if (r->queues[q]) {
-            (void)hipSetDevice(r->ctxs[q % nc]->device);
-            (void)hipStreamSynchronize(r->queues[q]);
-        }
-    for (auto& S : r->slots) {
-        if (S.ctx) (void)hipSetDevice(S.ctx->device);
-        if (S.ev) (void)hipEventDestroy(S.ev);
-        if (S.ev2) (void)hipEventDestroy(S.ev2);
-    }
-    for (size_t q = 0; q < r->queues.size(); ++q)
-        if (r->queues[q]) {
-            (void)hipSetDevice(r->ctxs[q % nc]->device);
-            (void)hipStreamDestroy(r->queues[q]);
-        }
     delete r;
 }

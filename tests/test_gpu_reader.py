@@ -122,9 +122,10 @@ def test_reader_output_beyond_speculative_prefix(engine, oracle, item):
 
 @pytest.mark.parametrize("seed", [0, 1, 2, 3])
 def test_reader_corrupt_block_payloads_one_launch_batches(engine, oracle, seed):
-    # batches of 64 KiB frames only: k_djump decodes them, the per-unit decoder takes the blocks its
-    # token index leaves, k_dframe_close closes the frames. Payload bytes of a few frames are flipped: the reader must deliver exactly the frames before the first failing
-    # one (the oracle decodes frame by frame) and then report that frame's status.
+    # batches of 64 KiB frames only: k_djump decodes them and runs the per-unit decoder itself for
+    # the blocks its token index leaves (waves 2-15 leave first), k_dframe_close closes the frames.
+    # Payload bytes of a few frames are flipped: the reader must deliver exactly the frames before
+    # the first failing one (the oracle decodes frame by frame) and then report that frame's status.
     import random
 
     import s3hc_lz4 as S
@@ -230,3 +231,36 @@ def test_reader_many_small_frames_stored_and_corrupt(engine, oracle, poison, cor
                     _drain(r, out)
                 assert e.value.status == want_st
                 assert bytes(out) == bytes(good), (batch, depth)
+
+
+def test_reader_slots_pooled_across_readers(engine, oracle):
+    # Readers of one context reuse each other's slots and queues (a GET opens one reader): a slot
+    # that served 64 KiB frames, reference 1 MiB frames or a failing stream must serve the next
+    # reader exactly (its batch state is cleared, its buffers regrow as needed)
+    import s3hc_lz4 as S
+
+    small = synth.log_text(3 * MiB + 77, 71)
+    big = synth.log_text(5 * MiB + 5, 72)
+    f_small = b"".join(engine.compress_frame(small[i:i + 65536]) for i in range(0, len(small), 65536))
+    f_big = b"".join(oracle.lz4flex_compress_frame(big[i:i + MiB]) for i in range(0, len(big), MiB))
+    bad = bytearray(f_small)
+    bad[-3] ^= 0x40  # content checksum of the last frame
+    for k in range(12):
+        kind = k % 3
+        depth = 1 + k % 4
+        if kind == 0:
+            out, r = _run(engine, f_small, 1 << 20, 256 << 10, depth)
+            assert out == small and r.total == len(small)
+        elif kind == 1:
+            out, r = _run(engine, f_big, 3 << 20, 256 << 10, depth)
+            assert out == big and r.total == len(big)
+        else:
+            r = S.RangeReader(engine, 256 << 10, depth)
+            r.feed(bytes(bad))
+            r.finish()
+            got = bytearray()
+            with pytest.raises(S.CodecError) as e:
+                _drain(r, got)
+            assert e.value.status == S.S3HC_CHECKSUM
+            assert bytes(got) == small[:len(small) // 65536 * 65536]
+        r.close()
