@@ -1424,8 +1424,23 @@ constexpr uint32_t kTbl = 1u << kHashLog;
 #ifndef S3HC_SHORT_GATE  // diagnostic builds: distance-1..4 candidate only without a verified table one
 #define S3HC_SHORT_GATE 0
 #endif
-#ifndef S3HC_LAZY  // diagnostic builds: one-step lazy match selection in the greedy walk
-#define S3HC_LAZY 0
+#ifndef S3HC_LAZY  // lazy match selection (diagnostic builds: 0 = plain greedy)
+#define S3HC_LAZY 1
+#endif
+#ifndef S3HC_PW_STRIDE  // prewarm: every S3HC_PW_STRIDE-th window position is inserted (1, 2 or 4)
+#define S3HC_PW_STRIDE 1
+#endif
+#ifndef S3HC_INS_MASK  // table pass: positions with (P & mask) != 0 are probed but not inserted
+#define S3HC_INS_MASK 0
+#endif
+#ifndef S3HC_TB64  // candidate dwords by 8-byte LDS reads
+#define S3HC_TB64 0
+#endif
+#ifndef S3HC_PS2_INS1  // probe stride 2: only the probed position of a lane is inserted
+#define S3HC_PS2_INS1 0
+#endif
+#ifndef S3HC_ABL  // diagnostic ablations of the match finder's phases (never shipped)
+#define S3HC_ABL 0
 #endif
 #ifndef S3HC_ENC_MINWAVES
 #define S3HC_ENC_MINWAVES 1
@@ -1433,7 +1448,7 @@ constexpr uint32_t kTbl = 1u << kHashLog;
 constexpr uint32_t kSteps = S3HC_STEPS;                     // 64-position steps per sub-block
 constexpr uint32_t kStash = 64 * kSteps / 4;                // hops per sub-block (a hop covers >= 4 bytes)
 #ifndef S3HC_PSTRIDE
-#define S3HC_PSTRIDE 1
+#define S3HC_PSTRIDE 2
 #endif
 constexpr uint32_t kPS = S3HC_PSTRIDE;                      // positions per lane and step: every position is
                                                             // inserted into the table, the first of a lane's
@@ -1476,6 +1491,18 @@ __device__ __forceinline__ uint32_t fwd_len(const uint32_t (&d)[N]) {
     return (m >> 3) + 4u;
 }
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
+#ifndef S3HC_HASH5  // table hash over 5 bytes (4-byte word + the next byte) instead of 4
+#define S3HC_HASH5 1
+#endif
+// Table hash of the 4 bytes v at a position and the byte after them (b5; ignored by the 4-byte hash)
+__device__ __forceinline__ uint32_t hash_pos(uint32_t v, uint32_t b5) {
+#if S3HC_HASH5
+    return (b5 * 0x9E3779u + v * 2654435761u) >> (32 - kHashLog);
+#else
+    (void)b5;
+    return hash4(v);
+#endif
+}
 __device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t l) {
     return (uint64_t)rdl((uint32_t)v, l) | ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32);
 }
@@ -1608,9 +1635,9 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
         for (uint32_t d0 = lane; 4 * d0 < lim; d0 += 64) {
             const uint32_t w0 = dw[d0], w1 = dw[d0 + 1];
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
+            for (uint32_t j = 0; j < 4; j += S3HC_PW_STRIDE) {
                 const uint32_t i = 4 * d0 + j;
-                tbl[i + 4 <= lim ? hash4(__builtin_amdgcn_alignbyte(w1, w0, j)) : kTbl] = (uint16_t)i;
+                tbl[i + 4 <= lim ? hash_pos(__builtin_amdgcn_alignbyte(w1, w0, j), __builtin_amdgcn_ubfe(w1, 8 * j, 8)) : kTbl] = (uint16_t)i;
             }
         }
     }
@@ -1638,22 +1665,28 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             vv[q] = __builtin_amdgcn_alignbyte(w1, w0, sh);
             vm[q] = __builtin_amdgcn_alignbyte(w0, wp, sh);    // bytes [P-4, P)
             vm8[q] = __builtin_amdgcn_alignbyte(wp, wpp, sh);  // bytes [P-8, P-4)
-            const uint32_t h = hash4(vv[q]);
+            const uint32_t h = hash_pos(vv[q], __builtin_amdgcn_ubfe(w1, 8 * sh, 8));
             if (kPS == 1) {
                 cc[q] = tbl[h];
+#if S3HC_INS_MASK
+                if ((P < sb_end) & ((P & S3HC_INS_MASK) == 0)) tbl[h] = (uint16_t)i;  // exec-masked: no sink conflicts
+#else
                 tbl[P < sb_end ? h : kTbl] = (uint16_t)i;
+#endif
             } else {
                 // (i even: sh + 1 <= 3) the lane's second position is inserted after the first; the
                 // two half-waves (64 positions each) read and insert one after the other, so a
                 // probe sees every position before its own 64 (as with one position per lane)
-                const uint32_t h1 = hash4(__builtin_amdgcn_alignbyte(w1, w0, sh + 1));
+                const uint32_t h1 = hash_pos(__builtin_amdgcn_alignbyte(w1, w0, sh + 1), __builtin_amdgcn_ubfe(w1, 8 * (sh + 1), 8));
                 const uint32_t t0 = P < sb_end ? h : kTbl, t1 = P + 1 < sb_end ? h1 : kTbl;
 #pragma unroll
                 for (uint32_t half = 0; half < 2; ++half) {
                     if (((uint32_t)lane >> 5) == half) {
                         cc[q] = tbl[h];
                         tbl[t0] = (uint16_t)i;
+#if !S3HC_PS2_INS1
                         tbl[t1] = (uint16_t)(i + 1);
+#endif
                     }
                     wave_sync();
                 }
@@ -1692,8 +1725,28 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             uint32_t O[kNQ + 1], T[kNQ + 3];
 #pragma unroll
             for (int j = 0; j < kNQ + 1; ++j) O[j] = dw[a + 1 + j];
+#if S3HC_TB64
+            {
+                // the candidate's dwords as 8-byte reads (merged into ds_read2_b64: 16-lane groups
+                // over 32 banks, fewer conflict cycles per dword than ds_read2_b32's 32-lane
+                // groups) from the even dword at or below ta - 1, shifted when ta - 1 is odd
+                const int tb = (int)ta - 1;
+                const uint2* d2 = (const uint2*)(dw + (tb & ~1));
+                const bool par = (tb & 1) != 0;
+                uint32_t Uu[kNQ + 5];
+#pragma unroll
+                for (int k2 = 0; k2 < (kNQ + 5) / 2; ++k2) {
+                    const uint2 u = d2[k2];
+                    Uu[2 * k2] = u.x;
+                    Uu[2 * k2 + 1] = u.y;
+                }
+#pragma unroll
+                for (int j = 0; j < kNQ + 3; ++j) T[j] = par ? Uu[j + 1] : Uu[j];
+            }
+#else
 #pragma unroll
             for (int j = 0; j < kNQ + 3; ++j) T[j] = dw[(int)ta - 1 + j];
+#endif
             uint32_t Q[kNQ + 1];  // Q[k] = bytes [P+4k, P+4k+4)
             Q[0] = v;
 #pragma unroll
@@ -1717,9 +1770,12 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             // the distance-1..4 candidate only where the table has no verified candidate (a run's
             // first positions: inside a run the table candidate lies in the run and measures the
             // same); the step's ballot then fires far less often
-            const bool want_short = valid & (e1 | e2 | e3 | e4) & !gt;
+            bool want_short = valid & (e1 | e2 | e3 | e4) & !gt;
 #else
-            const bool want_short = valid & (e1 | e2 | e3 | e4) & !(gt & (lt >= S3HC_SHORT_MIN));
+            bool want_short = valid & (e1 | e2 | e3 | e4) & !(gt & (lt >= S3HC_SHORT_MIN));
+#endif
+#if S3HC_ABL == 2  // diagnostic ablation: no distance-1..4 candidate
+            want_short = false;
 #endif
             if (S3HC_SHORT_CAND == 1 && __ballot(want_short)) {
                 const uint32_t df = (e1 & (i >= 1)) ? 1u : ((e2 & (i >= 2)) ? 2u : ((e3 & (i >= 3)) ? 3u : ((e4 & (i >= 4)) ? 4u : 0u)));
@@ -1738,7 +1794,17 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             }
             word[q] = dist | ((len - 4) << 16) | (nb << 24);
             flen[q] = len;
+#if S3HC_LAZY
+            // Lazy selection, off the walk's chain: a match is left out of the step's mask when the
+            // next position's match is longer (and it is not a wave-extended one); the walk then
+            // lands on the next one, so a run of growing matches lands on its longest. One literal
+            // buys >= 1 more matched byte: config 2's C/U 0.387 -> 0.379, fewer sequences to decode.
+            const uint32_t fv = (gt | gf) ? len : 0u;
+            const uint32_t fnext = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)fv, 0x130, 0xF, 0xF, false);  // wave_shl:1
+            mm[q] = __ballot((gt | gf) & !((fnext > fv) & (fv < kFwd)));
+#else
             mm[q] = __ballot(gt | gf);
+#endif
             if (q & 1) wave_sync();  // bounds the loads hoisted ahead (VGPR pressure)
         }
         const uint64_t tc1 = PROF_NOW();
@@ -1755,27 +1821,19 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             // per lane: greedy position after taking this lane's match (chunk-relative);
             // 0x1000 marks a match that reached kFwd and needs the wave-wide extension
             const uint32_t nxr = kPS * (uint32_t)lane + flen[q] + (flen[q] == kFwd ? 0x1000u : 0u);
-#if S3HC_LAZY
-            // one-step lazy evaluation: a landing on lane j takes lane j + 1's match instead when
-            // that one is longer (and j's is not a wave-extended one): one literal for >= 2 more
-            // matched bytes; lane j + 1's flen by a wave shift
-            const uint32_t fnext = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)flen[q], 0x130, 0xF, 0xF, false);
-            const bool nxm = ((mm[q] >> (uint32_t)lane) >> 1) & 1ull;
-            const uint64_t lz = __ballot(nxm && flen[q] < kFwd && fnext > flen[q]);
-#endif
             uint32_t r = x > base ? x - base : 0u, rend = 0;
+#if S3HC_ABL == 1  // diagnostic ablation: no serial walk (frames not valid)
+            hm = mm[q] & 0x1111111111111111ull;
+            r = kStepPos;
+            rend = r;
+#endif
             while (r < kStepPos) {
                 // the first probed position at or after r (a probe after r reaches back to it)
                 const uint32_t j0 = (r + kPS - 1u) / kPS;
                 if (j0 >= 64u) break;
                 const uint64_t av = mm[q] & (~0ull << j0);
                 if (!av) break;
-#if S3HC_LAZY
-                uint32_t j = (uint32_t)__builtin_ctzll(av);
-                j += (uint32_t)(lz >> j) & 1u;
-#else
                 const uint32_t j = (uint32_t)__builtin_ctzll(av);
-#endif
                 hm |= 1ull << j;
                 r = rdl(nxr, j);
                 if (r & 0x1000u) {  // long match: wave-wide forward extension
@@ -1824,7 +1882,12 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
         const uint64_t tf0 = PROF_NOW();
         wave_sync();
         {
+#if S3HC_ABL == 4  // diagnostic ablation: stash read once, no record formation
+            const uint32_t H = 0;
+            body += stash[lane].x + stash[lane].y;
+#else
             const uint32_t H = nseq - ns_sb;
+#endif
             uint32_t carry_end = le_sb;
             for (uint32_t g = 0; g < H; g += 64) {
                 const uint32_t idx = g + lane;
@@ -1860,6 +1923,9 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
 #endif
     if (lane == 0) {
         SegSummary S;
+#if S3HC_ABL == 1 || S3HC_ABL == 4  // ablations: the segment is written as literals (safe sizes)
+        nseq = 0;
+#endif
         S.nseq = nseq;
         S.ll0 = ll0;
         S.body = body;
