@@ -1439,6 +1439,9 @@ constexpr uint32_t kTbl = 1u << kHashLog;
 #ifndef S3HC_PS2_INS1  // probe stride 2: only the probed position of a lane is inserted
 #define S3HC_PS2_INS1 0
 #endif
+#ifndef S3HC_WALK_NX  // walk hops along per-lane precomputed next landings
+#define S3HC_WALK_NX 1
+#endif
 #ifndef S3HC_ABL  // diagnostic ablations of the match finder's phases (never shipped)
 #define S3HC_ABL 0
 #endif
@@ -1822,6 +1825,21 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             // 0x1000 marks a match that reached kFwd and needs the wave-wide extension
             const uint32_t nxr = kPS * (uint32_t)lane + flen[q] + (flen[q] == kFwd ? 0x1000u : 0u);
             uint32_t r = x > base ? x - base : 0u, rend = 0;
+#if S3HC_WALK_NX
+            // per lane: the next landing after taking this lane's match when it lies in this step
+            // (its lane, < 64), else 64 (the match leaves the step, or no match follows it here)
+            // or 0x80 (a long match: the walk extends it first). The hops are then one
+            // v_readlane each, lane index to lane index.
+            uint32_t nxl;
+            {
+                const uint64_t mq = mm[q];
+                const uint32_t kk = (kPS * (uint32_t)lane + flen[q] + kPS - 1u) / kPS;
+                const uint64_t rest = kk < 64u ? mq >> kk : 0ull;
+                const uint32_t lo = (uint32_t)rest, hi = (uint32_t)(rest >> 32);
+                const uint32_t tz = lo ? (uint32_t)__builtin_ctz(lo) : 32u + (uint32_t)__builtin_ctz(hi | 0x80000000u);
+                nxl = flen[q] == kFwd ? 0x80u : (rest ? kk + tz : 64u);
+            }
+#endif
 #if S3HC_ABL == 1  // diagnostic ablation: no serial walk (frames not valid)
             hm = mm[q] & 0x1111111111111111ull;
             r = kStepPos;
@@ -1833,8 +1851,18 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
                 if (j0 >= 64u) break;
                 const uint64_t av = mm[q] & (~0ull << j0);
                 if (!av) break;
+#if S3HC_WALK_NX
+                uint32_t j = (uint32_t)__builtin_ctzll(av);
+                for (;;) {
+                    hm |= 1ull << j;
+                    const uint32_t v = rdl(nxl, j);
+                    if (v >= 64u) break;
+                    j = v;
+                }
+#else
                 const uint32_t j = (uint32_t)__builtin_ctzll(av);
                 hm |= 1ull << j;
+#endif
                 r = rdl(nxr, j);
                 if (r & 0x1000u) {  // long match: wave-wide forward extension
                     const uint64_t tx0 = PROF_NOW();
