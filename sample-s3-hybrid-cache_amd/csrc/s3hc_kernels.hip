@@ -1439,9 +1439,6 @@ constexpr uint32_t kTbl = 1u << kHashLog;
 #ifndef S3HC_PS2_INS1  // probe stride 2: only the probed position of a lane is inserted
 #define S3HC_PS2_INS1 0
 #endif
-#ifndef S3HC_WALK_NX  // walk hops along per-lane precomputed next landings
-#define S3HC_WALK_NX 1
-#endif
 #ifndef S3HC_ABL  // diagnostic ablations of the match finder's phases (never shipped)
 #define S3HC_ABL 0
 #endif
@@ -1508,6 +1505,17 @@ __device__ __forceinline__ uint32_t hash_pos(uint32_t v, uint32_t b5) {
 }
 __device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t l) {
     return (uint64_t)rdl((uint32_t)v, l) | ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32);
+}
+
+// The walk's next landing after a match ending at step-relative position np: the first matched
+// lane of the step mask mq probing at or after np, or 64 when there is none in this step
+template <uint32_t kPSt>
+__device__ __forceinline__ uint32_t next_landing(uint64_t mq, uint32_t np) {
+    const uint32_t kk = (np + kPSt - 1u) / kPSt;
+    const uint64_t rest = kk < 64u ? mq >> kk : 0ull;
+    const uint32_t lo = (uint32_t)rest, hi = (uint32_t)(rest >> 32);
+    const uint32_t tz = lo ? (uint32_t)__builtin_ctz(lo) : 32u + (uint32_t)__builtin_ctz(hi | 0x80000000u);
+    return rest ? kk + tz : 64u;
 }
 
 // Stage block bytes [lo, hi) into lds (lds[x - lo]); any alignment. Every lane issues all of
@@ -1821,50 +1829,37 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             const uint32_t base = sb + kStepPos * q;
             if (x >= base + kStepPos || !mm[q]) continue;
             uint64_t hm = 0;
-            // per lane: greedy position after taking this lane's match (chunk-relative);
-            // 0x1000 marks a match that reached kFwd and needs the wave-wide extension
-            const uint32_t nxr = kPS * (uint32_t)lane + flen[q] + (flen[q] == kFwd ? 0x1000u : 0u);
-            uint32_t r = x > base ? x - base : 0u, rend = 0;
-#if S3HC_WALK_NX
-            // per lane: the next landing after taking this lane's match when it lies in this step
-            // (its lane, < 64), else 64 (the match leaves the step, or no match follows it here)
-            // or 0x80 (a long match: the walk extends it first). The hops are then one
-            // v_readlane each, lane index to lane index.
-            uint32_t nxl;
-            {
-                const uint64_t mq = mm[q];
-                const uint32_t kk = (kPS * (uint32_t)lane + flen[q] + kPS - 1u) / kPS;
-                const uint64_t rest = kk < 64u ? mq >> kk : 0ull;
-                const uint32_t lo = (uint32_t)rest, hi = (uint32_t)(rest >> 32);
-                const uint32_t tz = lo ? (uint32_t)__builtin_ctz(lo) : 32u + (uint32_t)__builtin_ctz(hi | 0x80000000u);
-                nxl = flen[q] == kFwd ? 0x80u : (rest ? kk + tz : 64u);
-            }
-#endif
+            const uint64_t mq = mm[q];
+            // per lane: the walk's move after taking this lane's match: the next landing's lane
+            // (< 64) when one lies in this step; else 0x100 | the step-relative position after the
+            // match (it leaves the step, or no match follows it here); 0x80 for a match that
+            // reached kFwd (extended wave-wide first). A hop is one v_readlane, lane to lane.
+            const uint32_t np = kPS * (uint32_t)lane + flen[q];
+            const uint32_t nl = next_landing<kPS>(mq, np);
+            const uint32_t nxl = flen[q] == kFwd ? 0x80u : (nl < 64u ? nl : 0x100u | np);
+            uint32_t r = x > base ? x - base : 0u;  // < kStepPos
+            // the first probed position at or after r (a probe after r reaches back to it)
+            uint32_t j0 = (r + kPS - 1u) / kPS;
+            uint64_t av = j0 < 64u ? mq & (~0ull << j0) : 0ull;
 #if S3HC_ABL == 1  // diagnostic ablation: no serial walk (frames not valid)
-            hm = mm[q] & 0x1111111111111111ull;
+            hm = mq & 0x1111111111111111ull;
             r = kStepPos;
-            rend = r;
+            av = 0;
 #endif
-            while (r < kStepPos) {
-                // the first probed position at or after r (a probe after r reaches back to it)
-                const uint32_t j0 = (r + kPS - 1u) / kPS;
-                if (j0 >= 64u) break;
-                const uint64_t av = mm[q] & (~0ull << j0);
-                if (!av) break;
-#if S3HC_WALK_NX
+            while (av) {
                 uint32_t j = (uint32_t)__builtin_ctzll(av);
+                uint32_t v;
                 for (;;) {
                     hm |= 1ull << j;
-                    const uint32_t v = rdl(nxl, j);
+                    v = rdl(nxl, j);
                     if (v >= 64u) break;
                     j = v;
                 }
-#else
-                const uint32_t j = (uint32_t)__builtin_ctzll(av);
-                hm |= 1ull << j;
-#endif
-                r = rdl(nxr, j);
-                if (r & 0x1000u) {  // long match: wave-wide forward extension
+                if (v & 0x100u) {  // no further landing in this step
+                    r = v & 0xFFu;
+                    break;
+                }
+                {  // long match: wave-wide forward extension
                     const uint64_t tx0 = PROF_NOW();
                     PROF_ADD(epr, 8, 1);
                     const uint32_t wj = rdl(word[q], j);
@@ -1894,7 +1889,8 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
                     r = kPS * j + lenf;
                     PROF_ADD(epr, 2, PROF_NOW() - tx0);
                 }
-                rend = r;
+                j0 = (r + kPS - 1u) / kPS;
+                av = j0 < 64u ? mq & (~0ull << j0) : 0ull;
             }
             x = base + r;
             if (hm) {
@@ -1902,7 +1898,7 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0));
                 const uint32_t hidx = (hm >> lane) & 1ull ? nseq - ns_sb + rank : kStash + ((uint32_t)lane & 7u);
                 stash[hidx] = make_uint2((base + kPS * lane - seg_lo) | (flen[q] << 16), word[q]);
-                last_end = base + rend;
+                last_end = base + r;
                 nseq += (uint32_t)__builtin_popcountll(hm);
             }
         }
