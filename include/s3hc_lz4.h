@@ -183,6 +183,17 @@ int s3hc_decode_dev(s3hc_ctx* ctx, s3hc_plan* plan, const uint8_t* d_src, uint8_
                     uint32_t* d_out_len, int32_t* d_status, void* stream);
 void s3hc_plan_free(s3hc_plan* plan);
 
+/* Match-finder mode of every GPU encode issued on ctx (s3hc_encode_dev, host-buffer encodes, writers
+ * and aggregators on ctx). Frames of either mode are valid lz4_flex frames and decode to the same
+ * bytes; only the compressed size and the encode time differ. S3HC_ENC_FAST (default): one probe per
+ * two positions, every position in the table (config 2: C/U 0.391). S3HC_ENC_SMALL: a probe at every
+ * position, odd positions left out of the table, lazy selection (config 2: C/U 0.375, the match
+ * finder ~35 % slower). Returns S3HC_INVALID_ARG for other values; get returns -1 for NULL. */
+#define S3HC_ENC_FAST 0
+#define S3HC_ENC_SMALL 1
+int s3hc_set_encode_mode(s3hc_ctx* ctx, int mode);
+int s3hc_get_encode_mode(const s3hc_ctx* ctx);
+
 /* Per-kernel timing for roofline accounting: with timing on, the phases of every *_dev launch are
  * bracketed by HIP events on its stream (no host sync; adjacent phases share their boundary
  * event). s3hc_timing_collect resolves them into per-name totals: s3hc_last_kernel_ms = summed

@@ -1427,18 +1427,6 @@ constexpr uint32_t kTbl = 1u << kHashLog;
 #ifndef S3HC_LAZY  // lazy match selection (diagnostic builds: 0 = plain greedy)
 #define S3HC_LAZY 1
 #endif
-#ifndef S3HC_PW_STRIDE  // prewarm: every S3HC_PW_STRIDE-th window position is inserted (1, 2 or 4)
-#define S3HC_PW_STRIDE 1
-#endif
-#ifndef S3HC_INS_MASK  // table pass: positions with (P & mask) != 0 are probed but not inserted
-#define S3HC_INS_MASK 0
-#endif
-#ifndef S3HC_TB64  // candidate dwords by 8-byte LDS reads
-#define S3HC_TB64 0
-#endif
-#ifndef S3HC_PS2_INS1  // probe stride 2: only the probed position of a lane is inserted
-#define S3HC_PS2_INS1 0
-#endif
 #ifndef S3HC_ABL  // diagnostic ablations of the match finder's phases (never shipped)
 #define S3HC_ABL 0
 #endif
@@ -1447,16 +1435,13 @@ constexpr uint32_t kTbl = 1u << kHashLog;
 #endif
 constexpr uint32_t kSteps = S3HC_STEPS;                     // 64-position steps per sub-block
 constexpr uint32_t kStash = 64 * kSteps / 4;                // hops per sub-block (a hop covers >= 4 bytes)
-#ifndef S3HC_PSTRIDE
-#define S3HC_PSTRIDE 2
-#endif
-constexpr uint32_t kPS = S3HC_PSTRIDE;                      // positions per lane and step: every position is
-                                                            // inserted into the table, the first of a lane's
-                                                            // kPS is probed (a match starting at one of the
-                                                            // others is found by the backward extension)
-constexpr uint32_t kStepPos = 64 * kPS;                     // positions of one step
-constexpr uint32_t kPSteps = kSteps / kPS;                  // steps of a sub-block (its 64 x kSteps positions)
-static_assert(kPS == 1 || kPS == 2, "probe stride 1 or 2");
+// Encoder modes (s3hc_set_encode_mode): the match finder is instantiated per mode.
+//   kPS  positions per lane and step: every position is inserted into the table, the first of a
+//        lane's kPS is probed (a match starting at one of the others is found by the backward
+//        extension of the next probe)
+//   kIns positions with (P & kIns) != 0 are probed but not inserted (fewer entries overwritten:
+//        a better ratio with lazy selection)
+//   fast  (default): kPS 2, kIns 0;   small: kPS 1, kIns 1
 #ifndef S3HC_FWD_DW
 #define S3HC_FWD_DW 5
 #endif
@@ -1491,20 +1476,9 @@ __device__ __forceinline__ uint32_t fwd_len(const uint32_t (&d)[N]) {
     return (m >> 3) + 4u;
 }
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
-#ifndef S3HC_HASH5  // table hash over 5 bytes (4-byte word + the next byte) instead of 4
-#define S3HC_HASH5 1
-#endif
-// Table hash of the 4 bytes v at a position and the byte after them (b5; ignored by the 4-byte hash)
+// Table hash of the 4 bytes v at a position and the byte after them (b5): a 5-byte hash
 __device__ __forceinline__ uint32_t hash_pos(uint32_t v, uint32_t b5) {
-#if S3HC_HASH5
     return (b5 * 0x9E3779u + v * 2654435761u) >> (32 - kHashLog);
-#else
-    (void)b5;
-    return hash4(v);
-#endif
-}
-__device__ __forceinline__ uint64_t rdl64(uint64_t v, uint32_t l) {
-    return (uint64_t)rdl((uint32_t)v, l) | ((uint64_t)rdl((uint32_t)(v >> 32), l) << 32);
 }
 
 // The walk's next landing after a match ending at step-relative position np: the first matched
@@ -1579,6 +1553,7 @@ __device__ void stage_in(const uint8_t* blk, uint32_t lo, uint32_t hi, uint8_t* 
 #else
 #define S3HC_ENC_WPE_ATTR
 #endif
+template <uint32_t kPS, uint32_t kIns>
 __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATTR void k_enc_parse(const uint8_t* __restrict__ src,
                                                               const EncBlock* __restrict__ blocks,
                                                               const uint2* __restrict__ groups, uint32_t ngroups,
@@ -1587,6 +1562,9 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
                                                               uint32_t* __restrict__ fhash, uint2* __restrict__ recs,
                                                               SegSummary* __restrict__ summ) {
     using namespace enc;
+    static_assert(kPS == 1 || kPS == 2, "probe stride 1 or 2");
+    constexpr uint32_t kStepPos = 64 * kPS;                     // positions of one step
+    constexpr uint32_t kPSteps = kSteps / kPS;                  // steps of a sub-block (64 x kSteps positions)
     __shared__ __attribute__((aligned(16))) uint8_t inb_raw[kGIn];
     __shared__ __attribute__((aligned(16))) uint16_t tbl_all[kGroupSegs][kTbl + 8];  // slot kTbl: sink
     __shared__ __attribute__((aligned(16))) uint2 stash_all[kGroupSegs][kStash + 8];  // hops of a sub-block (+ sink)
@@ -1646,7 +1624,7 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
         for (uint32_t d0 = lane; 4 * d0 < lim; d0 += 64) {
             const uint32_t w0 = dw[d0], w1 = dw[d0 + 1];
 #pragma unroll
-            for (uint32_t j = 0; j < 4; j += S3HC_PW_STRIDE) {
+            for (uint32_t j = 0; j < 4; ++j) {
                 const uint32_t i = 4 * d0 + j;
                 tbl[i + 4 <= lim ? hash_pos(__builtin_amdgcn_alignbyte(w1, w0, j), __builtin_amdgcn_ubfe(w1, 8 * j, 8)) : kTbl] = (uint16_t)i;
             }
@@ -1679,11 +1657,11 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             const uint32_t h = hash_pos(vv[q], __builtin_amdgcn_ubfe(w1, 8 * sh, 8));
             if (kPS == 1) {
                 cc[q] = tbl[h];
-#if S3HC_INS_MASK
-                if ((P < sb_end) & ((P & S3HC_INS_MASK) == 0)) tbl[h] = (uint16_t)i;  // exec-masked: no sink conflicts
-#else
-                tbl[P < sb_end ? h : kTbl] = (uint16_t)i;
-#endif
+                if constexpr (kIns != 0) {
+                    if ((P < sb_end) & ((P & kIns) == 0)) tbl[h] = (uint16_t)i;  // exec-masked: no sink conflicts
+                } else {
+                    tbl[P < sb_end ? h : kTbl] = (uint16_t)i;
+                }
             } else {
                 // (i even: sh + 1 <= 3) the lane's second position is inserted after the first; the
                 // two half-waves (64 positions each) read and insert one after the other, so a
@@ -1695,9 +1673,7 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
                     if (((uint32_t)lane >> 5) == half) {
                         cc[q] = tbl[h];
                         tbl[t0] = (uint16_t)i;
-#if !S3HC_PS2_INS1
                         tbl[t1] = (uint16_t)(i + 1);
-#endif
                     }
                     wave_sync();
                 }
@@ -1736,28 +1712,8 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             uint32_t O[kNQ + 1], T[kNQ + 3];
 #pragma unroll
             for (int j = 0; j < kNQ + 1; ++j) O[j] = dw[a + 1 + j];
-#if S3HC_TB64
-            {
-                // the candidate's dwords as 8-byte reads (merged into ds_read2_b64: 16-lane groups
-                // over 32 banks, fewer conflict cycles per dword than ds_read2_b32's 32-lane
-                // groups) from the even dword at or below ta - 1, shifted when ta - 1 is odd
-                const int tb = (int)ta - 1;
-                const uint2* d2 = (const uint2*)(dw + (tb & ~1));
-                const bool par = (tb & 1) != 0;
-                uint32_t Uu[kNQ + 5];
-#pragma unroll
-                for (int k2 = 0; k2 < (kNQ + 5) / 2; ++k2) {
-                    const uint2 u = d2[k2];
-                    Uu[2 * k2] = u.x;
-                    Uu[2 * k2 + 1] = u.y;
-                }
-#pragma unroll
-                for (int j = 0; j < kNQ + 3; ++j) T[j] = par ? Uu[j + 1] : Uu[j];
-            }
-#else
 #pragma unroll
             for (int j = 0; j < kNQ + 3; ++j) T[j] = dw[(int)ta - 1 + j];
-#endif
             uint32_t Q[kNQ + 1];  // Q[k] = bytes [P+4k, P+4k+4)
             Q[0] = v;
 #pragma unroll
@@ -2495,11 +2451,15 @@ hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock*
 }
 hipError_t launch_enc_parse(const uint8_t* src, const EncBlock* blocks, const uint2* groups, uint32_t ngroups,
                             const uint64_t* fsrc_off, const uint32_t* fsrc_len, uint32_t nframes, uint32_t* fhash,
-                            uint2* recs, SegSummary* summ, hipStream_t st) {
+                            uint2* recs, SegSummary* summ, int mode, hipStream_t st) {
     const uint32_t nxx = cdiv((uint64_t)nframes * 4, enc::kGThreads);
     if (!ngroups && !nxx) return hipSuccess;
-    hipLaunchKernelGGL(k_enc_parse, dim3(nxx + ngroups), dim3(enc::kGThreads), 0, st, src, blocks, groups, ngroups,
-                       nxx, fsrc_off, fsrc_len, nframes, fhash, recs, summ);
+    if (mode == 1)  // S3HC_ENC_SMALL
+        hipLaunchKernelGGL((k_enc_parse<1, 1>), dim3(nxx + ngroups), dim3(enc::kGThreads), 0, st, src, blocks, groups,
+                           ngroups, nxx, fsrc_off, fsrc_len, nframes, fhash, recs, summ);
+    else
+        hipLaunchKernelGGL((k_enc_parse<2, 0>), dim3(nxx + ngroups), dim3(enc::kGThreads), 0, st, src, blocks, groups,
+                           ngroups, nxx, fsrc_off, fsrc_len, nframes, fhash, recs, summ);
     return hipGetLastError();
 }
 hipError_t launch_enc_sizes(const EncBlock* blocks, uint32_t nblocks, const SegSummary* summ, SegPlace* place,

@@ -46,7 +46,7 @@ hipError_t launch_lb_parse(const LbArgs&, const uint8_t*, const DecBlock*, const
                            uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_lb_exec(const LbArgs&, const uint8_t*, uint8_t*, uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_enc_parse(const uint8_t*, const EncBlock*, const uint2*, uint32_t, const uint64_t*, const uint32_t*,
-                            uint32_t, uint32_t*, uint2*, SegSummary*, hipStream_t);
+                            uint32_t, uint32_t*, uint2*, SegSummary*, int, hipStream_t);
 hipError_t launch_enc_sizes(const EncBlock*, uint32_t, const SegSummary*, SegPlace*, uint32_t*, uint32_t*,
                             uint32_t*, hipStream_t);
 hipError_t launch_scan(const uint32_t*, uint32_t, uint64_t*, uint64_t*, hipStream_t);
@@ -626,6 +626,7 @@ struct s3hc_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     int timing = 0;  // 0 off, 1 every phase, 2 coarse (enc_parse, dec_all)
+    int enc_mode = S3HC_ENC_FAST;  // match-finder mode of this context's encodes
     std::map<std::string, float> kernel_ms;
     std::map<std::string, int> kernel_n;
     std::vector<TimedSpan> pending;
@@ -818,7 +819,7 @@ static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t
     T.begin("enc_parse");
     HIPCHK(launch_enc_parse(d_src, P->d_blocks.as<EncBlock>(), P->d_groups.as<uint2>(), (uint32_t)P->groups.size(),
                             P->d_frame_src_off.as<uint64_t>(), P->d_frame_src_len.as<uint32_t>(), nf,
-                            P->d_frame_hash.as<uint32_t>(), P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), st));
+                            P->d_frame_hash.as<uint32_t>(), P->d_recs.as<uint2>(), P->d_summ.as<SegSummary>(), ctx->enc_mode, st));
     T.end();
     const bool fine = T.fine();
     if (fine) T.begin("enc_sizes");
@@ -946,6 +947,13 @@ extern "C" void s3hc_destroy(s3hc_ctx* ctx) {
     reader_pool_release(ctx);
     delete ctx;
 }
+extern "C" int s3hc_set_encode_mode(s3hc_ctx* ctx, int mode) {
+    if (!ctx || (mode != S3HC_ENC_FAST && mode != S3HC_ENC_SMALL)) return fail(S3HC_INVALID_ARG, "bad arguments");
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->enc_mode = mode;
+    return S3HC_OK;
+}
+extern "C" int s3hc_get_encode_mode(const s3hc_ctx* ctx) { return ctx ? ctx->enc_mode : -1; }
 extern "C" void s3hc_set_timing(s3hc_ctx* ctx, int enabled) {
     if (ctx) ctx->timing = enabled == 2 ? 2 : (enabled != 0 ? 1 : 0);
 }

@@ -22,6 +22,7 @@ S3HC_OK, S3HC_CORRUPT, S3HC_CHECKSUM, S3HC_DST_TOO_SMALL = 0, 1, 2, 3
 S3HC_UNSUPPORTED, S3HC_DEVICE, S3HC_INVALID_ARG = 4, 5, 6
 STATUS_NAMES = {0: "OK", 1: "CORRUPT", 2: "CHECKSUM", 3: "DST_TOO_SMALL", 4: "UNSUPPORTED", 5: "DEVICE", 6: "INVALID_ARG"}
 BLK_AUTO_LZ4FLEX, BLK_64K_PER_FRAME, BLK_LZ4FLEX_COMPAT = 0, 1, 2
+ENC_FAST, ENC_SMALL = 0, 1  # match-finder modes (s3hc_set_encode_mode)
 ALG_LZ4, ALG_NONE = 0, 1
 
 
@@ -83,6 +84,8 @@ def _load():
         "s3hc_plan_free": (None, [vp]),
         "s3hc_last_kernel_ms": (ctypes.c_float, [vp, ctypes.c_char_p]),
         "s3hc_set_timing": (None, [vp, i32]),
+        "s3hc_set_encode_mode": (i32, [vp, i32]),
+        "s3hc_get_encode_mode": (i32, [vp]),
         "s3hc_timing_collect": (i32, [vp]),
         "s3hc_timing_reset": (None, [vp]),
         "s3hc_kernel_count": (i32, [vp, ctypes.c_char_p]),
@@ -310,6 +313,14 @@ class Engine:
 
     def stream(self) -> "FrameStream":
         return FrameStream(self)
+
+    # ---- match-finder mode of this engine's encodes (frames decode the same either way)
+    def set_encode_mode(self, mode: int):
+        _check(lib.s3hc_set_encode_mode(self.h, mode))
+
+    @property
+    def encode_mode(self) -> int:
+        return lib.s3hc_get_encode_mode(self.h)
 
     # ---- timing of the last *_dev call
     def set_timing(self, on, coarse: bool = False):

@@ -20,9 +20,11 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--tag", default=os.path.basename(os.environ.get("S3HC_LIB_PATH", "base")))
+    ap.add_argument("--mode", type=int, default=0, help="encode mode: 0 fast, 1 small")
     a = ap.parse_args()
     nb, block = 4096, 65536
     eng = S.Engine(0)
+    eng.set_encode_mode(a.mode)
     data = synth.log_text(nb * block, synth.SEED_BASE + 1)
     offs = [i * block for i in range(nb)]
     d_src = eng.upload(data)
@@ -39,7 +41,7 @@ def main():
     t = eng.timing()
     eng.set_timing(False)
     ilen = d_ilen.u32(nb)
-    out = {"tag": a.tag, "ratio": round(sum(ilen) / (nb * block), 4)}
+    out = {"tag": a.tag, "mode": a.mode, "ratio": round(sum(ilen) / (nb * block), 4)}
     out.update({k: round(v[0] / v[1], 4) for k, v in t.items() if k.startswith("enc")})
     if a.check:
         d_out = eng.alloc(nb * block)
