@@ -1421,11 +1421,17 @@ constexpr uint32_t kTbl = 1u << kHashLog;
 #ifndef S3HC_STEPS
 #define S3HC_STEPS 8
 #endif
-#ifndef S3HC_SHORT_GATE  // diagnostic builds: distance-1..4 candidate only without a verified table one
-#define S3HC_SHORT_GATE 0
+#ifndef S3HC_SHORT_GATE  // distance-1..4 candidate only without a verified table one (0: also under a short one)
+#define S3HC_SHORT_GATE 1
 #endif
 #ifndef S3HC_LAZY  // lazy match selection (diagnostic builds: 0 = plain greedy)
 #define S3HC_LAZY 1
+#endif
+#ifndef S3HC_SALU_PAD
+#define S3HC_SALU_PAD 0
+#endif
+#ifndef S3HC_VALU_PAD
+#define S3HC_VALU_PAD 0
 #endif
 #ifndef S3HC_ABL  // diagnostic ablations of the match finder's phases (never shipped)
 #define S3HC_ABL 0
@@ -1443,7 +1449,7 @@ constexpr uint32_t kStash = 64 * kSteps / 4;                // hops per sub-bloc
 //        a better ratio with lazy selection)
 //   fast  (default): kPS 2, kIns 0;   small: kPS 1, kIns 1
 #ifndef S3HC_FWD_DW
-#define S3HC_FWD_DW 5
+#define S3HC_FWD_DW 6
 #endif
 constexpr int kNQ = S3HC_FWD_DW;                            // dwords compared past the first 4 bytes
 constexpr uint32_t kFwd = 3 + 4 * kNQ;                      // forward bytes measured per probe; a probe
@@ -1771,6 +1777,22 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
             mm[q] = __ballot((gt | gf) & !((fnext > fv) & (fv < kFwd)));
 #else
             mm[q] = __ballot(gt | gf);
+#endif
+#if S3HC_SALU_PAD  // diagnostic: extra scalar instructions per step (scalar-unit sensitivity)
+            {
+                uint32_t d0 = q;
+#pragma unroll
+                for (int k = 0; k < S3HC_SALU_PAD; ++k) asm volatile("s_add_u32 %0, %0, 1" : "+s"(d0));
+                asm volatile("" ::"s"(d0));
+            }
+#endif
+#if S3HC_VALU_PAD  // diagnostic: extra vector instructions per step (VALU sensitivity)
+            {
+                uint32_t d1 = lane;
+#pragma unroll
+                for (int k = 0; k < S3HC_VALU_PAD; ++k) asm volatile("v_add_u32 %0, %0, 1" : "+v"(d1));
+                asm volatile("" ::"v"(d1));
+            }
 #endif
             if (q & 1) wave_sync();  // bounds the loads hoisted ahead (VGPR pressure)
         }
