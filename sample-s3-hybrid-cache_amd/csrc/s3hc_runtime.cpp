@@ -622,6 +622,9 @@ struct TimedSpan {
     bool shared_a;  // a is the previous span's b (returned to the pool once, with that span)
 };
 struct s3hc_ctx {
+    // references: the creator's (s3hc_destroy drops it) and one per reader / aggregator built on
+    // the context, so a context destroyed while they live is freed when the last one closes
+    std::atomic<int> refs{1};
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
@@ -940,12 +943,18 @@ extern "C" int s3hc_device_count(void) {
     int n = 0;
     return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
 }
-extern "C" void s3hc_destroy(s3hc_ctx* ctx) {
-    if (!ctx) return;
+namespace s3hc {
+void ctx_retain(s3hc_ctx* ctx) { ctx->refs.fetch_add(1, std::memory_order_relaxed); }
+void ctx_release(s3hc_ctx* ctx) {
+    if (ctx->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     reader_pool_release(ctx);
     delete ctx;
+}
+}  // namespace s3hc
+extern "C" void s3hc_destroy(s3hc_ctx* ctx) {
+    if (ctx) ctx_release(ctx);
 }
 extern "C" int s3hc_set_encode_mode(s3hc_ctx* ctx, int mode) {
     if (!ctx || (mode != S3HC_ENC_FAST && mode != S3HC_ENC_SMALL)) return fail(S3HC_INVALID_ARG, "bad arguments");
@@ -2508,6 +2517,7 @@ static int reader_new(s3hc_ctx* const* ctxs, int nctx, size_t batch_bytes, int d
     std::unique_ptr<s3hc_reader> r(new s3hc_reader);
     r->ctx = ctxs[0];
     r->ctxs.assign(ctxs, ctxs + nctx);
+    for (auto* c : r->ctxs) ctx_retain(c);  // released by ~s3hc_reader
     ReaderLock lk(r.get());
     r->batch_bytes = batch_bytes;
     r->batch_max = batch_bytes;
@@ -2650,6 +2660,7 @@ s3hc_reader::~s3hc_reader() {
     for (RSlot* S : slots) rslot_give(S);
     for (size_t q = 0; q < queues.size(); ++q)
         if (queues[q]) rqueue_give(ctxs[q % nc], queues[q]);
+    for (auto* c : ctxs) ctx_release(c);  // (the last reference frees a destroyed context)
 }
 extern "C" void s3hc_reader_close(s3hc_reader* r) {
     if (!r) return;

@@ -371,6 +371,10 @@ static void queue_batch(s3hc_writer* w) {
     a->pending.push_back(std::move(b));
 }
 
+namespace s3hc {
+void ctx_retain(s3hc_ctx* ctx);   // s3hc_runtime.cpp: a lane keeps its context alive
+void ctx_release(s3hc_ctx* ctx);
+}  // namespace s3hc
 static void free_lane(Lane& L) {
     s3hc_ctx* ctx = L.ctx;
     Staging& S = L.stg;
@@ -384,6 +388,7 @@ static void free_lane(Lane& L) {
     if (S.d_cout) s3hc_dev_free(ctx, S.d_cout);
     if (L.queue) s3hc_queue_destroy(ctx, L.queue);
     L = Lane();
+    if (ctx) s3hc::ctx_release(ctx);
 }
 
 static int aggregator_new(s3hc_ctx* const* ctxs, int nctx, size_t batch_size, size_t flush_bytes,
@@ -401,6 +406,7 @@ static int aggregator_new(s3hc_ctx* const* ctxs, int nctx, size_t batch_size, si
     a->lanes.resize(nctx);
     for (int i = 0; i < nctx; ++i) {
         a->lanes[i].ctx = ctxs[i];
+        s3hc::ctx_retain(ctxs[i]);  // released by free_lane
         int rc = s3hc_queue_create(ctxs[i], &a->lanes[i].queue);
         if (rc) {
             const std::string m = std::string("queue: ") + s3hc_last_error();

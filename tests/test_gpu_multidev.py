@@ -132,3 +132,33 @@ def test_multi_device_reader_corrupt_frame(engines, oracle):
             out += c
     assert e.value.status == S.S3HC_CHECKSUM
     assert bytes(out) == data[:29 * 65536]
+
+
+def test_context_destroyed_before_reader_and_aggregator(oracle):
+    """s3hc_destroy with a reader and an aggregator still open: they keep the context (reference
+    counted) and work to the end; the last of them frees it (no use of freed memory at close)."""
+    import s3hc_lz4 as S
+
+    e = S.Engine(0)
+    data = synth.log_text(3 * 65536 + 123, 77)
+    frames = b"".join(e.compress_frame(data[i:i + 65536]) for i in range(0, len(data), 65536))
+    rd = S.RangeReader(e, 256 << 10, 3)
+    agg = S.BatchAggregator(e, 65536, flush_batches=4)
+    e.close()
+    rd.feed(frames)
+    rd.finish()
+    out = b""
+    while True:
+        k = rd.read()
+        if not k:
+            break
+        out += k
+    assert out == data
+    w = agg.begin(0, len(data) - 1, True)
+    for i in range(0, len(data), 16_384):
+        w.write(data[i:i + 16_384])
+    f = w.file
+    w.commit()
+    assert oracle.decompress_data(bytes(f)) == data
+    rd.close()
+    agg.close()
