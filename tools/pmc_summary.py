@@ -7,13 +7,22 @@ import sys
 from collections import defaultdict
 
 
+def kernel_key(name):
+    """Base name of a kernel symbol: no return type, namespace, template arguments or parameters
+    ("void s3hc::k_enc_parse<2u, 0u>(...)" -> "k_enc_parse")."""
+    k = name.split("(")[0].split("<")[0].strip()
+    if k.startswith("void "):
+        k = k[5:]
+    return k.replace("s3hc::", "")
+
+
 def summarize(root):
     acc = defaultdict(lambda: defaultdict(list))
     for fn in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
         per = defaultdict(float)
         with open(fn) as fh:
             for row in csv.DictReader(fh):
-                k = row["Kernel_Name"].split("(")[0].replace("s3hc::", "")
+                k = kernel_key(row["Kernel_Name"])
                 per[(row["Dispatch_Id"], k, row["Counter_Name"])] += float(row["Counter_Value"])
         for (d, k, c), v in per.items():
             acc[k][c].append(v)
