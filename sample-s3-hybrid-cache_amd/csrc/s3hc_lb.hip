@@ -104,14 +104,67 @@ namespace {
 
 __device__ __forceinline__ int lane64() { return (int)(threadIdx.x & 63u); }
 
+// DPP lane moves (row_shr inside 16-lane rows, then row_bcast:15 / :31; lanes without a source
+// read 0): wave scans without the LDS round trip of __shfl's ds_bpermute
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t lb_dpp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, 0xF, false);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint64_t lb_dpp(uint64_t x) {
+    return (uint64_t)lb_dpp<CTRL, ROWMASK>((uint32_t)(x >> 32)) << 32 | lb_dpp<CTRL, ROWMASK>((uint32_t)x);
+}
 template <typename T>
-__device__ __forceinline__ T wave_incl_add(T x, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const T y = __shfl_up(x, d);
-        if (lane >= d) x += y;
-    }
+__device__ __forceinline__ T wave_incl_add(T x, int) {
+    x += lb_dpp<0x111, 0xF>(x);
+    x += lb_dpp<0x112, 0xF>(x);
+    x += lb_dpp<0x114, 0xF>(x);
+    x += lb_dpp<0x118, 0xF>(x);
+    x += lb_dpp<0x142, 0xA>(x);
+    x += lb_dpp<0x143, 0xC>(x);
     return x;
+}
+__device__ __forceinline__ uint32_t lb_umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = lb_umax(x, lb_dpp<0x111, 0xF>(x));
+    x = lb_umax(x, lb_dpp<0x112, 0xF>(x));
+    x = lb_umax(x, lb_dpp<0x114, 0xF>(x));
+    x = lb_umax(x, lb_dpp<0x118, 0xF>(x));
+    x = lb_umax(x, lb_dpp<0x142, 0xA>(x));
+    x = lb_umax(x, lb_dpp<0x143, 0xC>(x));
+    return x;
+}
+// Owner scan of a step (k_lb_run, k_lbw_init): thread t holds the 16-bit start marks of bytes
+// 8t .. 8t+7 (0 = no sequence starts there); each byte's owner is the running max of the marks
+// up to it. Every thread of the workgroup calls (one barrier); shm: 16 aligned words.
+__device__ __forceinline__ uint4 lb_owners(const uint4 m4, uint32_t* shm) {
+    const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
+    uint32_t mx = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) mx = lb_umax(mx, lb_umax(mw[k] & 0xFFFFu, mw[k] >> 16));
+    const uint32_t inc = wave_incl_max(mx);
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 63u) shm[w] = inc;
+    __syncthreads();
+    uint32_t cur = lb_dpp<0x138, 0xF>(inc);  // wave_shr:1: the max before this lane (lane 0: 0)
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {  // and before this wave
+        const uint4 v = ((const uint4*)shm)[k];
+        cur = lb_umax(cur, 4u * k < w ? v.x : 0u);
+        cur = lb_umax(cur, 4u * k + 1u < w ? v.y : 0u);
+        cur = lb_umax(cur, 4u * k + 2u < w ? v.z : 0u);
+        cur = lb_umax(cur, 4u * k + 3u < w ? v.w : 0u);
+    }
+    uint32_t ow[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t lo = mw[k] & 0xFFFFu, hi = mw[k] >> 16;
+        cur = lb_umax(cur, lo);
+        const uint32_t o0 = cur;
+        cur = lb_umax(cur, hi);
+        ow[k] = o0 | (cur << 16);
+    }
+    return make_uint4(ow[0], ow[1], ow[2], ow[3]);
 }
 
 // Workgroup exclusive sum (every thread calls; sh holds one entry per wave).
@@ -730,7 +783,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
     __shared__ __attribute__((aligned(16))) uint4 sq[kMaxSeqS];
     __shared__ uint16_t so[kMaxSeqS];
     __shared__ uint32_t rf[kLbMaxSteps + 1];
-    __shared__ uint32_t shm[16];
+    __shared__ __attribute__((aligned(16))) uint32_t shm[16];
     __shared__ uint32_t jflag[3];
     const uint32_t i = blockIdx.x;
     if (i >= A.ctl->nlb || A.lb_stat[i] != S3HC_OK) return;
@@ -832,39 +885,10 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         LB_T(0);
         LB_ADD(7, 1);
         // owner of each byte: running max of the start marks (thread t: bytes 8t .. 8t+7)
-        const uint4 m4 = dec ? ((const uint4*)marks)[t] : make_uint4(0, 0, 0, 0);
-        const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
-        uint32_t mx = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t lo = mw[k] & 0xFFFFu, hi = mw[k] >> 16;
-            mx = lo > mx ? lo : mx;
-            mx = hi > mx ? hi : mx;
-        }
-        uint32_t inc = mx;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(inc, d);
-            if (lane >= d) inc = y > inc ? y : inc;
-        }
-        if (lane == 63) shm[t >> 6] = inc;
-        __syncthreads();
-        uint32_t cur = __shfl_up(inc, 1);
-        if (lane == 0) cur = 0;
-        for (uint32_t w = 0; w < (t >> 6); ++w) cur = shm[w] > cur ? shm[w] : cur;
-        if (dec) {
-            // owners written over the marks (then read with the interleaved byte mapping)
-            uint32_t ow[4];
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t lo = mw[k] & 0xFFFFu, hi = mw[k] >> 16;
-                cur = lo > cur ? lo : cur;
-                const uint32_t o0 = cur;
-                cur = hi > cur ? hi : cur;
-                ow[k] = o0 | (cur << 16);
-            }
-            ((uint4*)marks)[t] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-        }
+        // (owners written over the marks, then read with the interleaved byte mapping; the
+        // hashing wave's marks are zero)
+        const uint4 own = lb_owners(dec ? ((const uint4*)marks)[t] : make_uint4(0, 0, 0, 0), shm);
+        if (dec) ((uint4*)marks)[t] = own;
         __syncthreads();
         // (a hashing wave more than 3 steps behind catches up here: the ring keeps 8)
         LB_HASH(R, R - 16u * hs > 3u * kLbStep ? (R - 16u * hs - 2u * kLbStep) / 16u
@@ -1117,13 +1141,12 @@ __global__ __launch_bounds__(960) void k_lbw_init(const uint8_t* __restrict__ sr
     __shared__ __attribute__((aligned(16))) uint32_t sqp[kMaxSeqS * 4];  // the tile's sequences, then its pointers
     __shared__ uint16_t so[kMaxSeqS];
     __shared__ __attribute__((aligned(16))) uint8_t val[kLbStep];
-    __shared__ uint32_t shm[16];
+    __shared__ __attribute__((aligned(16))) uint32_t shm[16];
     __shared__ uint32_t jflag[3];
     static_assert(kLbStep <= kMaxSeqS * 4, "pointers fit the sequence table's space");
     uint4* sq = (uint4*)sqp;
     uint32_t* ptr = sqp;
     const uint32_t t = threadIdx.x;
-    const int lane = lane64();
     const uint32_t ntiles = A.ctl->ntiles, nlb = A.ctl->nlb;
     for (uint32_t T = blockIdx.x; T < ntiles; T += gridDim.x) {
         const uint32_t i = lbw_block(A, nlb, T);
@@ -1148,38 +1171,8 @@ __global__ __launch_bounds__(960) void k_lbw_init(const uint8_t* __restrict__ sr
         }
         __syncthreads();
         // owner of each byte: running max of the start marks (thread t: bytes 8t .. 8t+7)
-        const uint4 m4 = ((const uint4*)marks)[t];
-        const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
-        uint32_t mx = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t lo = mw[k] & 0xFFFFu, hi = mw[k] >> 16;
-            mx = lo > mx ? lo : mx;
-            mx = hi > mx ? hi : mx;
-        }
-        uint32_t inc = mx;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(inc, d);
-            if (lane >= d) inc = y > inc ? y : inc;
-        }
-        if (lane == 63) shm[t >> 6] = inc;
-        __syncthreads();
-        uint32_t cur = __shfl_up(inc, 1);
-        if (lane == 0) cur = 0;
-        for (uint32_t w = 0; w < (t >> 6); ++w) cur = shm[w] > cur ? shm[w] : cur;
-        {
-            uint32_t ow[4];
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t lo = mw[k] & 0xFFFFu, hi = mw[k] >> 16;
-                cur = lo > cur ? lo : cur;
-                const uint32_t o0 = cur;
-                cur = hi > cur ? hi : cur;
-                ow[k] = o0 | (cur << 16);
-            }
-            ((uint4*)marks)[t] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-        }
+        const uint4 own = lb_owners(((const uint4*)marks)[t], shm);
+        ((uint4*)marks)[t] = own;
         __syncthreads();
         // classify (thread t: bytes t + kXT*j): literal (input address) or match source, taken in
         // the first period of an overlapping copy; sources inside the tile become LDS pointers,
