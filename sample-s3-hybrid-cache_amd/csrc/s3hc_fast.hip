@@ -199,16 +199,22 @@ __device__ __forceinline__ Tok hop2(const uint8_t* st, uint32_t mis, uint32_t p,
     return T;
 }
 
+// inclusive wave sum by DPP row shifts and row broadcasts (lanes without a source read 0; no
+// ds_bpermute round trip)
+__device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+    return x;
+}
 // exclusive scan over the NW waves of a workgroup; *total = sum
 template <uint32_t NW>
 __device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total) {
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-        if (lane >= d) x += y;
-    }
+    const uint32_t x = wave_incl_sum_dpp(v);
     if (lane == 63) scratch[w] = x;
     __syncthreads();
     uint32_t before = 0, all = 0;
@@ -227,15 +233,7 @@ template <uint32_t NW>
 __device__ __forceinline__ void wg_excl_scan2(uint32_t v, uint32_t u, uint32_t* scratch, uint32_t* ev, uint32_t* eu,
                                               uint32_t* tv, uint32_t* tu) {
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
-    uint32_t x = v, y = u;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t a = (uint32_t)__shfl_up((int)x, d, 64), b = (uint32_t)__shfl_up((int)y, d, 64);
-        if (lane >= d) {
-            x += a;
-            y += b;
-        }
-    }
+    const uint32_t x = wave_incl_sum_dpp(v), y = wave_incl_sum_dpp(u);
     if (lane == 63) {
         scratch[2 * w] = x;
         scratch[2 * w + 1] = y;

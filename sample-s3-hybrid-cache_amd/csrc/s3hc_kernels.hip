@@ -106,6 +106,19 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
     return x;
 }
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int) { return wave_incl_sum(v) - v; }
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint64_t dpp0_64(uint64_t x) {
+    return (uint64_t)dpp0<CTRL, ROWMASK>((uint32_t)(x >> 32)) << 32 | dpp0<CTRL, ROWMASK>((uint32_t)x);
+}
+__device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t x) {
+    x += dpp0_64<0x111, 0xF>(x);
+    x += dpp0_64<0x112, 0xF>(x);
+    x += dpp0_64<0x114, 0xF>(x);
+    x += dpp0_64<0x118, 0xF>(x);
+    x += dpp0_64<0x142, 0xA>(x);
+    x += dpp0_64<0x143, 0xC>(x);
+    return x;
+}
 
 // Wave-cooperative copy of n bytes global -> global, any alignment of either side.
 // Loads for up to 4 KiB are issued before the stores.
@@ -2187,12 +2200,7 @@ __device__ __forceinline__ void scan_u32_u64(const uint32_t* __restrict__ in, ui
             v[k] = i < n ? in[i] : 0;
             loc += v[k];
         }
-        uint64_t x = loc;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            uint64_t y = __shfl_up(x, d);
-            if (lane >= d) x += y;
-        }
+        const uint64_t x = wave_incl_sum64(loc);
         if (lane == 63) wsum[wv] = x;
         __syncthreads();
         uint64_t wpre = 0;
