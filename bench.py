@@ -208,6 +208,32 @@ def cpu_baseline(data_chunk: bytes, block: int, seconds: float):
     if threads < affinity:  # the same run oversubscribed to every thread of the affinity mask
         n, w, _, _ = run(affinity, seconds)
         over = round(n * block / w / GiB, 4)
+    # a labelled third-party C reference: liblz4's raw block API on the same
+    # blocks and threads — not the proxy's codec (no frames, no content checksum, its own parser)
+    lz4 = None
+    L.or_bench_blocks_liblz4.restype = ctypes.c_int
+    L.or_bench_blocks_liblz4.argtypes = L.or_bench_blocks.argtypes
+    probe = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    if L.or_bench_blocks_liblz4(buf, nb, block, 1, 0.0, 1, *[ctypes.byref(x) for x in probe]) == 0:
+        def run_lz4(th, secs):
+            done, wall, es, ds = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+            rc = L.or_bench_blocks_liblz4(buf, nb, block, th, secs, 0, ctypes.byref(done), ctypes.byref(wall),
+                                          ctypes.byref(es), ctypes.byref(ds))
+            assert rc == 0, f"liblz4 baseline round trip failed ({rc})"
+            return done.value, wall.value, es.value, ds.value
+        ln1, lw1, le1, ld1 = run_lz4(1, seconds)
+        lr = []
+        for _ in range(3):
+            n, w, _, _ = run_lz4(threads, seconds)
+            lr.append(n * block / w / GiB)
+        lz4 = {"value": round(statistics.median(lr), 4), "unit": "GiB/s", "cores": threads,
+               "kind": "third-party C LZ4 (liblz4 1.9.3), not the proxy's codec",
+               "sample": "LZ4_compress_default + LZ4_decompress_safe per 64 KiB block of the same batch (raw "
+                         "blocks: no frame, no xxh32), same threads and ranges; median of 3 runs",
+               "runs_gibps": [round(x, 4) for x in lr],
+               "single_thread_gibps": round(ln1 * block / lw1 / GiB, 4),
+               "single_thread_encode_gibps": round(ln1 * block / le1 / GiB, 4),
+               "single_thread_decode_gibps": round(ln1 * block / ld1 / GiB, 4)}
     return {
         "value": round(statistics.median(runs), 4),
         "unit": "GiB/s",
@@ -226,6 +252,7 @@ def cpu_baseline(data_chunk: bytes, block: int, seconds: float):
         "cpu_affinity": affinity,
         "cgroup_cpu_quota": quota,
         "cpu_model": model,
+        "third_party_liblz4": lz4,
     }
 
 

@@ -54,29 +54,7 @@ void s3hc_destroy(s3hc_ctx* ctx);
 const char* s3hc_last_error(void);
 const char* s3hc_version(void);
 
-/* Diagnostic / A-B switches (no reference counterpart: the reference has one codec). Read from
- * the environment (S3HC_FAST_DISABLE, S3HC_FAST, S3HC_LB_DISABLE, S3HC_LBW_DISABLE, S3HC_LBW_CAP,
- * S3HC_LBW_ROUNDS, S3HC_DEC_ONEWAVE, S3HC_FAST_TRACE, S3HC_LB_TRACE, S3HC_HOST_TRACE,
- * S3HC_READER_SLOTS, S3HC_POISON) once per
- * process at the first s3hc_create; this call changes one afterwards (value NULL = default; a
- * flag knob is on when its value is non-NULL, S3HC_FAST is on unless "0"). Process-wide. The
- * per-call decode path only reads the cached values. S3HC_INVALID_ARG for an unknown name.
- * S3HC_POISON=1 fills every device scratch buffer with 0xFF when it is (re)allocated, so a read
- * of memory no launch wrote fails the same way on every box. */
-int s3hc_set_knob(const char* name, const char* value);
-/* The knob's current raw value (S3HC_FAST reads S3HC_FAST_DISABLE's slot), and setting that raw
- * value back: tests save and restore knobs exactly (aliases share one slot). */
-int s3hc_get_knob(const char* name, long long* value);
-int s3hc_set_knob_value(const char* name, long long value);
-
-/* Diagnostics (no reference counterpart): the range reader's check of the frame results a batch
- * decode wrote (lengths, statuses) before they drive any device-to-host copy. Frame f's slot is
- * [dst_off[f], dst_off[f + 1]) (the last one up to slot_total). S3HC_OK with *good = frames before
- * the first failing one and *bytes = their decoded bytes; S3HC_DEVICE when a status is not one a
- * decoder assigns or a good frame's length exceeds its slot. Pure host code (tests forge results). */
-int s3hc_diag_check_batch_results(uint32_t n, const uint32_t* olen, const int32_t* status,
-                                  const uint64_t* dst_off, uint64_t slot_total, uint32_t* good,
-                                  uint64_t* bytes);
+/* Diagnostic switches and checks (no reference counterpart) are declared in s3hc_lz4_diag.h. */
 
 /* Largest framed size any s3hc_compress_* call can produce for n input bytes. */
 size_t s3hc_frame_bound(size_t n);
@@ -126,8 +104,12 @@ void s3hc_stream_close(s3hc_stream* s);
  * run on `depth` HIP queues, S3HC_READER_SLOTS (default 1) batches in flight per queue (pinned
  * H2D of input + host-walked frame tables, decode, one
  * frame-close launch = lengths + content xxh32 + EndMark checks, D2H), so batches overlap;
- * decoded bytes come back in stream order. Same semantics as s3hc_stream; the first failing
- * frame ends the stream after the bytes of every earlier frame.
+ * decoded bytes come back in stream order. The first failing frame ends the stream after the bytes
+ * of every earlier frame; a frame whose only fault is its content checksum is itself delivered
+ * first, as lz4_flex's FrameDecoder returns a frame's bytes before the EndMark check
+ * (disk_cache.rs:3884-3898). Frames of blocks > 64 KiB (the reference's cache files) have their
+ * checksums verified behind the delivered bytes by a second frame close on the batch's queue; no
+ * byte of a later frame is delivered before that verdict.
  * s3hc_reader_set_batch_max (optional, default = batch_bytes): while earlier batches are still
  * in flight, a new batch may take buffered frames up to max_bytes (the first batch after an idle
  * pipeline stays at batch_bytes, so time to first byte is unchanged). */
@@ -302,7 +284,9 @@ int s3hc_aggregator_create(s3hc_ctx* ctx, size_t batch_size, size_t flush_bytes,
  * http_proxy.rs:11608-11622, spread over a node's GPUs): each flush splits the queued batches
  * into contiguous shards of about equal bytes (s3hc_shard_items), encodes shard d on ctxs[d]
  * (concurrently, no collective), and delivers every frame in queue order, byte-identical to the
- * one-device aggregator. Duplicate context pointers are refused. */
+ * one-device aggregator. Duplicate context pointers are refused, and so are contexts whose encode
+ * modes (s3hc_set_encode_mode) differ — at creation, and at a flush if a mode changed since: the
+ * writers of that flush then fail with S3HC_INVALID_ARG rather than get device-dependent frames. */
 int s3hc_aggregator_create_multi(s3hc_ctx* const* ctxs, int nctx, size_t batch_size, size_t flush_bytes,
                                  uint32_t flush_batches, s3hc_handler* stats, s3hc_aggregator** out);
 /* Contiguous shards of n items of byte sizes len[] over ndev devices: item i goes to the shard

@@ -1293,6 +1293,9 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
 #endif
 }
 
+#ifndef S3HC_SMALL_JUMP  // 1: small launches decode by pointer jumping (k_djump), 0: k_dsmall's executor
+#define S3HC_SMALL_JUMP 1
+#endif
 // ------------------------------------------------------------------ k_dsmall
 namespace {
 constexpr uint32_t XH1 = 2654435761U, XH2 = 2246822519U, XH3 = 3266489917U, XH4 = 668265263U, XH5 = 374761393U;
@@ -1355,6 +1358,7 @@ __device__ __forceinline__ uint32_t hash_ring(const uint32_t* ring, volatile uin
 // (the frame's content xxh32 when the block is the whole frame: blk_hash, which k_dframe_close
 // takes instead of hashing again). One launch instead of the large-block path's chain; units it
 // does not take are left to k_decode_pe (exact statuses) and get blk_hash 0.
+#if !S3HC_SMALL_JUMP  // (the variant: compiled only when selected at build time)
 __global__ __launch_bounds__(fst::kTT) void k_dsmall(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                      const DecBlock* __restrict__ blk, const DecUnit* __restrict__ units,
                                                      uint32_t nunits, const uint8_t* __restrict__ unit_lb, FastArgs a,
@@ -1387,11 +1391,9 @@ __global__ __launch_bounds__(fst::kTT) void k_dsmall(const uint8_t* __restrict__
         __syncthreads();
     }
 }
+#endif  // !S3HC_SMALL_JUMP
 
 // ------------------------------------------------------------------ k_djump
-#ifndef S3HC_SMALL_JUMP  // 1: small launches decode by pointer jumping (k_djump), 0: k_dsmall's executor
-#define S3HC_SMALL_JUMP 1
-#endif
 // Small host-walked launches by pointer jumping, for the latency of a few-block batch (the range
 // reader's 256 KiB batches) rather than throughput: one 1024-thread workgroup per block indexes it
 // (dtok_unit with 1024 speculative segments: records, as k_dtok writes them) and decodes it with
@@ -1508,6 +1510,12 @@ __global__ __launch_bounds__(jmp::kT) void k_djump(const uint8_t* __restrict__ s
         if (!dtok_unit<kT>(u, src, blk, units, unit_lb, a, maxc, &F)) {  // (a unit it leaves: bh 0)
             __syncthreads();  // (every thread is done with the staged block)
             if (own_left && gridDim.x >= nunits) {  // (this workgroup's only unit)
+                // Invariant this relies on: waves 2-15 end the kernel here, and a workgroup
+                // barrier (s_barrier) waits only for the waves of the workgroup that have not
+                // ended, so every __syncthreads() inside decode_unit_pe pairs waves 0-1 with
+                // each other. That holds because no wave reaches any later barrier of this kernel:
+                // waves 0-1 return right after decode_unit_pe, waves 2-15 return now (the
+                // GPUTEST_r04 fault was waves waiting at a *different* barrier of the same kernel).
                 if (t >= 128u) return;
                 decode_unit_pe(u, dsm, src, dst, blk, units, blk_out, blk_status, nullptr, nullptr);
                 return;
@@ -1758,9 +1766,18 @@ hipError_t launch_fast_small(const uint8_t* src, uint8_t* dst, const DecBlock* b
     if (!nunits || !a.maxc) return hipSuccess;
     const uint32_t maxc = a.maxc < kFastMaxC ? a.maxc : kFastMaxC;
 #if S3HC_SMALL_JUMP
-    static const hipError_t attr = hipFuncSetAttribute((const void*)k_djump, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)jmp::kLds);  // (> 64 KiB of dynamic LDS)
-    if (attr != hipSuccess) return attr;
+    // > 64 KiB of dynamic LDS: the attribute belongs to the current device, so it is set once per
+    // device (a process-wide once would leave every device but the first without it)
+    static std::atomic<uint64_t> attr_set{0};
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev); e != hipSuccess) return e;
+    const uint64_t bit = dev < 64 ? 1ull << dev : 0ull;
+    if (!bit || !(attr_set.load(std::memory_order_acquire) & bit)) {
+        const hipError_t attr = hipFuncSetAttribute((const void*)k_djump, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    (int)jmp::kLds);
+        if (attr != hipSuccess) return attr;
+        attr_set.fetch_or(bit, std::memory_order_acq_rel);
+    }
     hipLaunchKernelGGL(k_djump, dim3(nunits), dim3(jmp::kT), jmp::kLds, st, src, dst, blk, units, nunits, unit_lb, a,
                        maxc, blk_out, blk_status, own_left ? 1u : 0u);
     *owned = own_left;

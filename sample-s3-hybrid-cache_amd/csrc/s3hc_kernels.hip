@@ -928,6 +928,9 @@ __device__ __forceinline__ uint32_t unit_count(const uint64_t* ucount, uint32_t 
 #ifndef S3HC_DEC_LDS_PAD
 #define S3HC_DEC_LDS_PAD 0  // diagnostic builds: extra LDS per workgroup to lower occupancy
 #endif
+// The one-wave-per-unit decoder (round 1's default; S3HC_DEC_ONEWAVE=1) is a comparison variant:
+// compiled only into diagnostic builds (make diag DIAG=-DS3HC_DIAG_VARIANTS=1), never shipped.
+#if S3HC_DIAG_VARIANTS
 __device__ __forceinline__ void decode_unit_wave(const uint32_t u, uint8_t* smem, const uint8_t* __restrict__ src,
                                                  uint8_t* dst, const DecBlock* __restrict__ blk,
                                                  const DecUnit* __restrict__ units, uint32_t* __restrict__ blk_out,
@@ -1005,6 +1008,7 @@ __global__ __launch_bounds__(256) void k_decode_units(const uint8_t* __restrict_
         if (u < nu) decode_unit_wave(u, smem, src, dst, blk, units, blk_out, blk_status, unit_lb, unit_fast);
     }
 }
+#endif  // S3HC_DIAG_VARIANTS
 
 // ====================================================== decode, parser + executor waves
 // k_decode_pe: the same decoder with the two halves of a window on two waves of one 128-thread
@@ -2404,7 +2408,8 @@ __device__ __forceinline__ void dframe_close_lane(uint32_t gid, const uint8_t* _
                                                   const uint64_t* __restrict__ blk_hash, const uint8_t* __restrict__ out,
                                                   const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ fwant,
                                                   uint32_t n, const int32_t* fstat_in, int32_t* fstatus,
-                                                  uint32_t* __restrict__ out_len, uint32_t* __restrict__ got_hash) {
+                                                  uint32_t* __restrict__ out_len, uint32_t* __restrict__ got_hash,
+                                                  uint32_t* __restrict__ pend) {
     const uint32_t f = gid / kCloseLanes, j = gid % kCloseLanes;
     const bool act = f < n;
     int st = S3HC_OK;
@@ -2426,7 +2431,13 @@ __device__ __forceinline__ void dframe_close_lane(uint32_t gid, const uint8_t* _
     }
     const uint32_t L = st == S3HC_OK ? (uint32_t)tot : 0u;
     const bool have = (pre >> 32) != 0;
-    uint32_t h = xxh32_lanes<32, true>(out + (act ? out_off[f] : 0), have ? 0u : L, act, j);
+    // pend (nullable): the range reader's first close of a batch (stream_range_data order,
+    // disk_cache.rs:3884-3898: lz4_flex checks the content checksum at the EndMark, after the
+    // frame's bytes were returned). A frame whose hash no decode kernel computed is left
+    // unverified here (pend[f] = 1, status without the checksum); a second, full close of the same
+    // frames follows on the queue and gives the final statuses behind the delivered bytes.
+    const bool defer = pend && act && st == S3HC_OK && !have && (src[frame_off[f] + 4] & 0x04);
+    uint32_t h = xxh32_lanes<32, true>(out + (act ? out_off[f] : 0), have || defer ? 0u : L, act, j);
     if (!act || j != 0) return;
     if (have) h = (uint32_t)pre;
     out_len[f] = L;
@@ -2435,8 +2446,9 @@ __device__ __forceinline__ void dframe_close_lane(uint32_t gid, const uint8_t* _
         const uint8_t* fp = src + frame_off[f];
         const uint32_t flg = fp[4];
         if ((flg & 0x08) && (rd32(fp + 6) | ((uint64_t)rd32(fp + 10) << 32)) != L) st = S3HC_CORRUPT;
-        else if ((flg & 0x04) && h != fwant[f]) st = S3HC_CHECKSUM;
+        else if ((flg & 0x04) && !defer && h != fwant[f]) st = S3HC_CHECKSUM;
     }
+    if (pend) pend[f] = defer && st == S3HC_OK ? 1u : 0u;
     fstatus[f] = st;
 }
 __global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__ src, const uint64_t* __restrict__ frame_off,
@@ -2446,9 +2458,10 @@ __global__ __launch_bounds__(64) void k_dframe_close(const uint8_t* __restrict__
                                                      const uint64_t* __restrict__ blk_hash, const uint8_t* __restrict__ out,
                                                      const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ fwant,
                                                      uint32_t n, const int32_t* fstat_in, int32_t* fstatus,
-                                                     uint32_t* __restrict__ out_len, uint32_t* __restrict__ got_hash) {
+                                                     uint32_t* __restrict__ out_len, uint32_t* __restrict__ got_hash,
+                                                     uint32_t* __restrict__ pend) {
     dframe_close_lane(blockIdx.x * blockDim.x + threadIdx.x, src, frame_off, blk_base, nblk, blocks, blk_out, blk_status,
-                      blk_hash, out, out_off, fwant, n, fstat_in, fstatus, out_len, got_hash);
+                      blk_hash, out, out_off, fwant, n, fstat_in, fstatus, out_len, got_hash, pend);
 }
 
 }  // namespace s3hc
@@ -2469,14 +2482,16 @@ hipError_t launch_decode_units(const uint8_t* src, uint8_t* dst, const DecBlock*
                                uint32_t nunits, const uint64_t* ucount, uint32_t grid, uint32_t* blk_out,
                                int32_t* blk_status, const uint8_t* unit_lb, const uint8_t* unit_fast, hipStream_t st) {
     if (!nunits || !grid) return hipSuccess;
-    // S3HC_DEC_ONEWAVE=1 (comparisons): one wave per unit doing both halves (k_decode_units)
-    const bool onewave = knob_on(KN_DEC_ONEWAVE);
-    if (onewave)
+#if S3HC_DIAG_VARIANTS
+    // S3HC_DEC_ONEWAVE=1 (diagnostic builds): one wave per unit doing both halves (k_decode_units)
+    if (knob_on(KN_DEC_ONEWAVE)) {
         hipLaunchKernelGGL(k_decode_units, dim3(cdiv(grid, dec::kWaves)), dim3(64 * dec::kWaves), 0, st, src, dst,
                            blk, units, nunits, ucount, blk_out, blk_status, unit_lb, unit_fast);
-    else
-        hipLaunchKernelGGL(k_decode_pe, dim3(grid), dim3(128), 0, st, src, dst, blk, units, nunits, ucount, blk_out,
-                           blk_status, unit_lb, unit_fast);
+        return hipGetLastError();
+    }
+#endif
+    hipLaunchKernelGGL(k_decode_pe, dim3(grid), dim3(128), 0, st, src, dst, blk, units, nunits, ucount, blk_out,
+                       blk_status, unit_lb, unit_fast);
     return hipGetLastError();
 }
 hipError_t launch_enc_parse(const uint8_t* src, const EncBlock* blocks, const uint2* groups, uint32_t ngroups,
@@ -2553,11 +2568,12 @@ hipError_t launch_dframe_close(const uint8_t* src, const uint64_t* frame_off, co
                                const uint32_t* nblk, const DecBlock* blocks, const uint32_t* blk_out,
                                const int32_t* blk_status, const uint64_t* blk_hash, const uint8_t* out,
                                const uint64_t* out_off, const uint32_t* fwant, uint32_t n, const int32_t* fstat_in,
-                               int32_t* fstatus, uint32_t* out_len, uint32_t* got_hash, hipStream_t st) {
+                               int32_t* fstatus, uint32_t* out_len, uint32_t* got_hash, hipStream_t st,
+                               uint32_t* pend) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_dframe_close, dim3(cdiv((uint64_t)n * kCloseLanes, 64)), dim3(64), 0, st, src, frame_off, blk_base, nblk,
                        blocks, blk_out, blk_status, blk_hash, out, out_off, fwant, n, fstat_in, fstatus, out_len,
-                       got_hash);
+                       got_hash, pend);
     return hipGetLastError();
 }
 hipError_t launch_dframe_verify(const uint8_t* src, const uint64_t* frame_off, uint32_t n, const uint32_t* fwant,

@@ -7,6 +7,12 @@
 #include <atomic>
 #include <stdint.h>
 
+// Comparison variants (the one-wave unit decoder): diagnostic builds only,
+// make diag DIAG=-DS3HC_DIAG_VARIANTS=1; the shipped library has neither the kernel nor the knob.
+#ifndef S3HC_DIAG_VARIANTS
+#define S3HC_DIAG_VARIANTS 0
+#endif
+
 namespace s3hc {
 
 enum Knob : int {
@@ -15,7 +21,7 @@ enum Knob : int {
     KN_LBW_DISABLE,       // S3HC_LBW_DISABLE=1: large blocks on the step loop, never spread
     KN_LBW_CAP,           // S3HC_LBW_CAP=<positions>: spread-execution capacity (-1: the size rule)
     KN_LBW_ROUNDS,        // S3HC_LBW_ROUNDS=<n>: fewer pointer-jumping launches (-1: all)
-    KN_DEC_ONEWAVE,       // S3HC_DEC_ONEWAVE=1: the one-wave unit decoder instead of parser + executor
+    KN_DEC_ONEWAVE,       // S3HC_DEC_ONEWAVE=1 (S3HC_DIAG_VARIANTS builds): the one-wave unit decoder
     KN_FAST_TRACE,        // S3HC_FAST_TRACE=1: stderr line per decode launch (serialises the stream)
     KN_LB_TRACE,          // S3HC_LB_TRACE=1: stderr line per large-block launch (serialises the stream)
     KN_HOST_TRACE,        // S3HC_HOST_TRACE=1: host-call stage times on stderr

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "s3hc_lz4.h"
+#include "s3hc_lz4_diag.h"
 #include "s3hc_plan.hpp"
 #include "s3hc_guard.hpp"
 #include "s3hc_knobs.hpp"
@@ -66,7 +67,8 @@ hipError_t launch_dframe_verify(const uint8_t*, const uint64_t*, uint32_t, const
                                 const uint32_t*, int32_t*, hipStream_t);
 hipError_t launch_dframe_close(const uint8_t*, const uint64_t*, const uint64_t*, const uint32_t*, const DecBlock*,
                                const uint32_t*, const int32_t*, const uint64_t*, const uint8_t*, const uint64_t*,
-                               const uint32_t*, uint32_t, const int32_t*, int32_t*, uint32_t*, uint32_t*, hipStream_t);
+                               const uint32_t*, uint32_t, const int32_t*, int32_t*, uint32_t*, uint32_t*, hipStream_t,
+                               uint32_t* pend = nullptr);
 }  // namespace s3hc
 
 using namespace s3hc;
@@ -132,6 +134,9 @@ struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
     ~DevBuf() { if (p) (void)hipFree(p); }
+    void trim(size_t keep) {  // free a buffer grown beyond `keep` bytes (the next ensure reallocates)
+        if (p && cap > keep) { (void)hipFree(p); p = nullptr; cap = 0; }
+    }
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
         // a buffer that grows again (per-batch sizes vary) takes 1.5x: no realloc churn
@@ -158,6 +163,9 @@ struct PinnedBuf {
     uint8_t* p = nullptr;
     size_t cap = 0;
     ~PinnedBuf() { if (p) (void)hipHostFree(p); }
+    void trim(size_t keep) {
+        if (p && cap > keep) { (void)hipHostFree(p); p = nullptr; cap = 0; }
+    }
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
         const size_t want = std::max<size_t>(regrow(n, cap), 1 << 16);
@@ -856,7 +864,10 @@ struct KnobName {
 constexpr KnobName kKnobNames[] = {
     {"S3HC_FAST_DISABLE", KN_FAST_DISABLE, 0}, {"S3HC_LB_DISABLE", KN_LB_DISABLE, 0},
     {"S3HC_LBW_DISABLE", KN_LBW_DISABLE, 0},   {"S3HC_LBW_CAP", KN_LBW_CAP, -1},
-    {"S3HC_LBW_ROUNDS", KN_LBW_ROUNDS, -1},    {"S3HC_DEC_ONEWAVE", KN_DEC_ONEWAVE, 0},
+    {"S3HC_LBW_ROUNDS", KN_LBW_ROUNDS, -1},
+#if S3HC_DIAG_VARIANTS
+    {"S3HC_DEC_ONEWAVE", KN_DEC_ONEWAVE, 0},
+#endif
     {"S3HC_FAST_TRACE", KN_FAST_TRACE, 0},     {"S3HC_LB_TRACE", KN_LB_TRACE, 0},
     {"S3HC_HOST_TRACE", KN_HOST_TRACE, 0},     {"S3HC_READER_SLOTS", KN_READER_SLOTS, 1},
     {"S3HC_POISON", KN_POISON, 0},
@@ -2074,10 +2085,18 @@ struct RSlot {
     uint32_t n = 0;
     std::vector<uint64_t> dst_off;
     hipEvent_t ev2 = nullptr;  // the batch's D2H of decoded bytes
+    hipEvent_t ev3 = nullptr;  // the batch's deferred content checksums (second close) read back
+    DevBuf d_v;                // second close: final statuses (i32[n]) and lengths (u32[n])
+    PinnedBuf h_v;             // its final statuses
     int state = 0;          // 0 decoding, 1 copying decoded bytes to h_out, 2 ready
     bool ready = false;     // h_out holds the batch's decoded bytes (in stream order)
-    uint32_t good = 0;      // frames before the first failing one
-    uint64_t out_len = 0;   // bytes in h_out
+    bool deferred = false;  // the batch's first close left content checksums to a second close
+    bool verdict = false;   // delivered frames still wait for those checksums (before any later byte)
+    uint32_t incl = 0;      // frames whose bytes were copied to h_out: [0, incl)
+    std::vector<uint32_t> olen;   // first close: lengths
+    std::vector<int32_t> st1;     // first close: statuses
+    std::vector<uint8_t> pend;    // first close: checksum deferred
+    uint64_t out_len = 0;   // bytes of h_out that may be read now
     uint64_t out_pos = 0;   // bytes already read
     uint64_t spec = 0;      // decoded-slot prefix copied to h_out right behind the decode (one round trip)
     bool covered = false;   // the good frames' bytes lie in that prefix: no second copy
@@ -2085,13 +2104,15 @@ struct RSlot {
     uint64_t slot = 0;      // decoded-slot bytes of the batch (frame f's slot: [dst_off[f], dst_off[f + 1]))
     int32_t err = 0;        // status of the first failing frame (good < n)
     void reset() {          // (a slot taken from its context's pool: buffers kept, batch state cleared)
-        n = 0; state = 0; ready = false; good = 0; out_len = 0; out_pos = 0; spec = 0; covered = false;
-        R = 0; slot = 0; err = 0; dst_off.clear(); st = nullptr;
+        n = 0; state = 0; ready = false; deferred = false; verdict = false; incl = 0; out_len = 0; out_pos = 0;
+        spec = 0; covered = false; R = 0; slot = 0; err = 0; dst_off.clear(); st = nullptr;
+        olen.clear(); st1.clear(); pend.clear();
     }
     ~RSlot() {
         if (ctx) (void)hipSetDevice(ctx->device);
         if (ev) (void)hipEventDestroy(ev);
         if (ev2) (void)hipEventDestroy(ev2);
+        if (ev3) (void)hipEventDestroy(ev3);
     }
 };
 constexpr size_t kReaderPoolMax = 64;  // pooled slots (and queues) per context
@@ -2110,11 +2131,23 @@ RSlot* rslot_take(s3hc_ctx* c) {
     S->ctx = c;
     if (hipEventCreateWithFlags(&S->ev, hipEventDisableTiming) != hipSuccess) return nullptr;
     if (hipEventCreateWithFlags(&S->ev2, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&S->ev3, hipEventDisableTiming) != hipSuccess) return nullptr;
     return S.release();
 }
+// A pooled slot keeps buffers up to this size: one GET with large batches or 4 MiB blocks must
+// not pin tens of MiB per slot for the life of the process; bigger ones are freed
+// when the slot returns to its pool and regrown by the next batch that needs them.
+constexpr size_t kReaderPoolKeep = 8u << 20;
 void rslot_give(RSlot* S) {  // (nothing of the slot in flight)
     if (!S) return;
     s3hc_ctx* c = S->ctx;
+    (void)hipSetDevice(c->device);
+    S->h_in.trim(kReaderPoolKeep);
+    S->h_out.trim(kReaderPoolKeep);
+    S->d_in.trim(kReaderPoolKeep);
+    S->d_out.trim(kReaderPoolKeep);
+    S->lb.wP.trim(kReaderPoolKeep);
+    S->lb.f_bmp.trim(kReaderPoolKeep);
     {
         std::lock_guard<std::mutex> g(c->rpool_mu);
         if (c->rslot_pool.size() < kReaderPoolMax) {
@@ -2172,10 +2205,12 @@ static int check_batch_results(uint32_t n, const uint32_t* olen, const int32_t* 
     for (; g < n; ++g) {
         const int32_t s = st[g];
         if (s < S3HC_OK || s > S3HC_INVALID_ARG) return fail(S3HC_DEVICE, "decode results: status out of range");
-        if (s != S3HC_OK) break;
         const uint64_t lo = dst_off[g], hi = g + 1 < n ? dst_off[g + 1] : slot_total;
-        if (lo > hi || hi > slot_total || olen[g] > hi - lo)
+        // (a frame that failed only its content checksum is delivered before the error: its
+        // length must fit its slot as well)
+        if ((s == S3HC_OK || s == S3HC_CHECKSUM) && (lo > hi || hi > slot_total || olen[g] > hi - lo))
             return fail(S3HC_DEVICE, "decode results: frame length beyond its slot");
+        if (s != S3HC_OK) break;
         b += olen[g];
     }
     *good = g;
@@ -2252,6 +2287,12 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     S.n = n;
     S.slot = slot;
     S.dst_off.resize(n);
+    // frames of blocks > 64 KiB with a content checksum (the reference's own cache files: one
+    // block of up to 4 MiB per frame) may have no hash from their decode (spread execution): their
+    // checksums are verified behind the delivered bytes by a second close (stream_range_data
+    // order, disk_cache.rs:3884-3898)
+    S.deferred = false;
+    for (uint32_t f = 0; f < n; ++f) S.deferred |= W.frames[f].bmax > 65536u && (W.frames[f].flg & 0x04u);
     std::vector<DecUnit> units;
     for (uint32_t f = 0; f < n; ++f) {
         const HFrame& F = W.frames[f];
@@ -2300,9 +2341,14 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     RTimer T_(r->tr, ReaderTrace::SUBMIT);
     ++r->tr.batches;
     HIPCHK(S.d_in.ensure(o_meta + nmeta + 64));
-    // one device-to-host copy per batch: the frame results, then (256-byte aligned) the slots
-    S.R = (8ull * n + 255) & ~255ull;
+    // one device-to-host copy per batch: the frame results (lengths, statuses and, deferred,
+    // the first close's pending flags), then (256-byte aligned) the slots
+    S.R = ((S.deferred ? 12ull : 8ull) * n + 255) & ~255ull;
     HIPCHK(S.d_out.ensure(S.R + slot + 64));
+    if (S.deferred) {
+        HIPCHK(S.d_v.ensure(8ull * n + 16));
+        HIPCHK(S.h_v.ensure(4ull * n + 16));
+    }
     HIPCHK(S.d_blk_out.ensure(4ull * nbk + 16));
     HIPCHK(S.d_blk_status.ensure(4ull * nbk + 16));
     {
@@ -2323,10 +2369,11 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
                          S.d_blk_status.as<int32_t>(), st, &bh, nullptr, 0));
     T.end();
     T.begin("dec_close");
+    uint32_t* d_pend = S.deferred ? (uint32_t*)(S.d_out.as<uint8_t>() + 8ull * n) : nullptr;
     HIPCHK(launch_dframe_close(src, (const uint64_t*)(dm + o_fo), (const uint64_t*)(dm + o_bb),
                                (const uint32_t*)(dm + o_nb), d_blk, S.d_blk_out.as<uint32_t>(),
                                S.d_blk_status.as<int32_t>(), bh, d_slots, (const uint64_t*)(dm + o_oo),
-                               (const uint32_t*)(dm + o_w), n, nullptr, d_st, d_olen, nullptr, st));
+                               (const uint32_t*)(dm + o_w), n, nullptr, d_st, d_olen, nullptr, st, d_pend));
     T.end();
     // speculative copy of the decoded slots behind the decode, in the same round trip: frames of
     // 64 KiB blocks fill their slots, so the prefix is the batch's output; a frame whose slot is
@@ -2335,9 +2382,24 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     HIPCHK(S.h_out.ensure(S.R + S.spec + 16));
     HIPCHK(hipMemcpyAsync(S.h_out.p, S.d_out.p, S.R + S.spec, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(S.ev, st));
+    if (S.deferred) {
+        // the second close: the same frames with every content checksum, behind the first
+        // close's results on the queue (the host delivers the bytes meanwhile)
+        T.begin("dec_verify");
+        int32_t* d_hst = S.d_v.as<int32_t>();
+        HIPCHK(launch_dframe_close(src, (const uint64_t*)(dm + o_fo), (const uint64_t*)(dm + o_bb),
+                                   (const uint32_t*)(dm + o_nb), d_blk, S.d_blk_out.as<uint32_t>(),
+                                   S.d_blk_status.as<int32_t>(), bh, d_slots, (const uint64_t*)(dm + o_oo),
+                                   (const uint32_t*)(dm + o_w), n, nullptr, d_hst, (uint32_t*)(d_hst + n), nullptr,
+                                   st));
+        T.end();
+        HIPCHK(hipMemcpyAsync(S.h_v.p, d_hst, 4ull * n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(S.ev3, st));
+    }
     S.state = 0;
     S.ready = false;
     S.covered = false;
+    S.verdict = false;
     r->in_head += end;
     return S3HC_OK;
 }
@@ -2406,21 +2468,50 @@ static int reader_pump(s3hc_reader* r) {
 static int reader_issue_copy(RSlot& S, ReaderTrace& tr) {
     RTimer T_(tr, ReaderTrace::ISSUE);
     HIPCHK(hipSetDevice(S.ctx->device));
-    // (the results head h_out; olen is copied before h_out may be reallocated below)
-    std::vector<uint32_t> olen((const uint32_t*)S.h_out.p, (const uint32_t*)S.h_out.p + S.n);
-    const int32_t* st = (const int32_t*)(S.h_out.p + 4ull * S.n);
+    // (the results head h_out; they are copied before h_out may be reallocated below)
+    const uint32_t n = S.n;
+    S.olen.assign((const uint32_t*)S.h_out.p, (const uint32_t*)S.h_out.p + n);
+    S.st1.assign((const int32_t*)(S.h_out.p + 4ull * n), (const int32_t*)(S.h_out.p + 4ull * n) + n);
+    const std::vector<uint32_t>& olen = S.olen;
     uint32_t good = 0;
     uint64_t bytes = 0;
-    if (int rc = check_batch_results(S.n, olen.data(), st, S.dst_off.data(), S.slot, &good, &bytes)) return rc;
+    if (int rc = check_batch_results(n, olen.data(), S.st1.data(), S.dst_off.data(), S.slot, &good, &bytes)) return rc;
+    // a frame that failed only its content checksum is delivered before the error, as lz4_flex's
+    // FrameDecoder returns a frame's bytes before it checks the checksum at the EndMark
+    // (stream_range_data, disk_cache.rs:3884-3898)
+    uint32_t incl = good;
+    if (good < n && S.st1[good] == S3HC_CHECKSUM) {
+        bytes += olen[good];
+        incl = good + 1;
+    }
     if (bytes > S.slot) return fail(S3HC_DEVICE, "decode results: batch output beyond its slots");
-    S.err = good < S.n ? st[good] : 0;
+    S.err = good < n ? S.st1[good] : 0;
+    // frames [0, incl) are copied; of them, the bytes up to and including the first frame whose
+    // checksum the first close deferred may be read now, the rest once the second close is in
+    uint32_t deliver = incl;
+    S.pend.assign(n, 0);
+    if (S.deferred) {
+        const uint32_t* pd = (const uint32_t*)(S.h_out.p + 8ull * n);
+        for (uint32_t f = 0; f < n; ++f) {
+            if (pd[f] > 1u || (pd[f] && S.st1[f] != S3HC_OK)) return fail(S3HC_DEVICE, "decode results: bad pending flag");
+            S.pend[f] = (uint8_t)pd[f];
+        }
+        for (uint32_t f = 0; f < incl; ++f)
+            if (S.pend[f]) {
+                deliver = f + 1;
+                S.verdict = true;
+                break;
+            }
+    }
+    uint64_t now = 0;
+    for (uint32_t f = 0; f < deliver; ++f) now += olen[f];
     // frames decode into slots of their block capacity; when every frame but the last filled
     // its slot (the normal case) the good output is already contiguous: one copy, or none when
     // the speculative prefix already holds it
     bool packed = true;
-    for (uint32_t f = 0; f + 1 < good; ++f) packed &= S.dst_off[f] + olen[f] == S.dst_off[f + 1];
-    S.good = good;
-    S.out_len = bytes;
+    for (uint32_t f = 0; f + 1 < incl; ++f) packed &= S.dst_off[f] + olen[f] == S.dst_off[f + 1];
+    S.incl = incl;
+    S.out_len = now;
     S.out_pos = 0;
     S.state = 1;
     if (packed && bytes <= S.spec) {
@@ -2438,7 +2529,7 @@ static int reader_issue_copy(RSlot& S, ReaderTrace& tr) {
     HIPCHK(S.h_out.ensure(S.R + bytes + 16));
     {
         uint64_t o = 0;
-        for (uint32_t f = 0; f < good; ++f) {
+        for (uint32_t f = 0; f < incl; ++f) {
             if (olen[f]) HIPCHK(hipMemcpyAsync(S.h_out.p + S.R + o, d_slots + S.dst_off[f], olen[f],
                                                hipMemcpyDeviceToHost, S.st));
             o += olen[f];
@@ -2461,52 +2552,111 @@ static int reader_advance(s3hc_reader* r) {
     return S3HC_OK;
 }
 
-// Wait until the oldest batch's decoded bytes are in its pinned output buffer.
-static int reader_complete(s3hc_reader* r) {
-    RSlot& S = *r->slots[r->inflight.front()];
+// Every context of a reader locked in one global order (ascending context address, whatever
+// order the caller listed them in: two readers over [c0, c1] and [c1, c0] cannot deadlock); the
+// reader's per-slot scratch and the contexts' timing state are used under them. unlock()/relock()
+// bracket host waits on a batch's events, so a wait on one device never holds the other devices'
+// contexts (their aggregator lanes and single-context readers keep running).
+struct ReaderLock {
+    std::vector<std::mutex*> mus;
+    bool held = false;
+    explicit ReaderLock(s3hc_reader* r) {
+        for (auto* c : r->ctxs) mus.push_back(&c->mu);
+        std::sort(mus.begin(), mus.end(), std::less<std::mutex*>());
+        relock();
+    }
+    void relock() {
+        for (auto* m : mus) m->lock();
+        held = true;
+    }
+    void unlock() {
+        if (!held) return;
+        for (auto it = mus.rbegin(); it != mus.rend(); ++it) (*it)->unlock();
+        held = false;
+    }
+    ~ReaderLock() { unlock(); }
+};
+// Wait for a slot's event with the contexts unlocked (the slot and its queue are the reader's own).
+static int reader_wait(RSlot& S, hipEvent_t e, ReaderLock& g, ReaderTrace& tr) {
     HIPCHK(hipSetDevice(S.ctx->device));
+    if (hipEventQuery(e) == hipSuccess) return S3HC_OK;
+    RTimer T_(tr, ReaderTrace::WAIT);
+    g.unlock();
+    const hipError_t e2 = hipEventSynchronize(e);
+    g.relock();
+    HIPCHK(e2);
+    return S3HC_OK;
+}
+
+// The stream ends inside the head batch with status err: every later batch is dropped (its queue
+// synchronised first), and so is the buffered input; the head's readable bytes still come first.
+static void reader_end_after_head(s3hc_reader* r, int err, const char* msg) {
+    r->error = err;
+    r->error_msg = msg;
+    for (size_t k = 1; k < r->inflight.size(); ++k) {
+        RSlot& L = *r->slots[r->inflight[k]];
+        (void)hipSetDevice(L.ctx->device);
+        (void)hipStreamSynchronize(L.st);
+        L.state = 0;
+        L.ready = false;
+        L.verdict = false;
+    }
+    r->inflight.resize(1);
+    r->in.clear();
+    r->in_head = 0;
+}
+
+// Wait until the oldest batch's decoded bytes are in its pinned output buffer.
+static int reader_complete(s3hc_reader* r, ReaderLock& g) {
+    RSlot& S = *r->slots[r->inflight.front()];
     if (S.state == 0) {
-        {
-            RTimer T_(r->tr, ReaderTrace::WAIT);
-            HIPCHK(hipEventSynchronize(S.ev));
-        }
+        if (int rc = reader_wait(S, S.ev, g, r->tr)) return rc;
         int rc = reader_issue_copy(S, r->tr);
         if (rc) return rc;
     }
-    if (!S.covered) {
-        RTimer T_(r->tr, ReaderTrace::WAIT);
-        HIPCHK(hipSetDevice(S.ctx->device));
-        HIPCHK(hipEventSynchronize(S.ev2));
-    }
+    if (!S.covered)
+        if (int rc = reader_wait(S, S.ev2, g, r->tr)) return rc;
     S.state = 2;
     S.ready = true;
-    r->total += S.out_len;
-    if (S.good < S.n) {  // earlier in stream order than any error found while walking later input
-        r->error = S.err;
-        r->error_msg = "frame decode failed";
-        for (size_t k = 1; k < r->inflight.size(); ++k) {
-            RSlot& L = *r->slots[r->inflight[k]];
-            (void)hipSetDevice(L.ctx->device);
-            (void)hipStreamSynchronize(L.st);
-            L.state = 0;
-            L.ready = false;
-        }
-        r->inflight.resize(1);  // drop everything after the failing frame
-        r->in.clear();
-        r->in_head = 0;
+    // a failing frame of the first close ends the stream inside this batch whatever the deferred
+    // checksums say (they can only end it earlier)
+    if (S.err) reader_end_after_head(r, S.err, S.err == S3HC_CHECKSUM ? "content checksum mismatch" : "frame decode failed");
+    return S3HC_OK;
+}
+
+// The head batch's readable bytes are read and some of its frames wait for their deferred
+// content checksums: take the second close's statuses. The readable bytes grow to the next
+// pending frame (or the batch's end), or the stream ends with S3HC_CHECKSUM after the bytes of
+// the first frame whose checksum failed — that frame's own bytes included, as lz4_flex reads them.
+static int reader_verdict(s3hc_reader* r, RSlot& S, ReaderLock& g) {
+    if (int rc = reader_wait(S, S.ev3, g, r->tr)) return rc;
+    const uint32_t n = S.n;
+    const int32_t* hv = (const int32_t*)S.h_v.p;
+    uint32_t g2 = 0;
+    for (; g2 < n; ++g2) {
+        const int32_t s = hv[g2];
+        if (s < S3HC_OK || s > S3HC_INVALID_ARG) return fail(S3HC_DEVICE, "verify results: status out of range");
+        // a frame the first close did not defer keeps its status; a deferred one may only fail its checksum
+        if (S.pend[g2] ? (s != S3HC_OK && s != S3HC_CHECKSUM) : s != S.st1[g2])
+            return fail(S3HC_DEVICE, "verify results: status differs from the first close");
+        if (s != S3HC_OK) break;
+    }
+    uint32_t incl = g2 < n && hv[g2] == S3HC_CHECKSUM ? g2 + 1 : g2;
+    if (incl > S.incl) incl = S.incl;  // (never more than the first close allowed and copied)
+    S.verdict = false;  // (every pending frame of the batch is resolved now)
+    uint64_t len = 0;
+    for (uint32_t f = 0; f < incl; ++f) len += S.olen[f];
+    if (len < S.out_pos) return fail(S3HC_DEVICE, "verify results: fewer bytes than already read");
+    S.out_len = len;
+    uint32_t good1 = 0;  // the first close's first failing frame
+    while (good1 < n && S.st1[good1] == S3HC_OK) ++good1;
+    if (g2 < good1) {  // a deferred checksum failed before it: the stream ends there instead
+        S.err = S3HC_CHECKSUM;
+        reader_end_after_head(r, S3HC_CHECKSUM, "content checksum mismatch");
     }
     return S3HC_OK;
 }
 
-// Every context of a reader locked in list order (the same order on every path: no deadlock);
-// the reader's per-slot scratch and the contexts' timing state are used under them.
-struct ReaderLock {
-    std::vector<std::unique_lock<std::mutex>> g;
-    explicit ReaderLock(s3hc_reader* r) {
-        g.reserve(r->ctxs.size());
-        for (auto* c : r->ctxs) g.emplace_back(c->mu);
-    }
-};
 static int reader_new(s3hc_ctx* const* ctxs, int nctx, size_t batch_bytes, int depth, s3hc_reader** out) {
     if (!ctxs || nctx < 1 || !out || depth < 1 || depth > 16 || batch_bytes == 0) return fail(S3HC_INVALID_ARG, "bad arguments");
     for (int i = 0; i < nctx; ++i) {
@@ -2596,6 +2746,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
                 const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
                 if (k) par_memcpy(dst, S.h_out.p + S.R + S.out_pos, k);
                 S.out_pos += k;
+                r->total += k;
                 *n = k;
                 if (S.out_pos < S.out_len) return S3HC_OK;
             }
@@ -2609,7 +2760,16 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
                     const size_t k = (size_t)std::min<uint64_t>(cap, S.out_len - S.out_pos);
                     if (k) par_memcpy(dst, S.h_out.p + S.R + S.out_pos, k);
                     S.out_pos += k;
+                    r->total += k;
                     *n = k;
+                }
+                if (S.out_pos == S.out_len && S.verdict) {
+                    // read up to a frame whose content checksum is still being verified: nothing
+                    // after it before the verdict (returned bytes first; a wait only when asked again)
+                    if (*n) return S3HC_OK;
+                    int rc = reader_verdict(r, S, g);
+                    if (rc) return rc;
+                    continue;
                 }
                 if (S.out_pos == S.out_len) {  // slot free again: queue the next batch
                     S.ready = false;
@@ -2643,7 +2803,7 @@ extern "C" int s3hc_reader_read(s3hc_reader* r, uint8_t* dst, size_t cap, size_t
             RSlot& H = *r->slots[r->inflight.front()];
             const bool done = reader_copy_done(H);
             if (!done && r->inflight.size() < r->slots.size() && !r->finished && !r->error) return S3HC_OK;
-            int rc = reader_complete(r);
+            int rc = reader_complete(r, g);
             if (rc) return rc;
         }
     });

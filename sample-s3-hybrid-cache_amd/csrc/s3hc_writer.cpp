@@ -300,12 +300,35 @@ static int aggregated_flush(s3hc_aggregator* a) {
             msg[d] = "internal error";
         }
     };
+    // every shard must encode with lane 0's match-finder mode, or the frames would depend on
+    // which device a batch landed on (the byte-identical guarantee of the one-device aggregator)
+    const int mode0 = s3hc_get_encode_mode(a->lanes[0].ctx);
+    bool mixed = false;
+    for (int d = 1; d < nl; ++d) mixed |= s3hc_get_encode_mode(a->lanes[d].ctx) != mode0;
+    if (mixed)
+        for (int d = 0; d < nl; ++d) {
+            rc[d] = S3HC_INVALID_ARG;
+            msg[d] = "aggregator contexts use different encode modes (s3hc_set_encode_mode)";
+        }
+    auto run_ok = [&](int d) {
+        if (rc[d] == S3HC_OK) run(d);
+    };
     if (nl == 1) {
-        run(0);
+        run_ok(0);
     } else {
+        // (a thread that cannot be started leaves its shard to this thread, after the others;
+        // every started thread is joined on every path)
         std::vector<std::thread> th;
-        for (int d = 1; d < nl; ++d) th.emplace_back(run, d);
-        run(0);
+        std::vector<int> inline_d;
+        for (int d = 1; d < nl; ++d) {
+            try {
+                th.emplace_back(run_ok, d);
+            } catch (...) {
+                inline_d.push_back(d);
+            }
+        }
+        run_ok(0);
+        for (int d : inline_d) run_ok(d);
         for (auto& t : th) t.join();
     }
     int first_rc = S3HC_OK;
@@ -398,6 +421,9 @@ static int aggregator_new(s3hc_ctx* const* ctxs, int nctx, size_t batch_size, si
         for (int j = 0; j < i; ++j)
             if (ctxs[j] == ctxs[i]) return werr(S3HC_INVALID_ARG, "a context is listed twice");
     }
+    for (int i = 1; i < nctx; ++i)
+        if (s3hc_get_encode_mode(ctxs[i]) != s3hc_get_encode_mode(ctxs[0]))
+            return werr(S3HC_INVALID_ARG, "contexts use different encode modes (s3hc_set_encode_mode)");
     std::unique_ptr<s3hc_aggregator> a(new s3hc_aggregator);
     a->batch_size = batch_size;
     a->flush_bytes = flush_bytes;

@@ -1,7 +1,9 @@
-"""Both 64 KiB-unit decoders agree with the oracle and with each other.
+"""The per-unit decoder agrees with the oracle, and with the one-wave variant when
+the library is a diagnostic build that has it.
 
-k_decode_pe (parser wave + executor wave per unit, the default) and k_decode_units (one wave per
-unit, S3HC_DEC_ONEWAVE=1) run the same lz4_flex FrameDecoder semantics (compression.rs:463-502):
+k_decode_pe (parser wave + executor wave per unit, the shipped one) and k_decode_units (one wave
+per unit, S3HC_DEC_ONEWAVE=1, compiled only with S3HC_DIAG_VARIANTS=1: run these tests with
+S3HC_LIB_PATH pointing at such a build) run the same lz4_flex FrameDecoder semantics (compression.rs:463-502):
 every output byte and every status must match the oracle, on GPU-encoded, oracle-encoded
 (lz4_flex layout) and liblz4 frames, multi-block and linked units, stored blocks, and corrupted
 frames. S3HC_LB_DISABLE=1 keeps every block on these decoders.
@@ -25,8 +27,20 @@ def _with_env(env, fn):
         return fn()
 
 
+def _onewave_built():
+    import s3hc_lz4 as S
+
+    try:
+        S.get_knob("S3HC_DEC_ONEWAVE")
+        return True
+    except S.CodecError:
+        return False
+
+
 def _both(fn):
     pe = _with_env({"S3HC_LB_DISABLE": "1"}, fn)
+    if not _onewave_built():  # (the shipped library: the per-unit decoder alone, against the oracle)
+        return pe, pe
     one = _with_env({"S3HC_LB_DISABLE": "1", "S3HC_DEC_ONEWAVE": "1"}, fn)
     return pe, one
 

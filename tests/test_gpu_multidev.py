@@ -131,7 +131,7 @@ def test_multi_device_reader_corrupt_frame(engines, oracle):
                 break
             out += c
     assert e.value.status == S.S3HC_CHECKSUM
-    assert bytes(out) == data[:29 * 65536]
+    assert bytes(out) == data[:30 * 65536]  # frame 29's bytes before its checksum error
 
 
 def test_context_destroyed_before_reader_and_aggregator(oracle):
@@ -162,3 +162,79 @@ def test_context_destroyed_before_reader_and_aggregator(oracle):
     assert oracle.decompress_data(bytes(f)) == data
     rd.close()
     agg.close()
+
+
+def test_multi_device_aggregator_refuses_mixed_encode_modes(engines):
+    # frames must not depend on the device a batch lands on — contexts whose
+    # match-finder modes differ are refused at creation, and a flush after a mode change fails
+    # every writer of that flush instead of writing device-dependent frames
+    import s3hc_lz4 as S
+
+    a, b = engines[0], engines[1]
+    try:
+        b.set_encode_mode(S.ENC_SMALL)
+        with pytest.raises(S.CodecError) as e:
+            S.BatchAggregator([a, b], 65536)
+        assert e.value.status == S.S3HC_INVALID_ARG
+        b.set_encode_mode(S.ENC_FAST)
+        agg = S.BatchAggregator([a, b], 65536, flush_batches=0)
+        data = [synth.log_text(200_000, 70 + k) for k in range(4)]
+        ws = [agg.begin(0, len(d) - 1, True) for d in data]
+        for w, d in zip(ws, data):
+            w.write(d)
+        b.set_encode_mode(S.ENC_SMALL)
+        with pytest.raises(S.CodecError) as e:
+            agg.flush()
+        assert e.value.status == S.S3HC_INVALID_ARG
+        for w in ws:  # every writer of the flush failed (a later call reports it)
+            with pytest.raises(S.CodecError):
+                w.commit()
+        agg.close()
+    finally:
+        b.set_encode_mode(S.ENC_FAST)
+
+
+def test_multi_device_readers_in_opposite_context_order(engines, oracle):
+    # readers over [c0, c1] and [c1, c0] used from two threads at once take the
+    # contexts' locks in one global order (no deadlock), and neither holds them while it waits
+    import s3hc_lz4 as S
+
+    data = synth.log_text(6 * MiB + 11, 63)
+    frames = b"".join(oracle.lz4flex_compress_frame(data[i:i + 65536]) for i in range(0, len(data), 65536))
+    frames += b"".join(oracle.lz4flex_compress_frame(data[i:i + MiB]) for i in range(0, 2 * MiB, MiB))
+    want = data + data[:2 * MiB]
+    outs, errs = [None, None], []
+
+    def run(k):
+        try:
+            order = engines[:2] if k == 0 else engines[1::-1]
+            for _ in range(4):
+                r = S.RangeReader(order, 256 << 10, 2)
+                out = bytearray()
+                for i in range(0, len(frames), MiB):
+                    r.feed(frames[i:i + MiB])
+                    while True:
+                        c = r.read(MiB)
+                        if not c:
+                            break
+                        out += c
+                r.finish()
+                while True:
+                    c = r.read(MiB)
+                    if not c:
+                        break
+                    out += c
+                r.close()
+                assert bytes(out) == want
+            outs[k] = True
+        except Exception as ex:  # pragma: no cover
+            errs.append(ex)
+
+    ts = [threading.Thread(target=run, args=(k,), daemon=True) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=90)
+    assert not any(t.is_alive() for t in ts), "readers in opposite context order deadlocked"
+    assert not errs, errs
+    assert outs == [True, True]

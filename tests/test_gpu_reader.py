@@ -1,7 +1,10 @@
 """Pipelined range reader (s3hc_reader_*): stream_range_data semantics over batched device
 decodes on several queues. Output must equal the oracle's
 decompress of the same frames, in order, for any feed piece size and batch size; errors end the
-stream after every earlier frame's bytes (tests/streaming_decompression_property_test.rs)."""
+stream after every earlier frame's bytes (tests/streaming_decompression_property_test.rs). A frame
+whose only fault is its content checksum is delivered before S3HC_CHECKSUM, as lz4_flex's
+FrameDecoder returns a frame's bytes before it checks the checksum at the EndMark
+(disk_cache.rs:3884-3898; oracle.stream_range_data)."""
 import pytest
 
 import synth
@@ -62,7 +65,9 @@ def test_reader_corrupt_frame_stops_after_earlier_frames(engine, oracle, batch_m
     with pytest.raises(S.CodecError) as e:
         _drain(r, out)
     assert e.value.status == S.S3HC_CHECKSUM
-    assert bytes(out) == data[:9 * 65536]
+    # frame 9's bytes come before the error (the reference's order), nothing after it
+    assert bytes(out) == data[:10 * 65536]
+    assert oracle.stream_range_data(fr[:9] + [bytes(bad)] + fr[10:]) == (S.S3HC_CHECKSUM, bytes(out))
 
 
 def test_reader_truncated_tail(engine):
@@ -138,13 +143,9 @@ def test_reader_corrupt_block_payloads_one_launch_batches(engine, oracle, seed):
         for _ in range(rng.randint(1, 6)):
             p = rng.randrange(11, len(f) - 8)  # inside the block payload (after header and block size)
             f[p] ^= 1 << rng.randrange(8)
-    good, first_bad, want_st = bytearray(), None, 0
-    for k, f in enumerate(fr):
-        st, out = oracle.decompress_status(bytes(f))
-        if st != 0:
-            first_bad, want_st = k, st
-            break
-        good += out
+    # (stream_range_data order: a frame that fails only its content checksum is delivered first)
+    want_st, good = oracle.stream_range_data([bytes(f) for f in fr])
+    first_bad = None if want_st == 0 else True
     r = S.RangeReader(engine, 256 << 10, 3)
     r.feed(b"".join(bytes(f) for f in fr))
     r.finish()
@@ -182,7 +183,7 @@ def test_reader_batches_per_queue(engine, oracle, slots):
         with pytest.raises(S.CodecError) as e:
             _drain(r, out)
         assert e.value.status == S.S3HC_CHECKSUM
-        assert bytes(out) == data[:40 * 65536]
+        assert bytes(out) == data[:41 * 65536]
 
 
 @pytest.mark.parametrize("poison", [None, "1"])
@@ -210,13 +211,7 @@ def test_reader_many_small_frames_stored_and_corrupt(engine, oracle, poison, cor
     fr = [bytearray(oracle.lz4flex_compress_frame(x)) for x in items]
     if corrupt_at is not None:
         fr[corrupt_at][-1] ^= 0x44  # content checksum
-    good, want_st = bytearray(), 0
-    for f in fr:
-        st, out = oracle.decompress_status(bytes(f))
-        if st != 0:
-            want_st = st
-            break
-        good += out
+    want_st, good = oracle.stream_range_data([bytes(f) for f in fr])
     with S.knobs({"S3HC_POISON": poison}):
         for batch, depth in ((256 << 10, 3), (64 << 10, 2)):
             r = S.RangeReader(engine, batch, depth)
@@ -262,5 +257,86 @@ def test_reader_slots_pooled_across_readers(engine, oracle):
             with pytest.raises(S.CodecError) as e:
                 _drain(r, got)
             assert e.value.status == S.S3HC_CHECKSUM
-            assert bytes(got) == small[:len(small) // 65536 * 65536]
+            assert bytes(got) == small  # the last frame's bytes, then its checksum error
         r.close()
+
+
+def _ref_frames(oracle, data, item=MiB):
+    return [bytearray(oracle.lz4flex_compress_frame(data[i:i + item])) for i in range(0, len(data), item)]
+
+
+@pytest.mark.parametrize("batch,depth,batch_max", [(256 << 10, 3, None), (256 << 10, 1, None), (64 << 10, 2, None),
+                                                   (256 << 10, 3, 8 * MiB), (16 * MiB, 2, None)])
+@pytest.mark.parametrize("fault", ["checksum", "payload"])
+def test_reader_reference_frames_checksum_after_bytes(engine, oracle, batch, depth, batch_max, fault):
+    # the reference's cache files are chains of ~1 MiB frames of one block
+    # (disk_cache.rs:1826-1847); their content checksums are verified behind the delivered bytes
+    # (the second close), and a mismatch ends the stream with S3HC_CHECKSUM after that frame's
+    # bytes and before any byte of a later frame (stream_range_data, disk_cache.rs:3884-3898).
+    import s3hc_lz4 as S
+
+    data = synth.log_text(7 * MiB + 4321, 91)
+    fr = _ref_frames(oracle, data)
+    k = 4
+    if fault == "checksum":
+        fr[k][-2] ^= 0x08                      # the stored checksum itself
+    else:
+        fr[k][len(fr[k]) // 2] ^= 0x01         # a payload byte: decodes (or not), checksum differs
+    want_st, want = oracle.stream_range_data([bytes(f) for f in fr])
+    assert want_st != 0
+    if fault == "checksum":
+        assert want_st == S.S3HC_CHECKSUM and want == data[:(k + 1) * MiB]
+    for piece in (3 * MiB, 700_001):
+        r = S.RangeReader(engine, batch, depth, batch_max)
+        out = bytearray()
+        with pytest.raises(S.CodecError) as e:
+            for i in range(0, sum(map(len, fr)), piece):
+                r.feed(b"".join(bytes(f) for f in fr)[i:i + piece])
+                _drain(r, out)
+            r.finish()
+            _drain(r, out)
+        assert e.value.status == want_st, (piece, batch, depth)
+        assert bytes(out) == want, (piece, batch, depth, len(out), len(want))
+        r.close()
+
+
+@pytest.mark.parametrize("order", ["checksum_first", "corrupt_first", "clean_checksum_then_corrupt"])
+def test_reader_deferred_checksum_and_decode_error_in_one_batch(engine, oracle, order):
+    # one batch (batch_max) holding several reference frames: a deferred checksum failure and a
+    # decode failure of a later frame — the first in stream order decides, with the bytes before it
+    import s3hc_lz4 as S
+
+    data = synth.log_text(6 * MiB, 92)
+    fr = _ref_frames(oracle, data)
+    if order == "checksum_first":
+        fr[1][-1] ^= 0x80
+        fr[3][9] ^= 0xFF                        # the first block word: a decode/structure error
+    elif order == "corrupt_first":
+        fr[1][9] ^= 0xFF
+        fr[3][-1] ^= 0x80
+    else:
+        fr[3][9] ^= 0xFF
+    want_st, want = oracle.stream_range_data([bytes(f) for f in fr])
+    for depth in (1, 3):
+        r = S.RangeReader(engine, 64 << 20, depth)
+        r.feed(b"".join(bytes(f) for f in fr))
+        r.finish()
+        out = bytearray()
+        with pytest.raises(S.CodecError) as e:
+            _drain(r, out)
+        assert e.value.status == want_st
+        assert bytes(out) == want
+        r.close()
+
+
+def test_reader_reference_frames_clean_many_depths(engine, oracle):
+    # the deferred-checksum path on clean reference frames: every byte, in order, every depth
+    import s3hc_lz4 as S
+
+    data = synth.log_text(12 * MiB + 99, 93)
+    frames = b"".join(bytes(f) for f in _ref_frames(oracle, data))
+    for depth in (1, 2, 3, 4):
+        for cap in (MiB, 100_000):
+            out, r = _run(engine, frames, 2 * MiB, 256 << 10, depth, cap=cap)
+            assert out == data, (depth, cap)
+            assert r.total == len(data)

@@ -7,13 +7,15 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "s3hc_lz4.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("s3hc_lz4.h", "s3hc_lz4_diag.h")]
 
 
 def declared_functions():
-    txt = open(HEADER).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(s3hc_[a-z0-9_]+)\s*\(", txt)))
+    names = set()
+    for h in HEADERS:
+        txt = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(s3hc_[a-z0-9_]+)\s*\(", txt))
+    return sorted(names)
 
 
 def test_library_exports_header_symbols():

@@ -107,3 +107,27 @@ def test_mixed_frames(oracle):
     b = oracle.store_mode_frame(b"incompressible-ish chunk")
     assert oracle.decompress_data(a + b) == b"A" * 200 + b"incompressible-ish chunk"
     assert len(oracle.lz4flex_compress_frame(b"A" * 200)) < len(oracle.store_mode_frame(b"A" * 200))
+
+
+def test_stream_range_data_delivers_frame_before_checksum_error(oracle):
+    # disk_cache.rs:3884-3898: FrameDecoder::read returns a frame's bytes before the EndMark's
+    # content checksum is compared, so stream_range_data sends them, then the error chunk
+    data = bytes(range(256)) * 1000
+    fr = [bytearray(oracle.lz4flex_compress_frame(data[i:i + 65536])) for i in range(0, len(data), 65536)]
+    assert oracle.stream_range_data([bytes(f) for f in fr]) == (0, data)
+    bad = [bytearray(f) for f in fr]
+    bad[2][-1] ^= 0x01
+    assert oracle.stream_range_data([bytes(f) for f in bad]) == (oracle.CHECKSUM, data[:3 * 65536])
+    # the same frame without its content checksum (header checksum recomputed) decodes on liblz4
+    g = oracle._without_content_checksum(bytes(bad[2]))
+    assert g[4] & 0x04 == 0 and len(g) == len(bad[2]) - 4
+    if lz4ref.available:
+        assert lz4ref.decompress(g, 65536) == data[2 * 65536:3 * 65536]
+    # a structural fault (block size word) delivers nothing of its frame
+    bad = [bytearray(f) for f in fr]
+    bad[1][9] ^= 0xFF
+    st, out = oracle.stream_range_data([bytes(f) for f in bad])
+    assert st != 0 and out == data[:65536]
+    # an empty frame does not end the stream (Ok(0) ends only the inner loop)
+    e = oracle.lz4flex_compress_frame(b"")
+    assert oracle.stream_range_data([bytes(fr[0]), e, bytes(fr[1])]) == (0, data[:2 * 65536])
