@@ -443,16 +443,7 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
     uint32_t o = 0;
     int32_t minsl = 0x7FFFFFFF;
     bool bad = false;
-    auto emit = [&](uint32_t q, uint32_t k) {  // the token at q is sequence k
-#if S3HC_DTOK_SKIP & 2  // diagnostic builds (timing only, output wrong): no token parse in the record pass
-        Tok T;
-        T.ll = q & 7u;
-        T.ml = 4u + (q & 3u);
-        T.off = 1u + (q & 15u);
-        T.nxt = k + 1u == N ? END : q + 1u;
-#else
-        const Tok T = S3HC_HOPF(stage, mis, q, C);
-#endif
+    auto emitT = [&](uint32_t q, uint32_t k, const Tok& T) {  // the token at q (parsed: T) is sequence k
         const uint32_t lit = T.ll == 0 ? 0u : q + 1u + (T.ll >= 15u ? (T.ll - 15u) / 255u + 1u : 0u);
         o += T.ll;
         uint32_t y = 0;
@@ -467,6 +458,18 @@ __device__ __forceinline__ bool dtok_unit(const uint32_t u, const uint8_t* __res
 #else
         rec[k] = make_uint2(lit | (T.ll << 15), y);
 #endif
+    };
+    auto emit = [&](uint32_t q, uint32_t k) {  // the token at q is sequence k
+#if S3HC_DTOK_SKIP & 2  // diagnostic builds (timing only, output wrong): no token parse in the record pass
+        Tok T;
+        T.ll = q & 7u;
+        T.ml = 4u + (q & 3u);
+        T.off = 1u + (q & 15u);
+        T.nxt = k + 1u == N ? END : q + 1u;
+#else
+        const Tok T = S3HC_HOPF(stage, mis, q, C);
+#endif
+        emitT(q, k, T);
     };
 #if S3HC_DTOK_BAL == 1
     // balanced: thread g decodes sequences [g K, g K + K) (K = ceil(N / TT)), found from the
@@ -591,6 +594,10 @@ constexpr uint32_t kWin = 2048;      // output bytes of one batch, at most
 constexpr uint32_t kFl = 1024;       // flush granule
 constexpr uint32_t kGD = 4;          // pending-match dwords per lane held in registers
 constexpr uint32_t kGW = 64 * kGD;
+#ifndef S3HC_REDIR  // levels of sequence-level source redirection per window (0: off; round 6 A/B:
+#define S3HC_REDIR 1  // one level 0.497 ms decode, none 0.518, two 0.510, three 0.551)
+#endif
+constexpr uint32_t kRedir = S3HC_REDIR;
 static_assert(2 * kWin + kFl <= kOR, "far sources of a batch must be flushed before it runs");
 }  // namespace fst
 
@@ -833,6 +840,8 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t x, uint32_t l) {
 struct DexLds {
     uint4 pinfo[64];
     uint8_t gmk[fst::kGW];
+    uint32_t segs[64];  // redirection: each lane's sequence end (window offset, inclusive scan)
+    uint32_t samp[8];   // segs[8k + 7]: the first level of the owner search
 };
 
 // One wave executes unit u (taken by the token index: F = its sequences and bytes) into the
@@ -1015,6 +1024,69 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
             const bool hasm = act && ml > 0;
             const bool far = hasm && far_c;
             bool pend = hasm && !far && ms + ml > upos;
+            // ---- sequence-level source redirection (round 6). A pending match whose source lies
+            // inside the literals of one sequence of this window is final before round 0 (literals
+            // are stored first); one whose source lies inside the match of one non-overlapping
+            // sequence of the window copies from that sequence's source instead (the offset into
+            // it carries over): when that source is final (not pending, or before the window) the
+            // match becomes a round-0 item (16-byte copies, no dword sweeps), otherwise it keeps
+            // the sweeps below with the redirected source (same bytes, a shorter chain). kRedir
+            // levels repeat the step through pending owners; one level measured fastest (the
+            // levels' LDS round trips cost more than the sweeps they save). Sources straddling
+            // sequences, and overlapping copies, keep the sweeps.
+            uint32_t src = ms;    // the match's source (redirected)
+            bool rfar = false;    // a redirected source older than the ring: read from HBM
+            if (kRedir && __ballot(pend && off >= ml && ms >= upos)) {
+                bool cand = pend && off >= ml && ms >= upos;
+                bool redir = false;
+                dl->segs[lane] = Sincl_c;
+                if ((lane & 7u) == 7u) dl->samp[lane >> 3] = Sincl_c;
+                for (uint32_t lev = 0; lev < kRedir; ++lev) {
+                    // snapshot of the window's sequences: match start, current source, (ml, ll),
+                    // bit 0 = its current source holds final bytes before round 0 (not pending, or
+                    // resolved at an earlier level), bit 1 = it does not overlap itself
+                    pinfo[lane] = make_uint4(md, src, ml | (ll << 16),
+                                             (pend && !redir ? 0u : 1u) | (off >= ml ? 2u : 0u));
+                    wsync();
+                    if (cand) {
+                        // the sequence owning window offset r: the lanes whose end is <= r, counted
+                        // over 8 samples, then over the 8 ends of that bucket (samp[7] = S_c > r)
+                        const uint32_t r = src - upos;
+                        const uint4 sa = *(const uint4*)&dl->samp[0], sb = *(const uint4*)&dl->samp[4];
+                        const uint32_t b = (uint32_t)(sa.x <= r) + (uint32_t)(sa.y <= r) + (uint32_t)(sa.z <= r) +
+                                           (uint32_t)(sa.w <= r) + (uint32_t)(sb.x <= r) + (uint32_t)(sb.y <= r) +
+                                           (uint32_t)(sb.z <= r);
+                        const uint4 ta = *(const uint4*)&dl->segs[8u * b], tb = *(const uint4*)&dl->segs[8u * b + 4u];
+                        const uint32_t j = 8u * b + (uint32_t)(ta.x <= r) + (uint32_t)(ta.y <= r) + (uint32_t)(ta.z <= r) +
+                                           (uint32_t)(ta.w <= r) + (uint32_t)(tb.x <= r) + (uint32_t)(tb.y <= r) +
+                                           (uint32_t)(tb.z <= r);
+                        const uint4 Pj = pinfo[j];
+                        const uint32_t mdj = Pj.x, mlj = Pj.z & 0xFFFFu, dj = mdj - (Pj.z >> 16);
+                        if (src >= dj && src + ml <= mdj) {  // inside its literals
+                            cand = false;
+                            redir = true;
+                        } else if (src >= mdj && src + ml <= mdj + mlj && (Pj.w & 2u)) {  // inside its match
+                            // (the owner's source is final, or the new source lies wholly before
+                            // the window: done; else look again while it lies in the window. A
+                            // source left pending stays in the ring: a far owner source is final)
+                            src = Pj.y + (src - mdj);
+                            redir = (Pj.w & 1u) != 0u || src + ml <= upos;
+                            cand = !redir && src >= upos;
+                        } else {
+                            cand = false;  // straddles sequences, or the owner overlaps itself
+                        }
+                    }
+                    if (lev + 1u < kRedir) {
+                        wsync();
+                        if (!__ballot(cand)) break;
+                    }
+                }
+                wsync();  // (round 0 rewrites pinfo)
+                if (redir) {
+                    pend = false;
+                    rfar = src + kOR < upos + S_c;
+                }
+            }
             // round 0: far sources (prefetched) and sources before the window (an overlapping
             // match is always pending: its source reaches its own output)
             if (!(S3HC_FXSKIP & 4) && hasm && !pend) {
@@ -1033,7 +1105,7 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                 const uint32_t chincl = incl_scan(nch, lane);
                 const uint32_t T0 = rdlane(chincl, 63);
                 if (T0) {
-                    pinfo[lane] = make_uint4(md + c0, ms + c0, (ml - c0) | (far ? 0x10000u : 0u), chincl - nch);
+                    pinfo[lane] = make_uint4(md + c0, src + c0, (ml - c0) | (far || rfar ? 0x10000u : 0u), chincl - nch);
                     ((uint32_t*)gmk)[lane] = 0u;
                     wsync();
                     if (nch) gmk[chincl - nch] = (uint8_t)(lane + 1u);
@@ -1068,7 +1140,7 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                 const uint32_t cincl = incl_scan(cnt, lane);
                 const uint32_t T = rdlane(cincl, 63);
                 if (T <= 64u * kGD) {
-                    pinfo[lane] = make_uint4(md, ms, ml | (off << 16), df - (cincl - cnt));
+                    pinfo[lane] = make_uint4(md, src, ml | (off << 16), df - (cincl - cnt));
                     ((uint32_t*)gmk)[lane] = 0u;  // kGW = 256 mark bytes
                     wsync();
                     if (cnt) gmk[cincl - cnt] = (uint8_t)(lane + 1u);
@@ -1154,10 +1226,10 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
                         if (!pm) break;
                         const uint32_t first = (uint32_t)__builtin_ctzll(pm);
                         const uint32_t h = rdlane(md, (int)first);
-                        const bool run = pend && (lane == first || (off >= ml && ms + ml <= h));
+                        const bool run = pend && (lane == first || (off >= ml && src + ml <= h));
                         const uint32_t step = off < 16u ? off : 16u;
                         for (uint32_t c = 0; __ballot(run && c < ml); c += step)
-                            if (run && c < ml) rst(ring, md + c, rld16(ring, ms + c), umin_(step, ml - c));
+                            if (run && c < ml) rst(ring, md + c, rld16(ring, src + c), umin_(step, ml - c));
                         pend = pend && !run;
                         ++nrounds;
                     }

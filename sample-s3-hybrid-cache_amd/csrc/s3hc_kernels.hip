@@ -293,8 +293,8 @@ constexpr uint32_t kWin = 1024;    // output bytes executed per window (byte-par
 constexpr uint32_t kMarks = 1280;  // marks entries: >= kWin + 3 rounded up to the 256-byte pass
 constexpr uint32_t kRefs = 256;    // refs entries: one 256-byte pass
 constexpr uint32_t kSink = 64;     // per-lane store sink for lanes with nothing to store
-constexpr uint32_t kWaveLds = kRing + kCring + kMarks + 2 * kRefs + kSink + kMaxMem * 8;
-constexpr int kWaves = 4;
+[[maybe_unused]] constexpr uint32_t kWaveLds = kRing + kCring + kMarks + 2 * kRefs + kSink + kMaxMem * 8;
+[[maybe_unused]] constexpr int kWaves = 4;  // (one-wave decoder: S3HC_DIAG_VARIANTS builds)
 enum : uint32_t { F_ERR = 1, F_LAST = 2, F_LONG = 4, F_MORE = 8 };
 static_assert(kInit * kChunk >= kAhead + 3, "initial stage must cover the look-ahead");
 static_assert(kMaxMem <= 255, "marks hold member index + 1 in a byte");
@@ -1598,7 +1598,9 @@ __global__ __launch_bounds__(enc::kGThreads, S3HC_ENC_MINWAVES) S3HC_ENC_WPE_ATT
     // The first nxx workgroups compute the frames' content xxh32 (they are dispatched first and
     // overlap the match finding; the emitter reads the hashes).
     if (blockIdx.x < nxx) {
+#ifndef S3HC_ENC_NOXXH  // diagnostic builds (timing only, frame checksums wrong): no content hashing
         xxh32_ranges_dev<32, false>(src, fsrc_off, fsrc_len, nframes, fhash, blockIdx.x * kGThreads + threadIdx.x);
+#endif
         return;
     }
     const uint32_t gi = blockIdx.x - nxx;

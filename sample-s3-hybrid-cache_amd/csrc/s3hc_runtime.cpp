@@ -827,6 +827,8 @@ static int run_encode(s3hc_ctx* ctx, s3hc_plan* P, const uint8_t* d_src, uint8_t
     const uint32_t nf = (uint32_t)P->frame_blk0.size(), ni = (uint32_t)P->item_blk0.size();
     KTimer T(ctx, st);
     // match finding; the grid's first workgroups compute the frames' content xxh32 meanwhile
+    // (measured round 6: the same hash as its own launch on a second queue beside the finder
+    // slowed the finder as much as the in-grid workgroups do — the cost is issue, not LDS slots)
     T.begin("enc_parse");
     HIPCHK(launch_enc_parse(d_src, P->d_blocks.as<EncBlock>(), P->d_groups.as<uint2>(), (uint32_t)P->groups.size(),
                             P->d_frame_src_off.as<uint64_t>(), P->d_frame_src_len.as<uint32_t>(), nf,

@@ -351,3 +351,53 @@ def test_device_plan_multiblock_frames_keep_their_parallelism(engine, capfd):
     assert ost == [0] * (n + 1) and olen == [MiB] * (n + 1)
     got = out.read((n + 1) * MiB)
     assert got[:n * MiB] == data and got[n * MiB:] == data[3 * MiB:4 * MiB]
+
+
+def _chained_copies(n, seed):
+    # text made of copies of recent copies (chains of in-window matches whose sources lie inside
+    # earlier matches: k_dexec's sequence-level source redirection, round 6), copies from far
+    # back (sources older than the 8 KiB ring, read from HBM) and short literal runs
+    rng = random.Random(seed)
+    out = bytearray(rng.randbytes(64))
+    while len(out) < n:
+        r = rng.random()
+        if r < 0.55:
+            L = rng.randint(4, 14)
+            d = rng.randint(L, min(len(out), 300))
+            s = len(out) - d
+            out += out[s:s + L]
+        elif r < 0.75 and len(out) > 9000:
+            L = rng.randint(5, 40)
+            s = rng.randint(0, len(out) - 8500 - L)
+            out += out[s:s + L]
+        else:
+            out += rng.randbytes(rng.randint(1, 6))
+    return bytes(out[:n])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_fast_path_chained_in_window_copies(engine, oracle, seed):
+    # every frame writer, one block and a 64-block device batch: the output must be the input
+    import s3hc_lz4 as S
+
+    data = _chained_copies(BLOCK, seed)
+    for f in (engine.compress_frame(data), oracle.lz4flex_compress_frame(data),
+              lz4ref.compress_frame(data, block_size_id=4, linked=False)):
+        assert oracle.decompress_data(f) == data
+        assert _fast(lambda: engine.decompress_frames(f)) == data
+    big = b"".join(_chained_copies(BLOCK, 100 * seed + k) for k in range(300))
+    fr = [oracle.lz4flex_compress_frame(big[i:i + BLOCK]) for i in range(0, len(big), BLOCK)]
+    offs, lens, pos = [], [], 0
+    for f in fr:
+        offs.append(pos)
+        lens.append(len(f))
+        pos += len(f)
+    src = engine.upload(b"".join(fr))
+    n = len(fr)
+    plan = engine.plan_decode(offs, lens, [i * BLOCK for i in range(n)], [BLOCK] * n)
+    out = engine.alloc(n * BLOCK)
+    olen, ost = engine.alloc(4 * n), engine.alloc(4 * n)
+    engine.decode_dev(plan, src, out, olen, ost)
+    engine.sync()
+    assert ost.i32(n) == [0] * n
+    assert out.read(len(big)) == big
