@@ -16,7 +16,8 @@ cp gpurun_out/traffic/traffic.json $O/traffic.json
 timeout -k 10 300 python -u tools/config3.py > $O/config3.json 2>&1 || exit 1
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --blocks 131072 --steps 3 --warmup 1 > $O/bench_config5_slice_131072.json 2>&1 || exit 1
 timeout -k 10 300 python -u tools/lb.py > $O/lb_decode.json 2> $O/lb_decode.err || exit 1
-timeout -k 10 300 python -u tools/reader_time.py --mib 256 --depths 3,6 --reps 2 > $O/reader_fixed256k.txt 2>&1 || exit 1
+timeout -k 10 300 python -u tools/reader_time.py --mib 256 --depths 3,4 --reps 3 > $O/reader_fixed256k.txt 2>&1 || exit 1
 timeout -k 10 200 python -u tools/reader_small.py 200 1024 > $O/reader_small_1MiB.json 2>&1 || exit 1
 timeout -k 10 200 python -u tools/reader_small.py 50 8192 > $O/reader_small_8MiB.json 2>&1 || exit 1
+timeout -k 10 400 python -u tools/e2e.py --gib 8 > $O/e2e.json 2> $O/e2e.err || exit 1
 echo evidence-ok
