@@ -42,6 +42,8 @@
 namespace s3hc {
 #ifdef FPROF
 __device__ unsigned long long g_fprof[32];
+// per executor unit (u < 8192): start, end (s_memtime), HW_ID, XCC_ID
+__device__ unsigned long long g_uprof[8192][4];
 #endif
 namespace fst {
 constexpr uint32_t kMaxC = kFastMaxC;
@@ -577,6 +579,9 @@ __global__ __launch_bounds__(fst::kTT) void k_dtok(const uint8_t* __restrict__ s
 //   flush      whole 1 KiB pieces of the ring to HBM.
 // A sequence longer than kWin runs alone, wave-wide, in 1 KiB pieces (overlapping matches by
 // growing multiples of their period).
+#ifndef S3HC_DEX_PRIO  // 1: k_dexec's issue priority falls with its progress through the block
+#define S3HC_DEX_PRIO 1
+#endif
 #ifndef S3HC_FXOR  // 1: a window's output range is cleared, then or-written (0: masked writes)
 #define S3HC_FXOR 0
 #endif
@@ -921,6 +926,18 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
     uint32_t nrounds = 0;
     for (uint32_t w = 0; w < nwin; ++w) {
         [[maybe_unused]] uint64_t tq0 = FP_NOW();
+#if S3HC_DEX_PRIO
+        // issue priority falls with progress (3 in the first quarter of the block's windows, 0 in
+        // the last): the SIMD's arbiter otherwise favours its oldest wave, so the executors of a
+        // one-pass batch finish one after another and the last runs alone, its latency unhidden
+        {
+            const uint32_t pq = umin_(3u, (4u * w) / nwin);  // (wave-uniform; the priority is an immediate)
+            if (pq == 0) __builtin_amdgcn_s_setprio(3);
+            else if (pq == 1) __builtin_amdgcn_s_setprio(2);
+            else if (pq == 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
         const uint32_t nact = umin_(64u, N - 64u * w);
         const bool act = lane < nact;
         // ---- stage A: window w+3's records (two windows of lead); stage C: window w+1 unpacked,
@@ -1361,6 +1378,20 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
         FP_ADD(22, nwin);
         FP_ADD(23, nrounds);
         FP_ADD(24, 1);
+        // the spread of the units' lives (one pass holds the whole batch: the launch lasts as long
+        // as its slowest wave): the longest, a histogram, the first start and the last end
+        const uint64_t tend = FP_NOW(), tot = tend - te0;
+        atomicMax(&g_fprof[31], (unsigned long long)tot);
+        FP_ADD(tot < 600000u ? 12 : (tot < 900000u ? 13 : (tot < 1200000u ? 14 : 15)), 1);
+        atomicMax(&g_fprof[8], (unsigned long long)~te0);
+        atomicMax(&g_fprof[11], (unsigned long long)tend);
+        atomicMax(&g_fprof[9], (unsigned long long)nwin);
+        if (u < 8192u) {
+            g_uprof[u][0] = te0;
+            g_uprof[u][1] = tend;
+            g_uprof[u][2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+            g_uprof[u][3] = (unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
+        }
     }
 #endif
 }
@@ -1819,6 +1850,11 @@ hipError_t launch_fast_tok(const uint8_t* src, const DecBlock* blk, const DecUni
     return hipGetLastError();
 }
 #ifdef FPROF
+extern "C" int s3hc_diag_uprof(unsigned long long* out, int n) {
+    if (n > 8192) n = 8192;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_uprof), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
+}
 extern "C" int s3hc_diag_fprof(unsigned long long* out, int n, int reset) {
     if (n > 32) n = 32;
     if (hipDeviceSynchronize() != hipSuccess) return -1;

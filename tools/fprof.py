@@ -48,6 +48,42 @@ def main():
     out = {"k_dtok_per_wave_cycles": {n: round(v[i] / (4 * wg), 1) for i, n in TOK.items() if i != 10},
            "k_dtok_max_ovf_per_wave": round(v[10] / (4 * wg), 2),
            "k_dexec_per_unit": {n: round(v[i] / (v[24] or 1), 1) for i, n in EXE.items()}}
+    if v[31]:  # builds with the spread counters: one more launch alone (max / histogram / span of its units)
+        f(buf, 32, 1)
+        eng.decode_dev(dplan, d_frames, d_out, d_olen, d_ost)
+        eng.sync()
+        f(buf, 32, 0)
+        w = list(buf)
+        out["k_dexec_spread_one_launch"] = {
+            "max_unit_total": w[31], "avg_unit_total": round(w[21] / (w[24] or 1), 1), "max_windows": w[9],
+            "units_lt600k_lt900k_lt1200k_ge": [w[k] for k in (12, 13, 14, 15)],
+            "span_first_start_to_last_end": w[11] - ((~w[8]) & (2**64 - 1))}
+        if hasattr(L, "s3hc_diag_uprof"):  # per-unit lives with the SIMD / CU / XCD that ran them
+            import numpy as np
+            ub = (ctypes.c_ulonglong * (4 * nb))()
+            L.s3hc_diag_uprof(ub, nb)
+            U = np.frombuffer(ub, dtype=np.uint64).reshape(nb, 4).astype(np.int64)
+            life = U[:, 1] - U[:, 0]
+            hw, xcc = U[:, 2], U[:, 3] & 15
+            simd, cu, se = (hw >> 4) & 3, (hw >> 8) & 15, (hw >> 13) & 7
+            key = ((xcc * 8 + se) * 16 + cu) * 4 + simd
+            sp = {}
+            # per XCD: its clock's first start and last end (s_memtime is per XCD), mean and max life
+            for x in sorted(set(xcc.tolist())):
+                m = xcc == x
+                sp[f"xcd{x}"] = {"units": int(m.sum()), "span": int(U[m, 1].max() - U[m, 0].min()),
+                                 "life_mean": int(life[m].mean()), "life_max": int(life[m].max()),
+                                 "start_spread": int(U[m, 0].max() - U[m, 0].min())}
+            _, cnt = np.unique(key, return_counts=True)
+            order = np.argsort(key, kind="stable")
+            # within a SIMD: lives sorted by start, the rank of each wave's end
+            ranks = {}
+            for k in np.unique(key):
+                idx = np.where(key == k)[0]
+                ends = np.sort(U[idx, 1] - U[idx, 0].min())
+                ranks.setdefault(len(idx), []).append(ends.tolist())
+            out["k_dexec_units"] = {"per_xcd": sp, "waves_per_simd_hist": {int(a): int(b) for a, b in zip(*np.unique(cnt, return_counts=True))},
+                                    "simd_end_times_mean_by_rank": {n: [int(v) for v in np.mean(np.array(r), axis=0)] for n, r in ranks.items()}}
     print(json.dumps(out, indent=1))
 
 
