@@ -666,6 +666,7 @@ struct s3hc_ctx {
     std::mutex rpool_mu;
     std::vector<void*> rslot_pool;         // RSlot* (reader section)
     std::vector<hipStream_t> rqueue_pool;  // non-blocking queues of this device
+    std::vector<void*> rin_pool;           // PinnedBuf* (readers' input buffers)
     ~s3hc_ctx();
 };
 static void reader_pool_release(s3hc_ctx* ctx);
@@ -2088,6 +2089,7 @@ struct RSlot {
     std::vector<uint64_t> dst_off;
     hipEvent_t ev2 = nullptr;  // the batch's D2H of decoded bytes
     hipEvent_t ev3 = nullptr;  // the batch's deferred content checksums (second close) read back
+    hipEvent_t ev_in = nullptr;  // the batch's input copied out of the reader's (pinned) input buffer
     DevBuf d_v;                // second close: final statuses (i32[n]) and lengths (u32[n])
     PinnedBuf h_v;             // its final statuses
     int state = 0;          // 0 decoding, 1 copying decoded bytes to h_out, 2 ready
@@ -2115,6 +2117,7 @@ struct RSlot {
         if (ev) (void)hipEventDestroy(ev);
         if (ev2) (void)hipEventDestroy(ev2);
         if (ev3) (void)hipEventDestroy(ev3);
+        if (ev_in) (void)hipEventDestroy(ev_in);
     }
 };
 constexpr size_t kReaderPoolMax = 64;  // pooled slots (and queues) per context
@@ -2134,6 +2137,7 @@ RSlot* rslot_take(s3hc_ctx* c) {
     if (hipEventCreateWithFlags(&S->ev, hipEventDisableTiming) != hipSuccess) return nullptr;
     if (hipEventCreateWithFlags(&S->ev2, hipEventDisableTiming) != hipSuccess) return nullptr;
     if (hipEventCreateWithFlags(&S->ev3, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&S->ev_in, hipEventDisableTiming) != hipSuccess) return nullptr;
     return S.release();
 }
 // A pooled slot keeps buffers up to this size: one GET with large batches or 4 MiB blocks must
@@ -2184,10 +2188,36 @@ void rqueue_give(s3hc_ctx* c, hipStream_t q) {  // (q synchronised)
     (void)hipStreamDestroy(q);
 }
 }  // namespace
+// A reader's pinned input buffer: from its first context's pool (kept up to kReaderPoolKeep).
+static PinnedBuf* rin_take(s3hc_ctx* c) {
+    {
+        std::lock_guard<std::mutex> g(c->rpool_mu);
+        if (!c->rin_pool.empty()) {
+            PinnedBuf* b = (PinnedBuf*)c->rin_pool.back();
+            c->rin_pool.pop_back();
+            return b;
+        }
+    }
+    return new PinnedBuf;
+}
+static void rin_give(s3hc_ctx* c, PinnedBuf* b) {  // (no copy out of it in flight)
+    if (!b) return;
+    b->trim(kReaderPoolKeep);
+    {
+        std::lock_guard<std::mutex> g(c->rpool_mu);
+        if (c->rin_pool.size() < kReaderPoolMax) {
+            c->rin_pool.push_back(b);
+            return;
+        }
+    }
+    delete b;
+}
 static void reader_pool_release(s3hc_ctx* c) {
     std::lock_guard<std::mutex> g(c->rpool_mu);
     for (void* p : c->rslot_pool) delete (RSlot*)p;
     c->rslot_pool.clear();
+    for (void* p : c->rin_pool) delete (PinnedBuf*)p;
+    c->rin_pool.clear();
     (void)hipSetDevice(c->device);
     for (hipStream_t q : c->rqueue_pool) (void)hipStreamDestroy(q);
     c->rqueue_pool.clear();
@@ -2226,21 +2256,6 @@ extern "C" int s3hc_diag_check_batch_results(uint32_t n, const uint32_t* olen, c
     return check_batch_results(n, olen, status, dst_off, slot_total, good, bytes);
 }
 
-// std::allocator that leaves bytes uninitialised on resize (the reader's input buffer is
-// overwritten by the feed copy right after growing)
-template <typename T>
-struct NoInitAlloc : std::allocator<T> {
-    template <typename U>
-    struct rebind { using other = NoInitAlloc<U>; };
-    NoInitAlloc() = default;
-    template <typename U>
-    NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
-    template <typename U>
-    void construct(U* p) noexcept { ::new ((void*)p) U; }
-    template <typename U, typename... A>
-    void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
-};
-
 // Host-time accounting of the reader (S3HC_HOST_TRACE=1, diagnostics: printed at close)
 struct ReaderTrace {
     enum { FEED, WALK, STAGE, SUBMIT, ISSUE, WAIT, DELIVER, N };
@@ -2267,7 +2282,16 @@ struct s3hc_reader {
     std::vector<RSlot*> slots;        // S3HC_READER_SLOTS batches per queue (default 1; more queue
                                       // a queue's next batch behind its running one: measured slower)
     std::vector<int> inflight;  // slot indices in stream order (head may be ready / being read)
-    std::vector<uint8_t, NoInitAlloc<uint8_t>> in;  // buffered input (grown without zero-fill); undecoded bytes start at in_head (a frame boundary)
+    // buffered input, pinned (each batch's input is copied to the device straight out of it; the
+    // bytes a submitted batch reads are never moved or freed before its ev_in): undecoded bytes
+    // start at in_head (a frame boundary)
+    struct Input {
+        PinnedBuf* b = nullptr;  // (from the first context's pool)
+        size_t n = 0;
+        uint8_t* data() const { return b->p; }
+        size_t size() const { return n; }
+        void clear() { n = 0; }
+    } in;
     size_t in_head = 0;
     bool finished = false;
     int error = S3HC_OK;        // reported once every byte before it was read
@@ -2312,10 +2336,11 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     const size_t o_fo = 0, o_bb = al(8ull * n), o_oo = o_bb + al(8ull * n), o_nb = o_oo + al(8ull * n),
                  o_w = o_nb + al(4ull * n), o_blk = o_w + al(4ull * n), o_u = o_blk + al(sizeof(DecBlock) * nbk),
                  nmeta = o_u + al(sizeof(DecUnit) * nu);
-    // one host-to-device copy per batch: the input, then (256-byte aligned) the tables
+    // two host-to-device copies per batch: the input straight out of the reader's pinned input
+    // buffer, then (256-byte aligned) the tables from the slot's
     const size_t o_meta = (nin + 255) & ~(size_t)255;
-    HIPCHK(S.h_in.ensure(o_meta + nmeta));
-    uint8_t* m = S.h_in.p + o_meta;
+    HIPCHK(S.h_in.ensure(nmeta));
+    uint8_t* m = S.h_in.p;
     for (uint32_t f = 0; f < n; ++f) {
         const HFrame& F = W.frames[f];
         ((uint64_t*)(m + o_fo))[f] = F.pos - F0.pos;
@@ -2336,10 +2361,6 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
     if (nu) memcpy(m + o_u, units.data(), sizeof(DecUnit) * nu);
     hipStream_t st = S.st;
     HIPCHK(hipSetDevice(S.ctx->device));
-    {
-        RTimer T_(r->tr, ReaderTrace::STAGE);
-        par_memcpy(S.h_in.p, r->in.data() + r->in_head + F0.pos, nin);
-    }
     RTimer T_(r->tr, ReaderTrace::SUBMIT);
     ++r->tr.batches;
     HIPCHK(S.d_in.ensure(o_meta + nmeta + 64));
@@ -2357,7 +2378,9 @@ static int reader_submit(s3hc_reader* r, RSlot& S, const HWalk& W, size_t nf) {
         // large blocks of the batch (the host walk knows every block)
         HIPCHK(prepare_host_launch(S.lb, mb, nbk, units.data(), nu, tok_entries));
     }
-    HIPCHK(hipMemcpyAsync(S.d_in.p, S.h_in.p, o_meta + nmeta, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.d_in.p, r->in.data() + r->in_head + F0.pos, nin, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(S.d_in.as<uint8_t>() + o_meta, S.h_in.p, nmeta, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(S.ev_in, st));
     const uint8_t* src = S.d_in.as<uint8_t>();
     const uint8_t* dm = S.d_in.as<uint8_t>() + o_meta;
     const DecBlock* d_blk = (const DecBlock*)(dm + o_blk);
@@ -2670,6 +2693,7 @@ static int reader_new(s3hc_ctx* const* ctxs, int nctx, size_t batch_bytes, int d
     r->ctx = ctxs[0];
     r->ctxs.assign(ctxs, ctxs + nctx);
     for (auto* c : r->ctxs) ctx_retain(c);  // released by ~s3hc_reader
+    r->in.b = rin_take(r->ctx);
     ReaderLock lk(r.get());
     r->batch_bytes = batch_bytes;
     r->batch_max = batch_bytes;
@@ -2710,16 +2734,29 @@ extern "C" int s3hc_reader_feed(s3hc_reader* r, const uint8_t* src, size_t n) {
         if (!r || (!src && n)) return fail(S3HC_INVALID_ARG, "bad arguments");
         if (r->finished) return fail(S3HC_INVALID_ARG, "reader already finished");
         if (r->error) return S3HC_OK;  // the stream has ended with an error; input is ignored
-        if (r->in_head && r->in_head >= r->in.size() / 2) {  // drop consumed input (amortized)
+        auto& in = r->in;
+        const bool compact = r->in_head && r->in_head >= in.n / 2;  // drop consumed input (amortized)
+        const bool grow = (compact ? in.n - r->in_head : in.n) + n > in.b->cap;
+        if (compact || grow) {
+            // the bytes move (or the buffer is replaced): every submitted batch's input copy first
             RTimer T_(r->tr, ReaderTrace::FEED);
-            r->in.erase(r->in.begin(), r->in.begin() + r->in_head);
+            for (int i : r->inflight) {
+                RSlot& S = *r->slots[i];
+                HIPCHK(hipSetDevice(S.ctx->device));
+                HIPCHK(hipEventSynchronize(S.ev_in));
+            }
+        }
+        if (compact) {
+            RTimer T_(r->tr, ReaderTrace::FEED);
+            memmove(in.b->p, in.b->p + r->in_head, in.n - r->in_head);
+            in.n -= r->in_head;
             r->in_head = 0;
         }
         {
             RTimer T_(r->tr, ReaderTrace::FEED);
-            const size_t old = r->in.size();
-            r->in.resize(old + n);
-            par_memcpy(r->in.data() + old, src, n);
+            HIPCHK(in.b->ensure_keep(in.n + n, in.n));
+            par_memcpy(in.b->p + in.n, src, n);
+            in.n += n;
         }
         ReaderLock g(r);
         int rc = reader_advance(r);
@@ -2822,6 +2859,7 @@ s3hc_reader::~s3hc_reader() {
     for (RSlot* S : slots) rslot_give(S);
     for (size_t q = 0; q < queues.size(); ++q)
         if (queues[q]) rqueue_give(ctxs[q % nc], queues[q]);
+    rin_give(ctx, in.b);  // (every queue synchronised above)
     for (auto* c : ctxs) ctx_release(c);  // (the last reference frees a destroyed context)
 }
 extern "C" void s3hc_reader_close(s3hc_reader* r) {
