@@ -42,7 +42,10 @@
 namespace s3hc {
 #ifdef FPROF
 __device__ unsigned long long g_fprof[32];
-// per executor unit (u < 8192): start, end (s_memtime), HW_ID, XCC_ID
+#endif
+#if defined(FPROF) || (defined(S3HC_UPROF) && S3HC_UPROF)
+#define UPROF 1
+// per executor unit (u < 8192): start, end (s_memrealtime, 100 MHz), HW_ID, XCC_ID | sweeps << 8 | windows << 32
 __device__ unsigned long long g_uprof[8192][4];
 #endif
 namespace fst {
@@ -922,6 +925,9 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
         lsh_c = (lit - (uint32_t)q0) | ((lit + 16u - (uint32_t)q1) << 8);
     }
     [[maybe_unused]] const uint64_t te0 = FP_NOW();
+#ifdef UPROF
+    const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();  // (constant 100 MHz clock, chip-wide)
+#endif
     [[maybe_unused]] uint64_t tsum[6] = {0, 0, 0, 0, 0, 0};
     uint32_t nrounds = 0;
     for (uint32_t w = 0; w < nwin; ++w) {
@@ -1386,12 +1392,15 @@ __device__ __forceinline__ void dexec_unit(const uint32_t u, const uint8_t* __re
         atomicMax(&g_fprof[8], (unsigned long long)~te0);
         atomicMax(&g_fprof[11], (unsigned long long)tend);
         atomicMax(&g_fprof[9], (unsigned long long)nwin);
-        if (u < 8192u) {
-            g_uprof[u][0] = te0;
-            g_uprof[u][1] = tend;
-            g_uprof[u][2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-            g_uprof[u][3] = (unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20);  // XCC_ID
-        }
+    }
+#endif
+#ifdef UPROF
+    if (lane == 0 && u < 8192u) {
+        g_uprof[u][0] = tr0;
+        g_uprof[u][1] = __builtin_amdgcn_s_memrealtime();
+        g_uprof[u][2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_ID
+        g_uprof[u][3] = (unsigned long long)(__builtin_amdgcn_s_getreg((15 << 11) | 20) & 15u) |  // XCC_ID
+                        ((unsigned long long)nrounds << 8) | ((unsigned long long)nwin << 32);
     }
 #endif
 }
@@ -1849,12 +1858,14 @@ hipError_t launch_fast_tok(const uint8_t* src, const DecBlock* blk, const DecUni
                        unit_lb, a, maxc);
     return hipGetLastError();
 }
-#ifdef FPROF
+#ifdef UPROF
 extern "C" int s3hc_diag_uprof(unsigned long long* out, int n) {
     if (n > 8192) n = 8192;
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_uprof), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
 }
+#endif
+#ifdef FPROF
 extern "C" int s3hc_diag_fprof(unsigned long long* out, int n, int reset) {
     if (n > 32) n = 32;
     if (hipDeviceSynchronize() != hipSuccess) return -1;

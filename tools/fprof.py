@@ -82,6 +82,20 @@ def main():
                 idx = np.where(key == k)[0]
                 ends = np.sort(U[idx, 1] - U[idx, 0].min())
                 ranks.setdefault(len(idx), []).append(ends.tolist())
+            sweeps, wins = (U[:, 3] >> 8) & 0xFFFFFF, U[:, 3] >> 32
+            # what a unit's life follows: its XCD, its sweeps, its windows, its index mod 8
+            out["k_dexec_units_corr"] = {
+                "life_vs_sweeps": round(float(np.corrcoef(life, sweeps)[0, 1]), 3),
+                "life_vs_windows": round(float(np.corrcoef(life, wins)[0, 1]), 3),
+                "sweeps_mean_by_xcd": {int(x): round(float(sweeps[xcc == x].mean()), 1) for x in sorted(set(xcc.tolist()))},
+                "life_mean_by_unit_mod8": [int(life[np.arange(nb) % 8 == k].mean()) for k in range(8)],
+                "life_mean_by_unit_quarter": [int(life[(np.arange(nb) * 4) // nb == k].mean()) for k in range(4)]}
+            t0 = U[:, 0].min()
+            out["k_dexec_units_realtime_us"] = {  # s_memrealtime: 100 MHz, one clock for the chip
+                "launch_span": round((U[:, 1].max() - t0) / 100, 1),
+                "per_xcd_first_start_last_end_mean_life": {int(x): [round((U[xcc == x, 0].min() - t0) / 100, 1), round((U[xcc == x, 1].max() - t0) / 100, 1), round(float(life[xcc == x].mean()) / 100, 1)] for x in sorted(set(xcc.tolist()))},
+                "start_quartiles": [round(float(np.percentile(U[:, 0] - t0, q)) / 100, 1) for q in (0, 25, 50, 75, 100)],
+                "end_quartiles": [round(float(np.percentile(U[:, 1] - t0, q)) / 100, 1) for q in (0, 25, 50, 75, 100)]}
             out["k_dexec_units"] = {"per_xcd": sp, "waves_per_simd_hist": {int(a): int(b) for a, b in zip(*np.unique(cnt, return_counts=True))},
                                     "simd_end_times_mean_by_rank": {n: [int(v) for v in np.mean(np.array(r), axis=0)] for n, r in ranks.items()}}
     print(json.dumps(out, indent=1))
