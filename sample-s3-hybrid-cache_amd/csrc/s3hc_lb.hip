@@ -97,7 +97,9 @@ constexpr uint32_t VALF = 0x80000000u;         // k_lb_run pointer-array entry o
 // diagnostic builds: k_lb_run phase times (s_memtime sums of every workgroup's thread 0):
 // 0 owners, 1 classify + literal loads, 2 ring/pointer stores, 3 next step's sequences,
 // 4 chain jumping, 5 flush, 6 -, 7 steps, 8 jump rounds, 9 loop top
-__device__ unsigned long long g_lbprof[20];  // 12..17: k_lb_mark phases (thread 0 of each chunk)
+__device__ unsigned long long g_lbprof[32];  // 12..17: k_lb_mark phases (thread 0 of each chunk); walks:
+// 12..15 k_lbt_walk phases, 16..19 k_lbt_mark phases, 20..23 per-chunk maxima of walk-2 hops, first-
+// position walk hops, entry-path hops and walk-2 re-marking hops (summed over chunks), 24 chunks
 #endif
 
 namespace {
@@ -125,6 +127,7 @@ __device__ __forceinline__ T wave_incl_add(T x, int) {
     return x;
 }
 __device__ __forceinline__ uint32_t lb_umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t umin32_lb(uint32_t a, uint32_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
     x = lb_umax(x, lb_dpp<0x111, 0xF>(x));
     x = lb_umax(x, lb_dpp<0x112, 0xF>(x));
@@ -422,6 +425,370 @@ __global__ __launch_bounds__(256) void k_lb_gran(const uint8_t* __restrict__ src
     A.nzg[(size_t)c * kGpc + gi] = sm[gi];
 }
 
+#if S3HC_LB_TOKV2
+// ---------------------------------------------------------------- chunk chains by segment walks
+// (round 6; replaces k_lb_exit / k_lb_entry / k_lb_mark's next-token-at-every-position tables and
+// their pointer doubling over 8 Ki positions, which cost 1.1 of 2.9 ms at 256 reference frames)
+//
+// A chunk's kLbWalkT threads each take a segment of segL = ceil(n / kLbWalkT) positions and walk
+// the token chain from its first position (speculatively: it may not be a token), marking every
+// position visited inside the segment (walk 1); from the first position past the segment each
+// walk goes on until it lands on a position some walk 1 marked (it merges with that segment's
+// walk from there on) or leaves the chunk (walk 2). The merges link the segments: a chain from any
+// position reaches, after the few hops until its first marked position, the chain of that
+// position's segment.
+//   k_lbt_walk   the walks; per segment (pointer doubling over the segments, 8 levels) the
+//                position where its chain leaves the chunk (or END / BAD), and from it the exits
+//                of the chunk's first kLbFirstX positions (where a chain enters a chunk unless a
+//                literal run spans more than kLbFirstX bytes into it). Marks, exits and both walks'
+//                ends go to A.J0 for the next two kernels.
+//   k_lbt_entry  per block, over its chunks in order: the true chain's entry into each chunk, one
+//                table load per chunk (a walk over the chunk's stored marks otherwise);
+//   k_lbt_mark   from its entry: the segments the true chain passes through (reachability by
+//                doubling from the entry's first marked position); the true tokens are the reached
+//                segments' walk-1 marks from their first true token on, their walk-2 paths and the
+//                entry's path to its first mark; then the records, exactly as k_lb_mark wrote them.
+// Walks use lb_next (the lz4_flex parse rules, exact for long runs and malformed tokens), so the
+// chain's nodes, its malformed last token and every record are the ones the doubling tables gave.
+namespace lb {
+constexpr uint32_t kWT = kLbWalkT;
+constexpr uint32_t kWLv = 8;  // doubling levels: chains over <= kWT segments
+static_assert((1u << kWLv) >= kWT, "doubling covers every segment chain");
+static_assert(kLbChunk % (32u * kWT) == 0, "whole bitmap words per walking thread");
+constexpr uint32_t kWW = kLbChunk / 32u / kWT;  // bitmap words per thread
+constexpr uint32_t kBW = kLbChunk / 32u;        // bitmap words per chunk
+// per chunk in A.J0 (as u32): marks, then per segment the chain exit, walk 1's end X, walk 2's end M
+constexpr uint32_t kGEx = kBW, kGX = kBW + kWT, kGM = kBW + 2u * kWT;
+static_assert(2u * (kBW + 3u * kWT) == kLbJ0PerChunk, "A.J0 layout");
+}  // namespace lb
+
+namespace {
+// Stage block bytes [cs, cs + ns) with aligned 16-byte loads, all of a thread's loads in flight
+// before its LDS stores (one HBM round trip); returns s with s[i] = byte cs + i. raw: 16-aligned,
+// >= ns + 32 bytes. Loads stay inside the 16-byte granules holding block bytes.
+template <uint32_t NT>
+__device__ __forceinline__ const uint8_t* lb_stage16(const uint8_t* g, uint32_t cs, uint32_t ns, uint8_t* raw) {
+    const uintptr_t a0 = (uintptr_t)(g + cs);
+    const uint32_t mis = (uint32_t)(a0 & 15u);
+    const uint4* av = (const uint4*)(a0 - mis);
+    const uint32_t nv = (mis + ns + 15u) >> 4;
+    constexpr uint32_t kL = (lb::kStage + 30u) / 16u / NT + 1u;
+    uint4 x[kL];
+#pragma unroll
+    for (uint32_t k = 0; k < kL; ++k) {
+        const uint32_t d = threadIdx.x + k * NT;
+        x[k] = d < nv ? av[d] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kL; ++k) {
+        const uint32_t d = threadIdx.x + k * NT;
+        if (d < nv) ((uint4*)raw)[d] = x[k];
+    }
+    return raw + mis;
+}
+}  // namespace
+
+#ifdef S3HC_LBPROF
+#define WK_T(k) { __syncthreads(); const uint64_t n_ = __builtin_amdgcn_s_memtime(); if (threadIdx.x == 0) atomicAdd(&g_lbprof[12 + (k)], (unsigned long long)(n_ - wt_)); wt_ = n_; }
+#define WK_MAX(k, h) { atomicMax(&wmx_[k], (h)); }
+#define WK_FLUSH() { __syncthreads(); if (threadIdx.x < 4) atomicAdd(&g_lbprof[20 + threadIdx.x], (unsigned long long)wmx_[threadIdx.x]); if (threadIdx.x == 0) atomicAdd(&g_lbprof[24], 1ull); }
+#define WK_INIT() __shared__ uint32_t wmx_[4]; if (threadIdx.x < 4) wmx_[threadIdx.x] = 0; uint64_t wt_ = __builtin_amdgcn_s_memtime();
+#define WK_CNT(x) ++(x)
+#else
+#define WK_T(k)
+#define WK_MAX(k, h)
+#define WK_FLUSH()
+#define WK_INIT()
+#define WK_CNT(x)
+#endif
+__global__ __launch_bounds__(lb::kWT) void k_lbt_walk(const uint8_t* __restrict__ src, LbArgs A) {
+    using namespace lb;
+    WK_INIT()
+    __shared__ __attribute__((aligned(16))) uint8_t raw[kStage + 32];
+    __shared__ uint32_t bits[kBW];
+    __shared__ uint16_t Jg[2][kWT + 1];  // successor segment of a walk (kWT: it left the chunk)
+    __shared__ uint32_t ex[2][kWT + 1];  // chain exit, once Jg is terminal
+    const uint32_t c = blockIdx.x;
+    const uint32_t g = threadIdx.x;
+    if (c >= A.ctl->nchunks) return;
+    const LbBlock B = A.lbt[A.chunk_blk[c]];
+    const uint32_t cs = (c - B.chunk0) * kLbChunk;
+    const uint32_t n = B.C - cs < kLbChunk ? B.C - cs : kLbChunk;
+    const uint32_t CE = cs + n;
+    const LbView v = lb_view(src, B, A.nzg, cs, lb_stage16<kWT>(src + B.src_off, cs, B.C - cs < kStage ? B.C - cs : kStage, raw));
+#pragma unroll
+    for (uint32_t k = 0; k < kWW; ++k) bits[g + k * kWT] = 0u;
+    __syncthreads();
+    WK_T(0)
+    auto marked = [&](uint32_t P) -> bool {  // P in [cs, CE)
+        const uint32_t r = P - cs;
+        return ((bits[r >> 5] >> (r & 31u)) & 1u) != 0u;
+    };
+    // ---- walk 1: the segment's positions on the chain from its first position
+    const uint32_t segL = (n + kWT - 1u) / kWT;
+    const uint32_t s0 = cs + (g * segL < n ? g * segL : n), s1 = cs + ((g + 1u) * segL < n ? (g + 1u) * segL : n);
+    const bool live = s0 < s1;
+    uint32_t X = NONE;  // first chain position past the segment, END or BAD
+    if (live) {
+        // the walk starts kLbWalkLead segments early (unmarked there): by the segment it has mostly
+        // fallen in with the token chain, so the walks of earlier segments merge into its marks
+        // within a few hops (walk 2's longest path per chunk 21.8 -> see DESIGN 4b)
+        uint32_t P = s0 - cs >= kLbWalkLead * segL ? s0 - kLbWalkLead * segL : cs;
+        for (;;) {
+            if (P >= s0) atomicOr(&bits[(P - cs) >> 5], 1u << ((P - cs) & 31u));
+            const uint32_t nx = lb_next(v, P);
+            if (nx >= s1) { X = nx; break; }  // (END / BAD compare above every position)
+            P = nx;
+        }
+    }
+    __syncthreads();
+    WK_T(1)
+    // ---- walk 2: until a marked position (merge) or out of the chunk
+    uint32_t M = X;
+    [[maybe_unused]] uint32_t nh2 = 0;
+    if (live)
+        while (M < CE) {  // (the mark and the next token are read together)
+            const bool mk = marked(M);
+            const uint32_t nx = lb_next(v, M);
+            if (mk) break;
+            M = nx;
+            WK_CNT(nh2);
+        }
+    WK_MAX(0, nh2)
+    WK_T(2)
+    Jg[0][g] = (uint16_t)(live && M < CE ? (M - cs) / segL : kWT);
+    ex[0][g] = live ? (M < CE ? 0u : M) : NONE;
+    if (g == 0) {
+        Jg[0][kWT] = Jg[1][kWT] = (uint16_t)kWT;
+        ex[0][kWT] = ex[1][kWT] = NONE;
+    }
+    __syncthreads();
+    // ---- the chain exit of every segment (pointer doubling: the exit is carried along)
+#pragma unroll
+    for (uint32_t k = 0; k < kWLv; ++k) {
+        const uint32_t j = Jg[k & 1][g];
+        uint32_t jn = (uint32_t)kWT, en = ex[k & 1][g];
+        if (j != kWT) { jn = Jg[k & 1][j]; en = ex[k & 1][j]; }
+        Jg[(k + 1) & 1][g] = (uint16_t)jn;
+        ex[(k + 1) & 1][g] = en;
+        __syncthreads();
+    }
+    const uint32_t* exf = ex[kWLv & 1];
+    uint32_t* gb = (uint32_t*)(A.J0 + (size_t)c * kLbJ0PerChunk);
+#pragma unroll
+    for (uint32_t k = 0; k < kWW; ++k) gb[g + k * kWT] = bits[g + k * kWT];
+    gb[kGEx + g] = exf[g];
+    gb[kGX + g] = X;
+    gb[kGM + g] = M;
+    WK_T(3)
+    if (g < kLbFirstX && g < n) {
+        uint32_t P = cs + g;
+        [[maybe_unused]] uint32_t nhf = 0;
+        while (P < CE) {
+            const bool mk = marked(P);
+            const uint32_t nx = lb_next(v, P);
+            if (mk) break;
+            P = nx;
+            WK_CNT(nhf);
+        }
+        WK_MAX(1, nhf)
+        A.E[(size_t)c * kLbFirstX + g] = P < CE ? exf[(P - cs) / segL] : P;
+    }
+    WK_FLUSH()
+}
+
+__global__ __launch_bounds__(lb::kWT) void k_lbt_mark(const uint8_t* __restrict__ src, LbArgs A) {
+    using namespace lb;
+    __shared__ __attribute__((aligned(16))) uint8_t raw[kStage + 32];
+    __shared__ uint32_t bits[kBW];
+    __shared__ uint16_t Jg[2][kWT + 1];
+    __shared__ uint8_t reach[kWT + 1];  // the true chain passes through the segment
+    __shared__ uint16_t svfrom[kWT];    // a reached segment's first true token (chunk-relative)
+    __shared__ uint16_t tokpos[kTokSlot];
+    __shared__ uint32_t shc[4];
+    __shared__ uint64_t shs[4];
+    __shared__ uint32_t sm0;            // the entry path's first marked position
+    __shared__ uint32_t bad_s;
+    const uint32_t c = blockIdx.x;
+    const uint32_t g = threadIdx.x;
+    if (c >= A.ctl->nchunks) return;
+    WK_INIT()
+    const uint32_t e = A.entry[c];
+    if (e == NONE) {  // no token of the block starts in this chunk
+        if (g == 0) { A.ntok[c] = 0; A.slsum[c] = 0; A.badrel[c] = NONE; }
+        return;
+    }
+    const LbBlock B = A.lbt[A.chunk_blk[c]];
+    const uint32_t cs = (c - B.chunk0) * kLbChunk;
+    const uint32_t n = B.C - cs < kLbChunk ? B.C - cs : kLbChunk;
+    const uint32_t CE = cs + n;
+    // k_lbt_walk's marks and walk ends (loads issued before the staging: both round trips overlap)
+    const uint32_t* gb = (const uint32_t*)(A.J0 + (size_t)c * kLbJ0PerChunk);
+    uint32_t bw[kWW];
+#pragma unroll
+    for (uint32_t k = 0; k < kWW; ++k) bw[k] = gb[g + k * kWT];
+    const uint32_t X = gb[kGX + g], M = gb[kGM + g];
+    const LbView v = lb_view(src, B, A.nzg, cs, lb_stage16<kWT>(src + B.src_off, cs, B.C - cs < kStage ? B.C - cs : kStage, raw));
+#pragma unroll
+    for (uint32_t k = 0; k < kWW; ++k) bits[g + k * kWT] = bw[k];
+    const uint32_t segL = (n + kWT - 1u) / kWT;
+    const uint32_t s0 = cs + (g * segL < n ? g * segL : n), s1 = cs + ((g + 1u) * segL < n ? (g + 1u) * segL : n);
+    const bool live = s0 < s1;
+    Jg[0][g] = (uint16_t)(live && M < CE ? (M - cs) / segL : kWT);
+    svfrom[g] = (uint16_t)0xFFFFu;
+    reach[g] = 0;
+    if (g == 0) {
+        Jg[0][kWT] = Jg[1][kWT] = (uint16_t)kWT;
+        reach[kWT] = 0;
+        bad_s = NONE;
+    }
+    __syncthreads();
+    WK_T(4)
+    auto marked = [&](uint32_t P) -> bool {  // P in [cs, CE)
+        const uint32_t r = P - cs;
+        return ((bits[r >> 5] >> (r & 31u)) & 1u) != 0u;
+    };
+    auto mark = [&](uint32_t P) {
+        const uint32_t r = P - cs;
+        atomicOr(&bits[r >> 5], 1u << (r & 31u));
+    };
+    // ---- the true chain: from the entry to its first marked position m0, then the segment of
+    // m0 and every segment reachable from it by merges
+    const uint32_t E0 = cs + e;
+    if (g == 0) {
+        uint32_t P = E0;
+        [[maybe_unused]] uint32_t nhe = 0;
+        while (P < CE && !marked(P)) { P = lb_next(v, P); WK_CNT(nhe); }
+        WK_MAX(2, nhe)
+        sm0 = P;
+        if (P < CE) {
+            const uint32_t h0 = (P - cs) / segL;
+            reach[h0] = 1;
+            svfrom[h0] = (uint16_t)(P - cs);
+        }
+    }
+    __syncthreads();
+    const uint32_t m0 = sm0;
+#pragma unroll
+    for (uint32_t k = 0; k < kWLv; ++k) {
+        const uint32_t h = Jg[k & 1][g];
+        if (reach[g]) reach[h] = 1;
+        Jg[(k + 1) & 1][g] = Jg[k & 1][h];
+        __syncthreads();
+    }
+    WK_T(5)
+    // a reached segment hands its merge point to its successor (that segment's first true token)
+    if (reach[g] && live && M < CE) svfrom[(M - cs) / segL] = (uint16_t)(M - cs);
+    __syncthreads();
+    // marks before a reached segment's first true token are speculative; a segment off the chain
+    // is cleared whole
+    const uint32_t vf = svfrom[g];
+    const bool valid = vf != 0xFFFFu;
+    if (live) {
+        const uint32_t c1 = valid ? vf : s1 - cs;  // clear [s0, c1) (chunk-relative)
+        for (uint32_t q = s0 - cs; q < c1;) {
+            const uint32_t w = q >> 5, lo = q & 31u, hi = umin32_lb(32u, c1 - (w << 5));
+            const uint32_t mk = (hi == 32u ? ~0u : (1u << hi) - 1u) & (~0u << lo);
+            atomicAnd(&bits[w], ~mk);
+            q = (w + 1u) << 5;
+        }
+    }
+    __syncthreads();
+    // the chain's tokens off the marks: a reached segment's walk-2 path and the entry's path
+    [[maybe_unused]] uint32_t nhm = 0;
+    if (valid && live)
+        for (uint32_t q = X; q < CE && q != M; q = lb_next(v, q)) { mark(q); WK_CNT(nhm); }
+    WK_MAX(3, nhm)
+    if (g == 0)
+        for (uint32_t q = E0; q < CE && q != m0; q = lb_next(v, q)) mark(q);
+    __syncthreads();
+    WK_T(6)
+    // ---- records in stream order (k_lb_mark's layout): thread g lists the marks of its bitmap
+    // words at their rank, then parses list entries g, g + kWT, ...
+    uint32_t nm = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kWW; ++k) nm += (uint32_t)__builtin_popcount(bits[g * kWW + k]);
+    uint32_t mtot;
+    uint32_t rank = wg_excl_add<uint32_t, kWT / 64>(nm, shc, mtot);
+#pragma unroll
+    for (uint32_t k = 0; k < kWW; ++k) {
+        uint32_t w = bits[g * kWW + k];
+        while (w) {
+            tokpos[rank++] = (uint16_t)(32u * (g * kWW + k) + (uint32_t)__builtin_ctz(w));
+            w &= w - 1u;
+        }
+    }
+    __syncthreads();
+    uint32_t cnt = 0;
+    uint64_t sl = 0;
+    for (uint32_t idx = g; idx < mtot; idx += kWT) {
+        const uint32_t r = tokpos[idx];
+        const LbTok T = lb_token(v, cs + r);
+        if (T.nxt == BAD) {
+            bad_s = r;  // the chain's last node (unique)
+        } else {
+            const uint64_t s1v = (uint64_t)T.ll + T.ml;
+            sl += s1v < (uint64_t)B.limit + 1u ? s1v : (uint64_t)B.limit + 1u;
+            A.trec[(size_t)c * kTokSlot + idx] =
+                make_uint4(T.lit | (T.nxt == END ? 0x80000000u : 0u), T.ll, T.ml, T.off);  // lit < 2^31
+            ++cnt;
+        }
+    }
+    uint32_t ctot;
+    uint64_t stot;
+    (void)wg_excl_add<uint32_t, kWT / 64>(cnt, shc, ctot);
+    (void)wg_excl_add<uint64_t, kWT / 64>(sl, shs, stot);
+    if (g == 0) {
+        A.ntok[c] = ctot;
+        A.slsum[c] = stot < 0xFFFFFFFFull ? (uint32_t)stot : 0xFFFFFFFFu;
+        A.badrel[c] = bad_s;
+    }
+    WK_T(7)
+    WK_FLUSH()
+}
+#undef WK_T
+#undef WK_MAX
+#undef WK_FLUSH
+#undef WK_INIT
+#undef WK_CNT
+
+// Per block, serial over its chunks: the true chain's entry into each chunk (chunk-relative; NONE
+// for chunks a literal run skips), from k_lbt_walk's exit tables.
+__global__ void k_lbt_entry(const uint8_t* __restrict__ src, LbArgs A) {
+    using namespace lb;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.ctl->nlb) return;
+    const LbBlock B = A.lbt[i];
+    uint32_t e = 0, c = 0;
+    while (c < B.nchunks && e < B.C) {
+        const uint32_t cc = e / kLbChunk;
+        for (; c < cc; ++c) A.entry[B.chunk0 + c] = NONE;
+        const uint32_t cs = cc * kLbChunk, rel = e - cs;
+        const size_t ch = (size_t)B.chunk0 + cc;
+        A.entry[ch] = rel;
+        c = cc + 1u;
+        if (rel < kLbFirstX) {
+            e = A.E[ch * kLbFirstX + rel];
+        } else {
+            // a literal run reached past the table: walk over the chunk's marks from HBM
+            const uint32_t* gb = (const uint32_t*)(A.J0 + ch * kLbJ0PerChunk);
+            const uint32_t n = B.C - cs < kLbChunk ? B.C - cs : kLbChunk, CE = cs + n;
+            const uint32_t segL = (n + kWT - 1u) / kWT;
+            LbView v;
+            v.g = src + B.src_off; v.s = nullptr; v.nzg = A.nzg; v.cs = cs; v.ns = 0; v.C = B.C;
+            v.chunk0 = B.chunk0; v.nch = B.nchunks;
+            uint32_t P = e;
+            while (P < CE) {
+                const uint32_t r = P - cs;
+                if ((gb[r >> 5] >> (r & 31u)) & 1u) break;
+                P = lb_next(v, P);
+            }
+            e = P < CE ? gb[kGEx + (P - cs) / segL] : P;
+        }
+    }
+    for (; c < B.nchunks; ++c) A.entry[B.chunk0 + c] = NONE;
+}
+#else  // !S3HC_LB_TOKV2
 // ---------------------------------------------------------------- chunk exits
 __global__ __launch_bounds__(1024) void k_lb_exit(const uint8_t* __restrict__ src, LbArgs A) {
     using namespace lb;
@@ -639,6 +1006,7 @@ __global__ __launch_bounds__(1024) void k_lb_mark(const uint8_t* __restrict__ sr
         A.badrel[c] = bad_s;
     }
 }
+#endif  // S3HC_LB_TOKV2
 
 // ---------------------------------------------------------------- sequence table
 __device__ __forceinline__ uint32_t lb_check(uint64_t produced, uint32_t ll, uint32_t ml, uint32_t off, bool last,
@@ -654,55 +1022,68 @@ __device__ __forceinline__ uint32_t lb_check(uint64_t produced, uint32_t ll, uin
     return st;
 }
 
-__global__ __launch_bounds__(1024) void k_lb_seq(const uint8_t* __restrict__ src, LbArgs A) {
+// 256 threads per chunk, thread t taking the contiguous ranks [t K, t K + K), K = ceil(ntok / 256)
+// <= kSeqK, every record load of a pass in flight at once (round 6: the 1024-thread form with three
+// records per thread held two workgroups per CU, so a launch of 13,824 chunks ran in 27
+// latency-bound rounds: 165 us at 256 reference frames)
+namespace lb {
+constexpr uint32_t kSeqT = 256;
+constexpr uint32_t kSeqK = (kTokSlot + kSeqT - 1u) / kSeqT;
+}
+__global__ __launch_bounds__(lb::kSeqT) void k_lb_seq(const uint8_t* __restrict__ src, LbArgs A) {
     using namespace lb;
-    __shared__ uint64_t shs[16];
+    __shared__ uint64_t shs[kSeqT / 64];
     const uint32_t c = blockIdx.x;
     if (c >= A.ctl->nchunks || A.entry[c] == NONE) return;
     const uint32_t bi = A.chunk_blk[c];
     const LbBlock B = A.lbt[bi];
     const uint32_t cs = (c - B.chunk0) * kLbChunk;
     const uint32_t ntc = A.ntok[c];
-    // thread t: the chunk's tokens [3t, 3t + 3) (records written by k_lb_mark, in stream order)
-    static_assert(3 * kT >= kTokSlot, "three records per thread cover a chunk");
-    const uint32_t i0 = 3 * threadIdx.x;
+    const uint32_t K = (ntc + kSeqT - 1u) / kSeqT;
+    const uint32_t i0 = umin32_lb(ntc, K * threadIdx.x), nk = umin32_lb(ntc, i0 + K) - i0;
+    const uint4* tr = A.trec + (size_t)c * kTokSlot + i0;
+    auto clampsl = [&](uint32_t ll, uint32_t ml) -> uint32_t {
+        const uint64_t s1 = (uint64_t)ll + ml;
+        return s1 < (uint64_t)B.limit + 1u ? (uint32_t)s1 : B.limit + 1u;
+    };
+    uint2 lm[kSeqK];
+#pragma unroll
+    for (uint32_t k = 0; k < kSeqK; ++k) lm[k] = k < nk ? *(const uint2*)((const uint32_t*)&tr[k] + 1) : make_uint2(0, 0);
     uint64_t sl = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < 3; ++i) {
-        const uint32_t* rw = (const uint32_t*)&A.trec[(size_t)c * kTokSlot + i0 + i];
-        const uint64_t s1 = i0 + i < ntc ? (uint64_t)rw[1] + rw[2] : 0u;
-        sl += s1 < (uint64_t)B.limit + 1u ? s1 : (uint64_t)B.limit + 1u;
-    }
+    for (uint32_t k = 0; k < kSeqK; ++k) sl += clampsl(lm[k].x, lm[k].y);
     uint64_t stot;
-    uint64_t opre = wg_excl_add<uint64_t, 16>(sl, shs, stot);
+    uint64_t opre = wg_excl_add<uint64_t, kSeqT / 64>(sl, shs, stot);
     const uint64_t tb0 = A.tokbase[B.chunk0];
     const uint64_t ob0 = A.outbase[B.chunk0];
     const uint64_t gbase = A.tokbase[c];
     const uint32_t brank0 = (uint32_t)(gbase - tb0);
     uint64_t produced = A.outbase[c] - ob0 + opre;
     uint32_t bad = 0xFFFFFFFFu;
+    uint4 rv[kSeqK];
 #pragma unroll
-    for (uint32_t i = 0; i < 3; ++i) {
-        if (i0 + i < ntc) {
-            const uint4 rec = A.trec[(size_t)c * kTokSlot + i0 + i];  // (second read: L2)
-            LbTok S;
-            S.lit = rec.x & 0x7FFFFFFFu; S.ll = rec.y; S.ml = rec.z; S.off = rec.w;
-            const bool last = (rec.x >> 31) != 0;
-            const uint32_t rank = i0 + i;
-            const uint32_t st = lb_check(produced, S.ll, S.ml, S.off, last, B.limit, B.cap);
-            const uint32_t br = brank0 + rank;
-            if (st != S3HC_OK && bad == 0xFFFFFFFFu) bad = (br << 3) | st;
-            A.seq4[gbase + rank] = make_uint4(produced < 0xFFFFFFFFull ? (uint32_t)produced : 0xFFFFFFFFu, S.lit,
-                                              S.ll, S.ml);
-            A.seqoff[gbase + rank] = (uint16_t)S.off;
-            // execution steps whose first byte this sequence produces
-            const uint64_t sl1 = (uint64_t)S.ll + S.ml;
-            if (st == S3HC_OK && sl1) {
-                const uint64_t r_lo = (produced + kLbStep - 1) / kLbStep, r_hi = (produced + sl1 - 1) / kLbStep;
-                for (uint64_t q = r_lo; q <= r_hi && q < kLbMaxSteps; ++q) A.rfirst[(size_t)bi * kLbMaxSteps + q] = br;
-            }
-            produced += sl1 < (uint64_t)B.limit + 1u ? sl1 : (uint64_t)B.limit + 1u;
+    for (uint32_t k = 0; k < kSeqK; ++k) rv[k] = k < nk ? tr[k] : make_uint4(0, 0, 0, 0);  // (second read: L2)
+#pragma unroll
+    for (uint32_t k = 0; k < kSeqK; ++k) {
+        if (k >= nk) continue;
+        const uint4 rec = rv[k];
+        LbTok S;
+        S.lit = rec.x & 0x7FFFFFFFu; S.ll = rec.y; S.ml = rec.z; S.off = rec.w;
+        const bool last = (rec.x >> 31) != 0;
+        const uint32_t rank = i0 + k;
+        const uint32_t st = lb_check(produced, S.ll, S.ml, S.off, last, B.limit, B.cap);
+        const uint32_t br = brank0 + rank;
+        if (st != S3HC_OK && bad == 0xFFFFFFFFu) bad = (br << 3) | st;
+        A.seq4[gbase + rank] = make_uint4(produced < 0xFFFFFFFFull ? (uint32_t)produced : 0xFFFFFFFFu, S.lit,
+                                          S.ll, S.ml);
+        A.seqoff[gbase + rank] = (uint16_t)S.off;
+        // execution steps whose first byte this sequence produces
+        const uint64_t sl1 = (uint64_t)S.ll + S.ml;
+        if (st == S3HC_OK && sl1) {
+            const uint64_t r_lo = (produced + kLbStep - 1) / kLbStep, r_hi = (produced + sl1 - 1) / kLbStep;
+            for (uint64_t q = r_lo; q <= r_hi && q < kLbMaxSteps; ++q) A.rfirst[(size_t)bi * kLbMaxSteps + q] = br;
         }
+        produced += clampsl(S.ll, S.ml);
     }
     if (bad != 0xFFFFFFFFu) atomicMin(&A.lb_err[bi], bad);
     if (threadIdx.x == 0) {
@@ -1366,12 +1747,18 @@ hipError_t launch_lb_parse(const LbArgs& A, const uint8_t* src, const DecBlock* 
                            hipStream_t st) {
     hipLaunchKernelGGL(k_lb_classify, dim3(1), dim3(1024), 0, st, blk, units, nunits, ucount, A);
     hipLaunchKernelGGL(k_lb_gran, dim3(A.chunk_cap), dim3(lb::kGpc), 0, st, src, A);
+#if S3HC_LB_TOKV2
+    hipLaunchKernelGGL(k_lbt_walk, dim3(A.chunk_cap), dim3(lb::kWT), 0, st, src, A);
+    hipLaunchKernelGGL(k_lbt_entry, dim3(cdiv_lb(A.lb_cap, 64)), dim3(64), 0, st, src, A);
+    hipLaunchKernelGGL(k_lbt_mark, dim3(A.chunk_cap), dim3(lb::kWT), 0, st, src, A);
+#else
     hipLaunchKernelGGL(k_lb_exit, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
     hipLaunchKernelGGL(k_lb_entry, dim3(cdiv_lb(A.lb_cap, 64)), dim3(64), 0, st, A);
     hipLaunchKernelGGL(k_lb_mark, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
+#endif
     hipError_t e = launch_scan2(A.ntok, A.slsum, A.chunk_cap, A.tokbase, A.outbase, A.total, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_lb_seq, dim3(A.chunk_cap), dim3(lb::kT), 0, st, src, A);
+    hipLaunchKernelGGL(k_lb_seq, dim3(A.chunk_cap), dim3(lb::kSeqT), 0, st, src, A);
     if (!A.wcap)  // (with the spread execution, k_lbw_plan does it)
         hipLaunchKernelGGL(k_lb_fin, dim3(cdiv_lb(A.lb_cap, 256)), dim3(256), 0, st, A, blk_out, blk_status);
     return hipGetLastError();
@@ -1399,9 +1786,9 @@ hipError_t launch_lb_exec(const LbArgs& A, const uint8_t* src, uint8_t* dst, uin
 #ifdef S3HC_LBPROF
 extern "C" int s3hc_diag_lbprof(unsigned long long* out, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(s3hc::g_lbprof), sizeof(unsigned long long) * 20) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(s3hc::g_lbprof), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[20] = {0};
+        unsigned long long z[32] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(s3hc::g_lbprof), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

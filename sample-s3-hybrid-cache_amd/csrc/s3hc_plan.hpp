@@ -108,6 +108,20 @@ struct DecUnit {         // a run of blocks decoded in order by one wave
 #endif
 constexpr uint32_t kLbChunk = S3HC_LB_CHUNK;  // compressed positions per tokenizing workgroup
 constexpr uint32_t kLbTokSlot = kLbChunk / 3 + 2;  // tokens of one chunk, at most (nodes >= 3 apart)
+#ifndef S3HC_LB_TOKV2  // 1: chunk chains by speculative segment walks (round 6); 0: next token at every
+#define S3HC_LB_TOKV2 1  // position + pointer doubling (rounds 1-5; diagnostic builds, A/B)
+#endif
+#ifndef S3HC_LB_WALKT
+#define S3HC_LB_WALKT 256
+#endif
+constexpr uint32_t kLbWalkT = S3HC_LB_WALKT;  // segment walks (threads) per chunk (S3HC_LB_TOKV2)
+#ifndef S3HC_LB_WALKLEAD
+#define S3HC_LB_WALKLEAD 1
+#endif
+constexpr uint32_t kLbWalkLead = S3HC_LB_WALKLEAD;  // segments a walk starts before its own (unmarked)
+constexpr uint32_t kLbFirstX = 64;        // chunk-relative positions whose chain exit is tabulated
+constexpr uint32_t kLbEPerChunk = S3HC_LB_TOKV2 ? kLbFirstX : kLbChunk;        // E entries per chunk
+constexpr uint32_t kLbJ0PerChunk = S3HC_LB_TOKV2 ? 2 * (kLbChunk / 32 + 3 * kLbWalkT) : kLbChunk;  // J0 (u16) per chunk
 constexpr uint32_t kLbStep = 7680;        // output bytes per step of the executing workgroup
 constexpr uint32_t kLbMaxSteps = 547;     // steps of one block (ceil(4 MiB / kLbStep))
 constexpr uint32_t kLbMinLimit = 65537;   // frame max block size above 64 KiB selects the path
@@ -160,8 +174,10 @@ struct LbArgs {
     uint8_t* unit_lb;      // per unit: 1 = decoded by this path
     uint32_t* chunk_blk;   // chunk -> LB block
     uint32_t* nzg;         // per chunk, per 64-byte granule: first non-255 byte at or after it (chunk-local)
-    uint32_t* E;           // per compressed position: chain exit of its chunk
-    uint16_t* J0;          // per compressed position: next token inside its chunk (chunk-relative; itself if none)
+    uint32_t* E;           // per chunk x kLbEPerChunk: chain exit of a chunk-relative position (walks: the
+                           // first kLbFirstX positions; doubling tables: every position)
+    uint16_t* J0;          // per chunk x kLbJ0PerChunk: walks: the walk-1 marks and segment exits (u32);
+                           // doubling tables: next token inside the chunk per position
     uint32_t* entry;       // per chunk: first chain position (chunk-relative) or ~0
     uint4* trec;           // per chunk, kLbTokSlot slots: its tokens in order (lit | last << 31, ll, ml, off)
     uint32_t* ntok;        // per chunk: sequences

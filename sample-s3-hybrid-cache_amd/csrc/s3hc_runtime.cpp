@@ -451,7 +451,7 @@ struct LbScratch {
         hipError_t e = hipSuccess;
 #define LBE(buf, bytes) if ((e = (buf).ensure((size_t)(bytes) + 64)) != hipSuccess) return e;
         LBE(lbt, nlb * sizeof(LbBlock)) LBE(ctl, sizeof(LbCtl)) LBE(unit_lb, nunits) LBE(chunk_blk, nch * 4)
-        LBE(nzg, nch * (kLbChunk / 64) * 4) LBE(E, nch * kLbChunk * 4) LBE(J0, nch * kLbChunk * 2) LBE(entry, nch * 4)
+        LBE(nzg, nch * (kLbChunk / 64) * 4) LBE(E, nch * kLbEPerChunk * 4) LBE(J0, nch * kLbJ0PerChunk * 2) LBE(entry, nch * 4)
         LBE(trec, nch * kLbTokSlot * 16) LBE(ntok, nch * 4) LBE(slsum, nch * 4) LBE(badrel, nch * 4)
         LBE(tokbase, nch * 8) LBE(outbase, nch * 8) LBE(total, 32) LBE(seq4, nseq * 16) LBE(seqoff, nseq * 2)
         LBE(lb_err, nlb * 4) LBE(lb_size, nlb * 4) LBE(lb_stat, nlb * 4) LBE(lb_tok0, nlb * 4) LBE(lb_ntok, nlb * 4)

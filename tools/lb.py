@@ -72,7 +72,7 @@ def main():
         print(json.dumps(case(eng, data, MiB, reps=2)))
         if hasattr(S.lib, "s3hc_diag_lbprof"):  # diagnostic build: k_lb_run phase times per step
             import ctypes
-            buf = (ctypes.c_ulonglong * 20)()
+            buf = (ctypes.c_ulonglong * 32)()
             S.lib.s3hc_diag_lbprof(buf, 1)
             v = list(buf)
             steps = max(v[7], 1)
@@ -81,6 +81,11 @@ def main():
             print(json.dumps({nm: (round(v[k] / steps, 1) if k not in (7,) else v[k]) for k, nm in enumerate(names)}))
             # k_lb_mark phases (cycles summed over chunks): load/stage, sub-range jumps, walks, tokenize, scans
             print(json.dumps({"mark_phases_Mcycles": [round(x / 1e6, 2) for x in v[12:17]]}))
+            ch = max(v[24], 1)  # segment-walk tokenizer (S3HC_LB_TOKV2): per-chunk phase cycles and hop maxima
+            print(json.dumps({"walk_phases_per_chunk": [round(x / ch) for x in v[12:16]],
+                              "mark_phases_per_chunk": [round(x / ch) for x in v[16:20]],
+                              "max_hops_per_chunk_w2_first_entry_remark": [round(x / ch, 1) for x in v[20:24]],
+                              "chunks": v[24]}))
         return
     for n in (1, 4, 16, 64, 256):
         out[f"log_1MiB_x{n}"] = case(eng, text[:n * MiB], MiB)
