@@ -140,7 +140,8 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
 // Owner scan of a step (k_lb_run, k_lbw_init): thread t holds the 16-bit start marks of bytes
 // 8t .. 8t+7 (0 = no sequence starts there); each byte's owner is the running max of the marks
 // up to it. Every thread of the workgroup calls (one barrier); shm: 16 aligned words.
-__device__ __forceinline__ uint4 lb_owners(const uint4 m4, uint32_t* shm) {
+template <typename Bar>
+__device__ __forceinline__ uint4 lb_owners_b(const uint4 m4, uint32_t* shm, Bar bar) {
     const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
     uint32_t mx = 0;
 #pragma unroll
@@ -148,7 +149,7 @@ __device__ __forceinline__ uint4 lb_owners(const uint4 m4, uint32_t* shm) {
     const uint32_t inc = wave_incl_max(mx);
     const uint32_t w = threadIdx.x >> 6;
     if ((threadIdx.x & 63u) == 63u) shm[w] = inc;
-    __syncthreads();
+    bar();
     uint32_t cur = lb_dpp<0x138, 0xF>(inc);  // wave_shr:1: the max before this lane (lane 0: 0)
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {  // and before this wave
@@ -168,6 +169,25 @@ __device__ __forceinline__ uint4 lb_owners(const uint4 m4, uint32_t* shm) {
         ow[k] = o0 | (cur << 16);
     }
     return make_uint4(ow[0], ow[1], ow[2], ow[3]);
+}
+__device__ __forceinline__ uint4 lb_owners(const uint4 m4, uint32_t* shm) {
+    return lb_owners_b(m4, shm, [] { __syncthreads(); });
+}
+
+// Barrier of k_lb_run's decoding waves only (S3HC_LB_XBAR): an LDS arrival counter; the hashing
+// wave of the workgroup never waits on it (s_barrier counts every wave of the workgroup). A
+// wave's LDS operations complete in order; the fences keep the compiler's order. (The spin is
+// bounded so that a wrong count cannot hang the GPU: it ends the wait, and the results would be
+// wrong, not the machine.)
+__device__ __forceinline__ void lb_xbar(uint32_t* ctr, uint32_t& tgt, uint32_t nw) {
+    tgt += nw;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63u) == 0u) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (uint32_t n = 0; n < (1u << 26); ++n)
+            if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= tgt) break;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // Workgroup exclusive sum (every thread calls; sh holds one entry per wave).
@@ -1022,10 +1042,9 @@ __device__ __forceinline__ uint32_t lb_check(uint64_t produced, uint32_t ll, uin
     return st;
 }
 
-// 256 threads per chunk, thread t taking the contiguous ranks [t K, t K + K), K = ceil(ntok / 256)
-// <= kSeqK, every record load of a pass in flight at once (round 6: the 1024-thread form with three
-// records per thread held two workgroups per CU, so a launch of 13,824 chunks ran in 27
-// latency-bound rounds: 165 us at 256 reference frames)
+// 256 threads per chunk: the records are read and the table written rank-strided (rank t + 256 k:
+// coalesced), the output offsets scanned over contiguous ranks through LDS (round 6: the
+// 1024-thread form read and wrote three consecutive records per thread)
 namespace lb {
 constexpr uint32_t kSeqT = 256;
 constexpr uint32_t kSeqK = (kTokSlot + kSeqT - 1u) / kSeqT;
@@ -1033,44 +1052,60 @@ constexpr uint32_t kSeqK = (kTokSlot + kSeqT - 1u) / kSeqT;
 __global__ __launch_bounds__(lb::kSeqT) void k_lb_seq(const uint8_t* __restrict__ src, LbArgs A) {
     using namespace lb;
     __shared__ uint64_t shs[kSeqT / 64];
+    __shared__ uint64_t opos[kSeqK * kSeqT];  // per rank: clamped output bytes, then output offset
     const uint32_t c = blockIdx.x;
     if (c >= A.ctl->nchunks || A.entry[c] == NONE) return;
     const uint32_t bi = A.chunk_blk[c];
     const LbBlock B = A.lbt[bi];
     const uint32_t cs = (c - B.chunk0) * kLbChunk;
     const uint32_t ntc = A.ntok[c];
-    const uint32_t K = (ntc + kSeqT - 1u) / kSeqT;
-    const uint32_t i0 = umin32_lb(ntc, K * threadIdx.x), nk = umin32_lb(ntc, i0 + K) - i0;
-    const uint4* tr = A.trec + (size_t)c * kTokSlot + i0;
-    auto clampsl = [&](uint32_t ll, uint32_t ml) -> uint32_t {
+    const uint32_t t = threadIdx.x;
+    const uint4* tr = A.trec + (size_t)c * kTokSlot;
+    auto clampsl = [&](uint32_t ll, uint32_t ml) -> uint64_t {
         const uint64_t s1 = (uint64_t)ll + ml;
-        return s1 < (uint64_t)B.limit + 1u ? (uint32_t)s1 : B.limit + 1u;
+        return s1 < (uint64_t)B.limit + 1u ? s1 : (uint64_t)B.limit + 1u;
     };
-    uint2 lm[kSeqK];
+    uint4 rv[kSeqK];
 #pragma unroll
-    for (uint32_t k = 0; k < kSeqK; ++k) lm[k] = k < nk ? *(const uint2*)((const uint32_t*)&tr[k] + 1) : make_uint2(0, 0);
+    for (uint32_t k = 0; k < kSeqK; ++k) {
+        const uint32_t i = t + kSeqT * k;
+        rv[k] = i < ntc ? tr[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kSeqK; ++k) {
+        const uint32_t i = t + kSeqT * k;
+        if (i < ntc) opos[i] = clampsl(rv[k].y, rv[k].z);
+    }
+    __syncthreads();
+    const uint32_t K = (ntc + kSeqT - 1u) / kSeqT;
+    const uint32_t i0 = umin32_lb(ntc, K * t), i1 = umin32_lb(ntc, i0 + K);
     uint64_t sl = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kSeqK; ++k) sl += clampsl(lm[k].x, lm[k].y);
+    for (uint32_t i = i0; i < i1; ++i) sl += opos[i];
     uint64_t stot;
-    uint64_t opre = wg_excl_add<uint64_t, kSeqT / 64>(sl, shs, stot);
+    const uint64_t opre = wg_excl_add<uint64_t, kSeqT / 64>(sl, shs, stot);
     const uint64_t tb0 = A.tokbase[B.chunk0];
     const uint64_t ob0 = A.outbase[B.chunk0];
     const uint64_t gbase = A.tokbase[c];
     const uint32_t brank0 = (uint32_t)(gbase - tb0);
-    uint64_t produced = A.outbase[c] - ob0 + opre;
+    {
+        uint64_t produced = A.outbase[c] - ob0 + opre;
+        for (uint32_t i = i0; i < i1; ++i) {
+            const uint64_t v = opos[i];
+            opos[i] = produced;
+            produced += v;
+        }
+    }
+    __syncthreads();
     uint32_t bad = 0xFFFFFFFFu;
-    uint4 rv[kSeqK];
-#pragma unroll
-    for (uint32_t k = 0; k < kSeqK; ++k) rv[k] = k < nk ? tr[k] : make_uint4(0, 0, 0, 0);  // (second read: L2)
 #pragma unroll
     for (uint32_t k = 0; k < kSeqK; ++k) {
-        if (k >= nk) continue;
+        const uint32_t rank = t + kSeqT * k;
+        if (rank >= ntc) continue;
+        const uint64_t produced = opos[rank];
         const uint4 rec = rv[k];
         LbTok S;
         S.lit = rec.x & 0x7FFFFFFFu; S.ll = rec.y; S.ml = rec.z; S.off = rec.w;
         const bool last = (rec.x >> 31) != 0;
-        const uint32_t rank = i0 + k;
         const uint32_t st = lb_check(produced, S.ll, S.ml, S.off, last, B.limit, B.cap);
         const uint32_t br = brank0 + rank;
         if (st != S3HC_OK && bad == 0xFFFFFFFFu) bad = (br << 3) | st;
@@ -1083,7 +1118,6 @@ __global__ __launch_bounds__(lb::kSeqT) void k_lb_seq(const uint8_t* __restrict_
             const uint64_t r_lo = (produced + kLbStep - 1) / kLbStep, r_hi = (produced + sl1 - 1) / kLbStep;
             for (uint64_t q = r_lo; q <= r_hi && q < kLbMaxSteps; ++q) A.rfirst[(size_t)bi * kLbMaxSteps + q] = br;
         }
-        produced += clampsl(S.ll, S.ml);
     }
     if (bad != 0xFFFFFFFFu) atomicMin(&A.lb_err[bi], bad);
     if (threadIdx.x == 0) {
@@ -1166,6 +1200,9 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
     __shared__ uint32_t rf[kLbMaxSteps + 1];
     __shared__ __attribute__((aligned(16))) uint32_t shm[16];
     __shared__ uint32_t jflag[3];
+    __shared__ uint32_t xb_ctr;    // S3HC_LB_XBAR: arrivals at the decoding waves' barriers
+    __shared__ uint32_t x_final;   // bytes of the block final in the ring (whole steps), for the hashing wave
+    __shared__ uint32_t x_hashed;  // stripes the hashing wave has hashed (ring slots it no longer reads)
     const uint32_t i = blockIdx.x;
     if (i >= A.ctl->nlb || A.lb_stat[i] != S3HC_OK) return;
     if (A.wcap && A.wbase[i] != lb::NONE) return;  // spread execution decodes it (k_lbw_*)
@@ -1198,8 +1235,8 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
     // hash stripes [hs, min(avail / 16, hs + budget)) of the finished output, read from the LDS
     // ring (aligned dwords: ring slots are output positions mod 64 KiB; the hashing wave lags the
     // decode by about one step, far less than the ring's 8)
-#ifdef S3HC_LB_NOHASH  // diagnostic builds: no hashing wave work (k_dframe_close hashes)
-#define LB_HASH(avail, budget)
+#if defined(S3HC_LB_NOHASH) || S3HC_LB_XBAR  // (S3HC_LB_NOHASH diagnostic builds: k_dframe_close hashes;
+#define LB_HASH(avail, budget)                   // S3HC_LB_XBAR: the hashing wave runs its own loop)
 #else
 #define LB_HASH(avail, budget)                                                                  \
     if (!dec) {                                                                                 \
@@ -1221,6 +1258,11 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
     // step q covers sequences [rf[q], rf[q+1]) (+1 when the next step starts inside one)
     for (uint32_t q = t; q <= nsteps; q += kXWG)
         rf[q] = q < nsteps ? A.rfirst[(size_t)i * kLbMaxSteps + q] : ntok;
+    if (t == 0) {
+        xb_ctr = 0;
+        x_final = 0;
+        x_hashed = 0;
+    }
     __syncthreads();
     // sequences of a step: loaded into registers one step ahead, stored (with the start marks)
     // into LDS once the current step no longer needs them (kMaxSeqS <= 3 x kXT)
@@ -1261,6 +1303,66 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
     LB_INSTALL(0)
     if (1 < nsteps) LB_PREFETCH(1)
     __syncthreads();
+#if S3HC_LB_XBAR
+    // From here the decoding waves synchronise among themselves (lb_xbar) and the hashing wave
+    // runs free: it hashes every whole step the decoders publish (x_final), from the ring, and
+    // publishes its progress (x_hashed); the decoders wait for it only before overwriting ring
+    // slots it has not read (it trails by about a step; the ring holds eight). In rounds 2-5 it
+    // took part in every barrier of the step loop with slices sized to the phases, and the phases
+    // it overran cost 0.28 of k_lb_run's 1.6 ms at 256 reference frames.
+    uint32_t xtgt = 0;
+    constexpr uint32_t kXW = kXT / 64u;
+#define LB_SYNC() lb_xbar(&xb_ctr, xtgt, kXW)
+    if (!dec) {
+#ifndef S3HC_LB_NOHASH
+        for (uint32_t n = 0; hs < hns && n < (1u << 26);) {
+            uint32_t lim = __hip_atomic_load(&x_final, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> 4;
+            lim = lim < hns ? lim : hns;
+            if (lim <= hs) {
+                __builtin_amdgcn_s_sleep(1);
+                ++n;
+                continue;
+            }
+            for (; hs + 16u <= lim; hs += 16u) {
+                // lane 4k + a loads stripe k's dword a and multiplies it by P2 (off the chain)
+                const uint32_t mv = *(const uint32_t*)(ring + ((16u * hs + 4u * (uint32_t)lane) & kMask)) * XH2;
+                uint32_t m[16];
+#pragma unroll
+                for (uint32_t k = 0; k < 16; ++k) m[k] = __shfl(mv, (int)(4u * k + ha));
+#pragma unroll
+                for (uint32_t k = 0; k < 16; ++k) hacc = xh_rotl(hacc + m[k], 13) * XH1;
+            }
+            for (; hs < lim; ++hs) hacc = xh_round(hacc, *(const uint32_t*)(ring + ((16u * hs + 4u * ha) & kMask)));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&x_hashed, hs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        // every step is final: the tail (from the ring) and the avalanche
+        for (uint32_t n = 0; n < (1u << 26) && __hip_atomic_load(&x_final, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < size; ++n)
+            __builtin_amdgcn_s_sleep(1);
+        const int qb = lane & ~3;
+        const uint32_t v1 = __shfl(hacc, qb), v2 = __shfl(hacc, qb + 1), v3 = __shfl(hacc, qb + 2),
+                       v4 = __shfl(hacc, qb + 3);
+        if (lane == 0) {
+            uint32_t h = size >= 16 ? xh_rotl(v1, 1) + xh_rotl(v2, 7) + xh_rotl(v3, 12) + xh_rotl(v4, 18) : XH5;
+            h += size;
+            uint32_t p = hns * 16u;
+            auto rb = [&](uint32_t x) -> uint32_t { return ring[x & kMask]; };
+            for (; p + 4u <= size; p += 4u)
+                h = xh_rotl(h + (rb(p) | rb(p + 1) << 8 | rb(p + 2) << 16 | rb(p + 3) << 24) * XH3, 17) * XH4;
+            for (; p < size; ++p) h = xh_rotl(h + rb(p) * XH5, 11) * XH1;
+            h ^= h >> 15;
+            h *= XH2;
+            h ^= h >> 13;
+            h *= XH3;
+            h ^= h >> 16;
+            A.blk_hash[B.blk] = (1ull << 32) | h;
+        }
+#endif
+        return;
+    }
+#else
+#define LB_SYNC() __syncthreads()
+#endif
     for (uint32_t q = 0; q < nsteps; ++q) {
         const uint32_t R = q * kLbStep;
         LB_T(0);
@@ -1268,9 +1370,9 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         // owner of each byte: running max of the start marks (thread t: bytes 8t .. 8t+7)
         // (owners written over the marks, then read with the interleaved byte mapping; the
         // hashing wave's marks are zero)
-        const uint4 own = lb_owners(dec ? ((const uint4*)marks)[t] : make_uint4(0, 0, 0, 0), shm);
+        const uint4 own = lb_owners_b(dec ? ((const uint4*)marks)[t] : make_uint4(0, 0, 0, 0), shm, [&] { LB_SYNC(); });
         if (dec) ((uint4*)marks)[t] = own;
-        __syncthreads();
+        LB_SYNC();
         // (a hashing wave more than 3 steps behind catches up here: the ring keeps 8)
         LB_HASH(R, R - 16u * hs > 3u * kLbStep ? (R - 16u * hs - 2u * kLbStep) / 16u
                                                 : (R - 16u * hs > kHashLag ? kHashClassify : 0u))
@@ -1317,7 +1419,15 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
 #pragma unroll
         for (uint32_t j = 0; j < kXPer; ++j) vb[j] = (litm >> j) & 1u ? lv[j] & 0xFFu : vb[j];
         LB_T(2);
-        __syncthreads();  // every read of the ring slots this step overwrites, and of marks/sq, is done
+#if S3HC_LB_XBAR
+        // the ring slots this step overwrites ([R + kLbStep - kRing, R)'s) were hashed
+        if (t == 0 && R + kLbStep > kRing)
+            for (uint32_t n = 0; n < (1u << 26) &&
+                                 16u * __hip_atomic_load(&x_hashed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + kRing < R + kLbStep;
+                 ++n)
+                __builtin_amdgcn_s_sleep(1);
+#endif
+        LB_SYNC();  // every read of the ring slots this step overwrites, and of marks/sq, is done
         if (dec) {
 #pragma unroll
             for (uint32_t j = 0; j < kXPer; ++j) {
@@ -1329,7 +1439,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         }
         if (t == 0) jflag[0] = 0u;
         LB_HASH(R, kHashStores)
-        __syncthreads();
+        LB_SYNC();
         LB_T(3);
         if (q + 1 < nsteps) LB_INSTALL(q + 1)
         if (q + 2 < nsteps) LB_PREFETCH(q + 2)
@@ -1375,11 +1485,16 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
 #ifdef S3HC_LBPROF
             lbp[11] += __builtin_amdgcn_s_memtime() - tb1;
 #endif
-            __syncthreads();
+            LB_SYNC();
             LB_ADD(8, 1);
             if (!jflag[it % 3u]) break;
         }
         LB_T(5);
+#if S3HC_LB_XBAR
+        // every byte of the step is final in the ring (the rounds' last barrier): publish it
+        if (t == 0)
+            __hip_atomic_store(&x_final, R + kLbStep < size ? R + kLbStep : size, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
         // flush the step (thread t: dwords t and t + kXT of the step)
         if (dec) {
             const bool al = (((uintptr_t)(ob + R)) & 3u) == 0;
@@ -1398,6 +1513,8 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         }
         LB_T(6);
     }
+#undef LB_SYNC
+#if !S3HC_LB_XBAR
     // every step is flushed: the hashing wave finishes the stripes, the tail and the avalanche
     __syncthreads();
     LB_HASH(size, hns)
@@ -1421,6 +1538,7 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         }
     }
 #endif
+#endif  // !S3HC_LB_XBAR
 #ifdef S3HC_LBPROF
     if (t == 0)
         for (int k = 0; k < 12; ++k) atomicAdd(&g_lbprof[k], (unsigned long long)lbp[k]);

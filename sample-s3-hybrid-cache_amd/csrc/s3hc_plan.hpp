@@ -123,6 +123,9 @@ constexpr uint32_t kLbFirstX = 64;        // chunk-relative positions whose chai
 constexpr uint32_t kLbEPerChunk = S3HC_LB_TOKV2 ? kLbFirstX : kLbChunk;        // E entries per chunk
 constexpr uint32_t kLbJ0PerChunk = S3HC_LB_TOKV2 ? 2 * (kLbChunk / 32 + 3 * kLbWalkT) : kLbChunk;  // J0 (u16) per chunk
 constexpr uint32_t kLbStep = 7680;        // output bytes per step of the executing workgroup
+#ifndef S3HC_LB_XBAR  // 1: k_lb_run's decoding waves synchronise by an LDS counter and its hashing wave
+#define S3HC_LB_XBAR 1  // runs free (round 6); 0: every wave at every s_barrier (rounds 2-5; diag A/B)
+#endif
 constexpr uint32_t kLbMaxSteps = 547;     // steps of one block (ceil(4 MiB / kLbStep))
 constexpr uint32_t kLbMinLimit = 65537;   // frame max block size above 64 KiB selects the path
 constexpr uint32_t kLbFewBlocks = 256;    // batches with at most this many blocks: every compressed
