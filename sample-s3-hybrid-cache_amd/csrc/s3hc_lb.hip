@@ -12,13 +12,14 @@
 //                  kLbChunk compressed positions per block.
 //   k_lb_gran      per chunk: first non-255 byte at or after each 64-byte granule (length
 //                  extension runs are 255-runs; this makes every run length O(64) to find).
-//   k_lb_exit      per chunk: the next-token position of a token assumed at EVERY position
-//                  (lz4_flex parse rules, exact for long runs), then pointer doubling in LDS:
-//                  each position learns where its token chain leaves the chunk.
-//   k_lb_entry     per block, serial over chunks: the true chain's entry into each chunk.
-//   k_lb_mark      per chunk: marks the nodes reachable from the entry (= the block's real
-//                  tokens) by sub-range exits, parses them one per thread and writes their
-//                  records; per-chunk sequence count and output bytes.
+//   k_lbt_walk     per chunk: speculative token walks from every 32-position segment, merged
+//                  where they meet; each segment's chain exit (doubling over segments) and the
+//                  exits of the chunk's first 64 positions.
+//   k_lbt_entry    per block, serial over chunks: the true chain's entry into each chunk.
+//   k_lbt_mark     per chunk: the true chain from the entry through the walks' marks (= the
+//                  block's real tokens), parsed one per thread into records; per-chunk sequence
+//                  count and output bytes. (k_lb_exit / k_lb_entry / k_lb_mark: the rounds 1-5
+//                  tokenizer by next-token tables and pointer doubling, S3HC_LB_TOKV2=0 builds.)
 //   (scans)        global sequence index and output offset of each chunk.
 //   k_lb_seq       per chunk: the sequence table (out, literal, ll, ml, offset) from the records
 //                  and the lz4_flex bound checks in stream order (first failing sequence decides).
@@ -27,7 +28,8 @@
 //                  output in 7.5 KiB steps: in each step every byte gets its value (literal, or a
 //                  match source before the step: 64 KiB LDS ring of recent output) or a pointer
 //                  to its source inside the step (overlapping copies folded into the first
-//                  period), and the pointers are jumped in LDS until every byte is final.
+//                  period), and the pointers are jumped in LDS until every byte is final; its
+//                  16th wave hashes the finished steps beside the 15 decoding waves' LDS barrier.
 //   k_lbw_*        (launches of few large blocks) spread execution: every 7.5 KiB tile of every
 //                  block at once, chains across tiles resolved by global pointer jumping.
 //

@@ -96,8 +96,8 @@ struct DecUnit {         // a run of blocks decoded in order by one wave
 // ---- large-block decode ---------------------------------
 // Blocks whose frame allows more than 64 KiB (BD 0x50 / 0x70: what lz4_flex writes for the
 // reference's ~1 MiB cache batches) are decoded by a whole workgroup each instead of one wave:
-// the token chain is found by pointer doubling over 16 Ki-position chunks of the compressed
-// block (all chunks of all blocks in parallel), the sequence table comes from scans, and one
+// the token chain is found by speculative segment walks over 8 Ki-position chunks of the
+// compressed block (all chunks of all blocks in parallel), the sequence table comes from scans, and one
 // 1024-thread workgroup per block then writes the output in 7.5 KiB steps (15 waves, 8 bytes per
 // lane), resolving each step's match chains in LDS by pointer jumping against a 64 KiB ring of
 // recent output, while its 16th wave hashes the flushed output (the frame's content xxh32 when
