@@ -58,6 +58,10 @@ INPUTS = {
     "runs_2MiB": lambda: _runs(2 * MiB, 6),
     "deep_1MiB": lambda: _deep_chain(MiB, 7),
     "half_random_1MiB": lambda: synth.log_text(MiB // 2, 8) + _rnd(MiB // 2, 9),
+    # text with 3 KiB random stretches: literal runs of ~3 KiB start and end all over the block, so
+    # chains enter many 8 KiB tokenizing chunks past the first 64 positions (k_lbt_entry's walk
+    # over the stored marks instead of the exit table)
+    "mixed_1MiB": lambda: b"".join(synth.log_text(4096, 20 + k) + _rnd(3072, 40 + k) for k in range(150))[:MiB],
     "random_300k": lambda: _rnd(300_000, 10),            # stored block: not on this path
 }
 _CACHE = {}
