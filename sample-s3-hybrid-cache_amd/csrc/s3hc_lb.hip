@@ -175,6 +175,41 @@ __device__ __forceinline__ uint4 lb_owners_b(const uint4 m4, uint32_t* shm, Bar 
 __device__ __forceinline__ uint4 lb_owners(const uint4 m4, uint32_t* shm) {
     return lb_owners_b(m4, shm, [] { __syncthreads(); });
 }
+// The same scan in two halves with a barrier between them supplied by the caller (k_lb_run runs
+// them inside the previous step's jumping rounds): lb_own1 publishes the wave's maximum and
+// returns it (inclusive, per lane), lb_own2 gives the owners.
+__device__ __forceinline__ uint32_t lb_own1(const uint4 m4, uint32_t* shm) {
+    const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
+    uint32_t mx = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) mx = lb_umax(mx, lb_umax(mw[k] & 0xFFFFu, mw[k] >> 16));
+    const uint32_t inc = wave_incl_max(mx);
+    if ((threadIdx.x & 63u) == 63u) shm[threadIdx.x >> 6] = inc;
+    return inc;
+}
+__device__ __forceinline__ uint4 lb_own2(const uint4 m4, uint32_t inc, const uint32_t* shm) {
+    const uint32_t mw[4] = {m4.x, m4.y, m4.z, m4.w};
+    const uint32_t w = threadIdx.x >> 6;
+    uint32_t cur = lb_dpp<0x138, 0xF>(inc);  // wave_shr:1: the max before this lane (lane 0: 0)
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {  // and before this wave
+        const uint4 v = ((const uint4*)shm)[k];
+        cur = lb_umax(cur, 4u * k < w ? v.x : 0u);
+        cur = lb_umax(cur, 4u * k + 1u < w ? v.y : 0u);
+        cur = lb_umax(cur, 4u * k + 2u < w ? v.z : 0u);
+        cur = lb_umax(cur, 4u * k + 3u < w ? v.w : 0u);
+    }
+    uint32_t ow[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t lo = mw[k] & 0xFFFFu, hi = mw[k] >> 16;
+        cur = lb_umax(cur, lo);
+        const uint32_t o0 = cur;
+        cur = lb_umax(cur, hi);
+        ow[k] = o0 | (cur << 16);
+    }
+    return make_uint4(ow[0], ow[1], ow[2], ow[3]);
+}
 
 // Barrier of k_lb_run's decoding waves only (S3HC_LB_XBAR): an LDS arrival counter; the hashing
 // wave of the workgroup never waits on it (s_barrier counts every wave of the workgroup). A
@@ -1365,6 +1400,11 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
 #else
 #define LB_SYNC() __syncthreads()
 #endif
+#if S3HC_LB_OWNFUSE
+    uint32_t os = 0, oinc = 0;  // the next step's owner scan: halves done; this lane's wave maximum
+    uint4 om4 = make_uint4(0, 0, 0, 0);
+    bool own_sync = false;
+#endif
     for (uint32_t q = 0; q < nsteps; ++q) {
         const uint32_t R = q * kLbStep;
         LB_T(0);
@@ -1372,9 +1412,23 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
         // owner of each byte: running max of the start marks (thread t: bytes 8t .. 8t+7)
         // (owners written over the marks, then read with the interleaved byte mapping; the
         // hashing wave's marks are zero)
+#if S3HC_LB_OWNFUSE
+        // (steps after the first: the previous step's jumping rounds ran the scan, os == 2;
+        // own_sync: its owners were stored after the rounds' last barrier)
+        if (q == 0) {
+            const uint4 own = lb_owners_b(dec ? ((const uint4*)marks)[t] : make_uint4(0, 0, 0, 0), shm, [&] { LB_SYNC(); });
+            if (dec) ((uint4*)marks)[t] = own;
+            LB_SYNC();
+        } else if (own_sync) {
+            LB_SYNC();
+        }
+        os = 0;
+        own_sync = false;
+#else
         const uint4 own = lb_owners_b(dec ? ((const uint4*)marks)[t] : make_uint4(0, 0, 0, 0), shm, [&] { LB_SYNC(); });
         if (dec) ((uint4*)marks)[t] = own;
         LB_SYNC();
+#endif
         // (a hashing wave more than 3 steps behind catches up here: the ring keeps 8)
         LB_HASH(R, R - 16u * hs > 3u * kLbStep ? (R - 16u * hs - 2u * kLbStep) / 16u
                                                 : (R - 16u * hs > kHashLag ? kHashClassify : 0u))
@@ -1461,6 +1515,20 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
 #ifdef S3HC_LBPROF
             const uint64_t tb1 = __builtin_amdgcn_s_memtime();
 #endif
+#if S3HC_LB_OWNFUSE
+            // the next step's owner scan, one half per round: its marks were installed before
+            // round 0's barrier, the wave maxima are read after a later one, and the owners'
+            // stores precede this round's barrier
+            if (q + 1 < nsteps && it >= 1 && os < 2) {
+                if (os == 0) {
+                    om4 = ((const uint4*)marks)[t];
+                    oinc = lb_own1(om4, shm);
+                } else {
+                    ((uint4*)marks)[t] = lb_own2(om4, oinc, shm);
+                }
+                ++os;
+            }
+#endif
             // up to kJumpHops hops per round between barriers: pointers other threads stored in
             // this round are read as soon as they land (LDS), which only shortens the chains
             // (a final entry is VALF | byte value: one gather gives both the state and the value)
@@ -1491,6 +1559,19 @@ __global__ __launch_bounds__(1024) void k_lb_run(const uint8_t* __restrict__ src
             LB_ADD(8, 1);
             if (!jflag[it % 3u]) break;
         }
+#if S3HC_LB_OWNFUSE
+        // the halves the rounds did not reach (fewer than three rounds)
+        if (q + 1 < nsteps && os < 2) {
+            if (os == 0) {
+                om4 = ((const uint4*)marks)[t];
+                oinc = lb_own1(om4, shm);
+                LB_SYNC();
+            }
+            ((uint4*)marks)[t] = lb_own2(om4, oinc, shm);
+            os = 2;
+            own_sync = true;
+        }
+#endif
         LB_T(5);
 #if S3HC_LB_XBAR
         // every byte of the step is final in the ring (the rounds' last barrier): publish it

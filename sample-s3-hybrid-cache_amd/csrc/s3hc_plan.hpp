@@ -126,6 +126,9 @@ constexpr uint32_t kLbStep = 7680;        // output bytes per step of the execut
 #ifndef S3HC_LB_XBAR  // 1: k_lb_run's decoding waves synchronise by an LDS counter and its hashing wave
 #define S3HC_LB_XBAR 1  // runs free (round 6); 0: every wave at every s_barrier (rounds 2-5; diag A/B)
 #endif
+#ifndef S3HC_LB_OWNFUSE  // 1: k_lb_run runs the next step's owner scan inside the jumping rounds (two
+#define S3HC_LB_OWNFUSE S3HC_LB_XBAR  // barriers fewer per step when there are >= 3 rounds)
+#endif
 constexpr uint32_t kLbMaxSteps = 547;     // steps of one block (ceil(4 MiB / kLbStep))
 constexpr uint32_t kLbMinLimit = 65537;   // frame max block size above 64 KiB selects the path
 constexpr uint32_t kLbFewBlocks = 256;    // batches with at most this many blocks: every compressed
